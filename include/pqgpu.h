@@ -1,0 +1,211 @@
+/*
+ * pqgpu.h — C ABI of the MI355X-native Parquet column-chunk decoder.
+ *
+ * This is the drop-in boundary for the read path of fraugster/parquet-go
+ * (v0.12.0 line). Each entry point names the reference interface it
+ * replaces (file:line under the reference tree). A Go `gpudecode` package
+ * binds these through cgo; the same symbols are bound
+ * from Python via ctypes for the parity tests and the benchmark.
+ *
+ * Conventions
+ *  - Plain C types only; no HIP or torch types in signatures. `stream` is a
+ *    hipStream_t passed as void* (NULL = the context's own stream).
+ *  - Every function returns a pqgpu status (PQ_OK = 0) and, where it takes
+ *    a pqgpu_error*, fills it with the error class, the failing chunk/page
+ *    and a message mirroring the reference's error text.
+ *  - Error classes mirror the Go error values the reference returns; the
+ *    numbering is shared with the CPU oracle (oracle/oracle.h).
+ *  - Thread safety: one pqgpu_ctx per GPU; a ctx and its batches are used
+ *    by one host thread at a time (the reference FileReader is not
+ *    goroutine-safe either, file_reader.go:18).
+ */
+#ifndef PQGPU_H
+#define PQGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQGPU_ABI_VERSION 1
+
+/* Error classes (Go error value the reference returns in the same case). */
+enum pqgpu_status {
+  PQ_OK = 0,
+  PQ_ERR_EOF = 1,            /* io.EOF */
+  PQ_ERR_UNEXPECTED_EOF = 2, /* io.ErrUnexpectedEOF */
+  PQ_ERR_INVALID = 3,        /* malformed data: errors.New / fmt.Errorf in the decoders */
+  PQ_ERR_UNSUPPORTED = 4,    /* unsupported type / encoding / codec */
+  PQ_ERR_DICT_INDEX = 5,     /* "dict: invalid index %d, values count are %d" type_dict.go:52-54 */
+  PQ_ERR_CRC = 6,            /* "CRC32 check failed" chunk_reader.go:173-177 */
+  PQ_ERR_DECOMPRESS = 7,     /* "decompression failed" / size mismatch compress.go:102-123 */
+  PQ_ERR_THRIFT = 8,         /* thrift decode error (readThrift helpers.go:103-109) */
+  PQ_ERR_RANGE = 9,          /* "int32 out of range" helpers.go:176 / varint overflow */
+  PQ_ERR_NOMEM = 10,         /* host or device allocation failure */
+  PQ_ERR_ARG = 11,           /* bad argument to this API */
+  PQ_ERR_HIP = 12,           /* HIP runtime error (no GPU, launch failure, ...) */
+};
+
+/* parquet.Type (parquet/parquet.go) */
+enum { PQ_BOOLEAN = 0, PQ_INT32 = 1, PQ_INT64 = 2, PQ_INT96 = 3, PQ_FLOAT = 4, PQ_DOUBLE = 5,
+       PQ_BYTE_ARRAY = 6, PQ_FIXED_LEN_BYTE_ARRAY = 7 };
+
+typedef struct {
+  int32_t code;     /* enum pqgpu_status */
+  int32_t chunk;    /* batch chunk id, -1 if not chunk specific */
+  int32_t page;     /* data-page index within the chunk, -1 for chunk-level errors */
+  char msg[244];
+} pqgpu_error;
+
+typedef struct pqgpu_ctx pqgpu_ctx;
+typedef struct pqgpu_file pqgpu_file;
+typedef struct pqgpu_batch pqgpu_batch;
+
+/* Leaf column schema: Column.maxD/maxR from readColumnSchema schema.go:893-924. */
+typedef struct {
+  int32_t physical_type;   /* parquet.Type */
+  int32_t type_length;     /* FIXED_LEN_BYTE_ARRAY length */
+  int32_t max_def;         /* Column.MaxDefinitionLevel() */
+  int32_t max_rep;         /* Column.MaxRepetitionLevel() */
+  int32_t repetition;      /* leaf parquet.FieldRepetitionType */
+  char path[236];          /* dotted ColumnPath */
+} pqgpu_column_info;
+
+/* The subset of parquet.ColumnMetaData that readChunk consults
+ * (chunk_reader.go:299-362). Offsets are absolute file offsets. */
+typedef struct {
+  int32_t physical_type;
+  int32_t codec;                   /* parquet.CompressionCodec */
+  int64_t num_values;
+  int64_t total_compressed_size;
+  int64_t data_page_offset;
+  int64_t dictionary_page_offset;  /* -1 when unset */
+  int32_t has_file_path;           /* ColumnChunk.FilePath != nil -> "nyi" error */
+  int32_t pad;
+} pqgpu_chunk_meta;
+
+/* Decoded column chunk. Device pointers stay owned by the batch.
+ *  values     fixed-width values of the non-null slots, in order (the
+ *             reference's []interface{} returned by readValues,
+ *             page_v1.go:53 / page_v2.go:51): INT32/FLOAT 4 B, INT64/DOUBLE
+ *             8 B, INT96 12 B, BOOLEAN 1 B (0/1), FIXED_LEN_BYTE_ARRAY
+ *             type_length B. NULL for BYTE_ARRAY.
+ *  offsets    BYTE_ARRAY: int32[num_values+1] into payload.
+ *  payload    BYTE_ARRAY bytes.
+ *  def_levels uint8 per slot (the reference's dLevel packedArray) when
+ *             max_def > 0; NULL otherwise (all levels are 0).
+ *  rep_levels uint8 per slot when max_rep > 0, else NULL.
+ *  validity   bitmap, bit i (LSB-first) = def_levels[i] == max_def
+ *             (Arrow layout); NULL when max_def == 0 (all valid).
+ *  list_offsets (max_rep > 0): int32[num_records+1]; record r spans slots
+ *             [list_offsets[r], list_offsets[r+1]) — record boundaries are
+ *             the slots with rep_level == 0 (ColumnStore.get data_store.go:285-308).
+ */
+typedef struct {
+  int64_t num_slots;
+  int64_t num_values;
+  int64_t num_records;
+  int64_t payload_bytes;
+  int32_t physical_type;
+  int32_t value_width;
+  int32_t max_def;
+  int32_t max_rep;
+  void *values;
+  int32_t *offsets;
+  uint8_t *payload;
+  uint8_t *def_levels;
+  uint8_t *rep_levels;
+  uint32_t *validity;
+  int32_t *list_offsets;
+} pqgpu_chunk_result;
+
+/* Per-batch statistics, for the roofline accounting. */
+typedef struct {
+  int64_t num_chunks;
+  int64_t num_pages;
+  int64_t num_slots;
+  int64_t num_values;
+  int64_t input_bytes;       /* rep+def+value section bytes (decompressed) + dictionary payloads */
+  int64_t output_bytes;      /* values + levels + validity + offsets + payload materialised */
+  int64_t staged_bytes;      /* bytes resident in HBM as the decoder's input */
+  double host_plan_ms;       /* page-header walk + descriptor build (host) */
+  double host_decompress_ms; /* SNAPPY/GZIP on host threads */
+  int64_t levels_kernel_bytes; /* algorithmic bytes of k_levels: level sections + validity/levels written */
+  int64_t values_kernel_bytes; /* algorithmic bytes of k_values: value sections + values/offsets written */
+} pqgpu_batch_stats;
+
+/* ---- version / device ---------------------------------------------- */
+int pqgpu_abi_version(void);
+const char *pqgpu_status_string(int code);
+
+/* One context per GPU. Replaces the per-FileReader decode state. */
+int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err);
+void pqgpu_ctx_destroy(pqgpu_ctx *ctx);
+
+/* ---- file metadata (host) ------------------------------------------- */
+/* ReadFileMetaData(r, true) + makeSchema: file_meta.go:24-74,
+ * schema.go:1048-1079. `buf` is borrowed and must outlive the file. */
+int pqgpu_file_open(const uint8_t *buf, size_t len, pqgpu_file **out, pqgpu_error *err);
+void pqgpu_file_close(pqgpu_file *f);
+int pqgpu_file_num_row_groups(const pqgpu_file *f);
+int pqgpu_file_num_columns(const pqgpu_file *f);
+int64_t pqgpu_file_row_group_num_rows(const pqgpu_file *f, int rg);
+int pqgpu_file_column(const pqgpu_file *f, int col, pqgpu_column_info *out);
+int pqgpu_file_chunk_meta(const pqgpu_file *f, int rg, int col, pqgpu_chunk_meta *out, pqgpu_error *err);
+
+/* ---- batched chunk decode ------------------------------------------- */
+/* ctx may be NULL: a plan-only batch that walks and validates page headers
+ * (add_chunk) without a GPU; upload/decode then fail with PQ_ERR_HIP. */
+int pqgpu_batch_create(pqgpu_ctx *ctx, pqgpu_batch **out, pqgpu_error *err);
+void pqgpu_batch_destroy(pqgpu_batch *b);
+/* Drop all chunks (keeps device allocations for reuse). */
+int pqgpu_batch_reset(pqgpu_batch *b);
+
+/* readChunk + readPages (chunk_reader.go:182-362): walk the chunk's page
+ * headers on the host, validate them exactly as the reference does, and
+ * stage the page sections (decompressed on host threads when the codec is
+ * SNAPPY/GZIP) for upload. `file_bytes` is the whole file (offsets in `meta`
+ * are absolute); `col` carries maxD/maxR (schema.go:893-924).
+ * A chunk-level error is recorded and returned here; the chunk id is still
+ * assigned so its error can be queried later. */
+int pqgpu_batch_add_chunk(pqgpu_batch *b, const uint8_t *file_bytes, size_t file_len,
+                          const pqgpu_column_info *col, const pqgpu_chunk_meta *meta,
+                          int validate_crc, int32_t *chunk_id, pqgpu_error *err);
+/* Convenience: column `col` of row group `rg` of an opened file
+ * (FileReader.readRowGroupData chunk_reader.go:375-404). */
+int pqgpu_batch_add_file_chunk(pqgpu_batch *b, const pqgpu_file *f, int rg, int col, int validate_crc,
+                               int32_t *chunk_id, pqgpu_error *err);
+
+/* Copy staged page bytes and descriptors to HBM (hipMemcpyAsync from
+ * pinned memory) and allocate the outputs. */
+int pqgpu_batch_upload(pqgpu_batch *b, void *stream, pqgpu_error *err);
+/* Launch the decode kernels (pageReader.readValues for every page of every
+ * chunk, page_v1.go:33-63 / page_v2.go:31-60). Asynchronous except for
+ * BYTE_ARRAY dictionary chunks, whose payload size is read back once. */
+int pqgpu_batch_decode(pqgpu_batch *b, void *stream, pqgpu_error *err);
+/* Wait for the batch and return the first error in (chunk, page, stage)
+ * order — the error the reference's readValues would have returned. */
+int pqgpu_batch_sync(pqgpu_batch *b, void *stream, pqgpu_error *err);
+
+int pqgpu_batch_num_chunks(const pqgpu_batch *b);
+/* Per-chunk status after sync (the error of that chunk alone). */
+int pqgpu_batch_chunk_status(const pqgpu_batch *b, int32_t chunk_id, pqgpu_error *err);
+int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t chunk_id, pqgpu_chunk_result *out, pqgpu_error *err);
+/* Copy one chunk's outputs to host buffers sized from pqgpu_batch_chunk_result
+ * (any pointer may be NULL to skip that array). */
+int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values, int32_t *offsets, uint8_t *payload,
+                           uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
+                           pqgpu_error *err);
+int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out);
+
+/* Timing hook for the benchmark: average duration (ms) of the dominant
+ * decode kernel over the last `pqgpu_batch_decode` calls, measured with HIP
+ * events on the stream the kernel runs on; and its name. */
+int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
+int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1284 @@
+// host.cpp — C ABI of the MI355X Parquet column-chunk decoder (include/pqgpu.h).
+//
+// Host side of the boundary: walks Thrift page headers and validates them
+// exactly as the reference's readChunk/readPages/page read() do
+// (chunk_reader.go:182-362, page_v1.go:87-122, page_v2.go:79-131), stages the
+// page sections (decompressing SNAPPY/GZIP pages on host threads), builds the
+// flat page/work descriptor tables and drives the gfx950 kernels
+// (kernels.hip). There is no CPU decode path: every value, level, offset and
+// payload byte is produced on the GPU; if the HIP runtime or device is
+// missing, pqgpu_ctx_create fails with PQ_ERR_HIP.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/pqgpu.h"
+#include "format.h"
+#include "kernels.h"
+#include "pq_device.h"
+
+namespace pq {
+hipError_t launch_ba_offsets_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, const uint64_t *tile_off,
+                                  uint32_t max_tiles, uint64_t *totals, hipStream_t s);
+hipError_t launch_ba_gather_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, uint32_t grid_x,
+                                 hipStream_t s);
+}  // namespace pq
+
+using namespace pq;
+
+static void set_err(pqgpu_error *e, int code, int chunk, int page, const std::string &msg) {
+  if (!e) return;
+  e->code = code;
+  e->chunk = chunk;
+  e->page = page;
+  snprintf(e->msg, sizeof(e->msg), "%s", msg.c_str());
+}
+static void clear_err(pqgpu_error *e) {
+  if (e) set_err(e, PQ_OK, -1, -1, "");
+}
+
+#define HIPCHECK(expr, errp)                                                                           \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess) {                                                                            \
+      set_err(errp, PQ_ERR_HIP, -1, -1, std::string(#expr) + ": " + hipGetErrorString(_e));           \
+      return PQ_ERR_HIP;                                                                               \
+    }                                                                                                  \
+  } while (0)
+
+struct pqgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+struct pqgpu_file {
+  FileMeta meta;
+  const uint8_t *buf = nullptr;
+  int64_t len = 0;
+};
+
+namespace {
+
+// Go-semantics varint readers over a byte range (helpers.go:151-208, Go 1.17 binary.ReadUvarint).
+struct GoReader {
+  const uint8_t *p;
+  int64_t n, i = 0;
+  int uvarint(uint64_t *out) {
+    uint64_t x = 0;
+    unsigned s = 0;
+    for (int k = 0;; k++) {
+      if (i >= n) { *out = x; return PQ_ERR_EOF; }
+      uint8_t b = p[i++];
+      if (b < 0x80) {
+        if (k > 9 || (k == 9 && b > 1)) return PQ_ERR_RANGE;
+        if (s < 64) x |= (uint64_t)b << s;
+        *out = x;
+        return PQ_OK;
+      }
+      if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
+      s += 7;
+    }
+  }
+  int uvariant32(int32_t *out) {
+    uint64_t v;
+    int e = uvarint(&v);
+    if (e) return e;
+    if (v > 0x7fffffffULL) return PQ_ERR_RANGE;
+    *out = (int32_t)v;
+    return PQ_OK;
+  }
+  int varint64(int64_t *out) {
+    uint64_t u;
+    int e = uvarint(&u);
+    int64_t x = (int64_t)(u >> 1);
+    if (u & 1) x = ~x;
+    *out = x;
+    return e;
+  }
+  int variant32(int32_t *out) {
+    int64_t v;
+    int e = varint64(&v);
+    if (e) return e;
+    if (v > 2147483647LL || v < -2147483648LL) return PQ_ERR_RANGE;
+    *out = (int32_t)v;
+    return PQ_OK;
+  }
+  int readfull(int64_t k) {  // io.ReadFull semantics, bytes skipped
+    if (k <= 0) return PQ_OK;
+    if (i >= n) return PQ_ERR_EOF;
+    if (n - i < k) { i = n; return PQ_ERR_UNEXPECTED_EOF; }
+    i += k;
+    return PQ_OK;
+  }
+};
+
+struct HostChunk {
+  pqgpu_column_info col{};
+  pqgpu_chunk_meta meta{};
+  pqgpu_error err{};  // readPages-level (host) error
+  uint32_t first_page = 0, num_pages = 0;
+  uint64_t num_slots = 0;
+  int32_t value_width = 0;
+  bool has_dict = false;
+  uint64_t dict_off = 0;  // stage offset
+  uint32_t dict_len = 0, dict_count = 0;
+  // device outputs (offsets into the arena)
+  uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0,
+           o_dict_offsets = 0;
+  uint64_t payload_cap = 0;
+  uint8_t *payload = nullptr;  // separately allocated (size known after the offsets scan)
+  // results after sync
+  int64_t nn = 0, records = 0, payload_bytes = 0;
+  pqgpu_error dev_err{};
+};
+
+// Value-decoder choice: getValuesDecoder chunk_reader.go:106-159.
+int pick_vkind(int32_t enc, int32_t type, int32_t type_length, uint8_t *vk, std::string *msg) {
+  if (enc == ENC_PLAIN_DICTIONARY) enc = ENC_RLE_DICTIONARY;
+  auto unsup = [&](const char *what) {
+    *msg = std::string("unsupported encoding ") + std::to_string(enc) + " for " + what;
+    return PQ_ERR_UNSUPPORTED;
+  };
+  auto gpu_gap = [&]() {
+    *msg = "DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY are not implemented by the GPU decoder yet";
+    return PQ_ERR_UNSUPPORTED;
+  };
+  switch (type) {
+    case T_BOOLEAN:
+      if (enc == ENC_PLAIN) { *vk = VK_PLAIN_BOOL; return PQ_OK; }
+      if (enc == ENC_RLE) { *vk = VK_RLE_BOOL; return PQ_OK; }
+      return unsup("boolean");
+    case T_BYTE_ARRAY:
+      if (enc == ENC_PLAIN) { *vk = VK_PLAIN_BA; return PQ_OK; }
+      if (enc == ENC_DELTA_LENGTH_BYTE_ARRAY || enc == ENC_DELTA_BYTE_ARRAY) return gpu_gap();
+      if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
+      return unsup("binary");
+    case T_FLBA:
+      if (enc == ENC_PLAIN) { *vk = type_length == 0 ? VK_PLAIN_BA : VK_PLAIN_FIXED; return PQ_OK; }
+      if (enc == ENC_DELTA_BYTE_ARRAY) return gpu_gap();
+      if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
+      return unsup("fixed_len_byte_array");
+    case T_FLOAT: case T_DOUBLE:
+      if (enc == ENC_PLAIN) { *vk = VK_PLAIN_FIXED; return PQ_OK; }
+      if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
+      return unsup("float/double");
+    case T_INT96:
+      if (enc == ENC_PLAIN) { *vk = VK_PLAIN_INT96; return PQ_OK; }
+      if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
+      return unsup("int96");
+    case T_INT32: case T_INT64:
+      if (enc == ENC_PLAIN) { *vk = VK_PLAIN_FIXED; return PQ_OK; }
+      if (enc == ENC_DELTA_BINARY_PACKED) { *vk = type == T_INT32 ? VK_DELTA32 : VK_DELTA64; return PQ_OK; }
+      if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
+      return unsup("int32/int64");
+  }
+  *msg = "unsupported type";
+  return PQ_ERR_UNSUPPORTED;
+}
+
+int value_width_of(int32_t type, int32_t type_length) {
+  switch (type) {
+    case T_BOOLEAN: return 1;
+    case T_INT32: case T_FLOAT: return 4;
+    case T_INT64: case T_DOUBLE: return 8;
+    case T_INT96: return 12;
+    case T_FLBA: return type_length;  // 0 -> length-prefixed (byte array layout)
+  }
+  return 0;  // BYTE_ARRAY
+}
+
+int bits_len16(int v) {
+  int n = 0;
+  while (v) { n++; v >>= 1; }
+  return n;
+}
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct KernelTimer {
+  bool enabled = false;
+  struct Rec { int slot; hipEvent_t a, b; };
+  std::vector<Rec> recs;          // pending launch records
+  std::vector<hipEvent_t> pool;   // free events
+  double total_ms[8] = {0};
+  int64_t launches[8] = {0};
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  // Resolve pending records (the caller has synchronised the stream).
+  void resolve() {
+    for (auto &r : recs) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) { total_ms[r.slot] += ms; launches[r.slot] += 1; }
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    recs.clear();
+  }
+  void destroy() {
+    for (auto &r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
+    recs.clear();
+    for (auto e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+  }
+};
+static const char *kTimerNames[8] = {"k_levels", "k_values", "k_scan_runs", "k_bases",
+                                     "k_dict_ba", "k_ba_offsets", "k_ba_gather", "k_records"};
+
+struct pqgpu_batch {
+  pqgpu_ctx *ctx = nullptr;
+  std::vector<HostChunk> chunks;
+  std::vector<PageDesc> pages;
+  std::vector<uint8_t> stage;
+  std::vector<WorkItem> items;
+  std::vector<uint32_t> level_pages, scan_pages, base_chunks, dict_ba_chunks, ba_chunks, rec_pages;
+  std::vector<uint64_t> run_base, tile_base;
+  uint64_t run_total = 0, tile_total = 0;
+  std::vector<uint32_t> page_nn_init;
+  std::vector<uint64_t> ba_tile_off;
+  uint64_t ba_tiles_total = 0;
+  uint32_t ba_max_tiles = 0;
+  // device
+  uint8_t *d_stage = nullptr;
+  size_t d_stage_cap = 0;
+  uint8_t *h_pinned = nullptr;
+  size_t h_pinned_cap = 0;
+  uint8_t *d_arena = nullptr;
+  size_t d_arena_cap = 0;
+  uint64_t arena_size = 0;
+  // arena offsets of batch-level arrays
+  uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
+           o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
+           o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
+  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
+  std::vector<ChunkDesc> chunk_desc;
+  bool uploaded = false, decoded = false;
+  pqgpu_batch_stats stats{};
+  KernelTimer timer;
+  std::vector<uint8_t *> payload_allocs;
+};
+
+// ---------------------------------------------------------------------------
+// Planning: readChunk / readPages on the host
+// ---------------------------------------------------------------------------
+static int chunk_fail(pqgpu_batch *b, HostChunk &hc, int32_t id, int code, int page, const std::string &msg,
+                      pqgpu_error *err) {
+  set_err(&hc.err, code, id, page, msg);
+  if (err) *err = hc.err;
+  // drop the pages staged for this chunk: the reference returns before any readValues
+  b->pages.resize(hc.first_page);
+  hc.num_pages = 0;
+  return code;
+}
+
+static uint64_t stage_append(pqgpu_batch *b, const uint8_t *src, int64_t n) {
+  uint64_t off = align_up(b->stage.size(), 16);
+  b->stage.resize(off + (size_t)n);
+  if (n) memcpy(b->stage.data() + off, src, (size_t)n);
+  return off;
+}
+
+// readPageBlock (chunk_reader.go:161-180) + newBlockReader (compress.go:102-123) for a whole block.
+static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *count, int32_t csize, int32_t usize,
+                      int validate_crc, const PageHeader &ph, int32_t codec, std::vector<uint8_t> *out,
+                      int64_t skip_levels, std::string *msg) {
+  if (csize < 0 || usize < 0) { *msg = "invalid page data size"; return PQ_ERR_INVALID; }
+  int64_t avail = *off >= flen ? 0 : flen - *off;
+  int64_t take = std::min<int64_t>(csize, avail);
+  const uint8_t *blk = file + std::min<int64_t>(*off, flen);
+  *off += take;
+  *count += take;
+  if (validate_crc && ph.has_crc) {
+    uint32_t sum = (uint32_t)crc32(0L, blk, (uInt)take);
+    if (sum != (uint32_t)ph.crc) { *msg = "CRC32 check failed"; return PQ_ERR_CRC; }
+  }
+  // V2: the level bytes are copied raw, only the values part goes through the codec (page_v2.go:112-127)
+  if (skip_levels > 0) {
+    if (skip_levels > take) { *msg = "slice bounds out of range"; return PQ_ERR_INVALID; }
+    out->insert(out->end(), blk, blk + skip_levels);
+    blk += skip_levels;
+    take -= skip_levels;
+    csize -= (int32_t)skip_levels;
+    usize -= (int32_t)skip_levels;
+    if (csize < 0 || usize < 0) { *msg = "invalid page data size"; return PQ_ERR_INVALID; }
+  }
+  if (take != csize) {
+    *msg = "compressed data must be " + std::to_string(csize) + " byte but its " + std::to_string(take) + " byte";
+    return PQ_ERR_INVALID;
+  }
+  size_t before = out->size();
+  Status st = Decompress(codec, blk, take, out);
+  if (!st.ok()) { *msg = st.msg; return st.code; }
+  if ((int64_t)(out->size() - before) != usize) {
+    *msg = "decompressed data must be " + std::to_string(usize) + " byte but its " +
+           std::to_string(out->size() - before) + " byte";
+    return PQ_ERR_DECOMPRESS;
+  }
+  return PQ_OK;
+}
+
+// Values decoder init() (reference: valuesDecoder.init called from page read()).
+static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_t vk, PageDesc *pd,
+                       std::string *msg) {
+  GoReader r{page + vstart, plen - vstart};
+  pd->val_off = (uint32_t)vstart;
+  pd->val_len = (uint32_t)(plen - vstart);
+  if (vk == VK_DICT) {  // dictDecoder.init type_dict.go:22-38
+    if (r.i >= r.n) { *msg = "EOF"; return PQ_ERR_EOF; }
+    uint8_t w = r.p[0];
+    if (w > 32) { *msg = "invalid bitwidth " + std::to_string(w); return PQ_ERR_INVALID; }
+    pd->dict_bw = w;
+    pd->val_off += 1;
+    pd->val_len -= 1;
+    return PQ_OK;
+  }
+  if (vk == VK_RLE_BOOL) {  // booleanRLEDecoder.init type_boolean.go:104-107 (hybrid initSize)
+    int e = r.readfull(4);
+    if (e) { *msg = "boolean rle size"; return e; }
+    uint32_t size;
+    memcpy(&size, r.p, 4);
+    int64_t rem = r.n - 4;
+    pd->dict_bw = 1;
+    pd->val_off += 4;
+    pd->val_len = (uint32_t)std::min<int64_t>(size, rem);
+    return PQ_OK;
+  }
+  if (vk == VK_DELTA32 || vk == VK_DELTA64) {  // deltaBitPackDecoder.init deltabp_decoder.go:35-111
+    bool is64 = vk == VK_DELTA64;
+    int32_t bs, mbc, vc;
+    int e;
+    if ((e = r.uvariant32(&bs))) { *msg = "failed to read block size"; return e; }
+    if ((e = r.uvariant32(&mbc))) { *msg = "failed to read number of mini blocks"; return e; }
+    if (mbc <= 0 || bs % mbc != 0) { *msg = "int/delta: invalid number of mini blocks"; return PQ_ERR_INVALID; }
+    int32_t mbvc = bs / mbc;
+    if (mbvc == 0) { *msg = "invalid mini block value count, it can't be zero"; return PQ_ERR_INVALID; }
+    if ((e = r.uvariant32(&vc))) { *msg = "failed to read total value count"; return e; }
+    int64_t first;
+    if (is64) {
+      if ((e = r.varint64(&first))) { *msg = "failed to read first value"; return e; }
+    } else {
+      int32_t f32;
+      if ((e = r.variant32(&f32))) { *msg = "failed to read first value"; return e; }
+      first = f32;
+    }
+    int64_t mb_start = r.i;
+    int64_t md;
+    if (is64) {
+      if ((e = r.varint64(&md))) { *msg = "failed to read min delta"; return e; }
+    } else {
+      int32_t m32;
+      if ((e = r.variant32(&m32))) { *msg = "failed to read min delta"; return e; }
+    }
+    int64_t wstart = r.i;
+    if ((e = r.readfull(mbc))) { *msg = "not enough data to read all miniblock bit widths"; return e; }
+    for (int32_t k = 0; k < mbc; k++)
+      if (r.p[wstart + k] > (is64 ? 64 : 32)) { *msg = "invalid miniblock bit width"; return PQ_ERR_INVALID; }
+    pd->delta_first = first;
+    pd->delta_count = vc;
+    pd->delta_mbc = (uint16_t)std::min<int32_t>(mbc, 65535);
+    pd->delta_mbvc = (uint32_t)mbvc;
+    pd->delta_first_mb = (uint32_t)(vstart + mb_start);
+    if (mbvc % 8 != 0 || (int64_t)bs / 8 > 256 || mbc > 64) pd->flags |= PF_DELTA_SLOW;
+    if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
+    return PQ_OK;
+  }
+  return PQ_OK;
+}
+
+static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, const pqgpu_column_info *col,
+                          const pqgpu_chunk_meta *meta, int validate_crc, int32_t *chunk_id, pqgpu_error *err) {
+  auto t0 = std::chrono::steady_clock::now();
+  int32_t id = (int32_t)b->chunks.size();
+  if (chunk_id) *chunk_id = id;
+  b->chunks.emplace_back();
+  HostChunk &hc = b->chunks.back();
+  hc.col = *col;
+  hc.meta = *meta;
+  clear_err(&hc.err);
+  hc.err.chunk = id;
+  hc.first_page = (uint32_t)b->pages.size();
+  hc.value_width = value_width_of(col->physical_type, col->type_length);
+  b->uploaded = false;
+  clear_err(err);
+  if (meta->has_file_path) return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, -1, "nyi: data is in another file", err);
+  if (meta->physical_type != col->physical_type)
+    return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "wrong type in Column chunk metadata", err);
+  if (col->max_def > 255 || col->max_rep > 255)
+    return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, -1, "levels deeper than 255 are not supported", err);
+  int64_t off = meta->dictionary_page_offset >= 0 ? meta->dictionary_page_offset : meta->data_page_offset;
+  if (off < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "seek: negative position", err);
+  const int max_rep = col->max_rep, max_def = col->max_def;
+  int64_t count = 0;
+  std::string msg;
+  std::vector<uint8_t> block;
+  double decomp_ms = 0;
+  while (meta->total_compressed_size - count > 0) {
+    PageHeader ph;
+    int64_t consumed = 0;
+    bool ok = off < flen && ParsePageHeader(file + off, flen - off, &ph, &consumed);
+    off += consumed;
+    count += consumed;
+    if (!ok) return chunk_fail(b, hc, id, PQ_ERR_THRIFT, -1, "thrift: invalid page header", err);
+    if (ph.type == 2) {  // DICTIONARY_PAGE page_dict.go:35-72
+      if (hc.has_dict) return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "there should be only one dictionary", err);
+      if (col->physical_type == T_BOOLEAN)
+        return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, -1, "type BOOLEAN is not supported for dict value encoder", err);
+      if (!ph.has_dict) return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "null DictionaryPageHeader", err);
+      if (ph.dict.num_values < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "negative NumValues in DICTIONARY_PAGE", err);
+      if (ph.dict.encoding != ENC_PLAIN && ph.dict.encoding != ENC_PLAIN_DICTIONARY)
+        return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, -1,
+                          "only Encoding_PLAIN and Encoding_PLAIN_DICTIONARY is supported for dict values encoder", err);
+      block.clear();
+      auto d0 = std::chrono::steady_clock::now();
+      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg);
+      decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+      if (e) return chunk_fail(b, hc, id, e, -1, msg, err);
+      hc.has_dict = true;
+      hc.dict_count = (uint32_t)ph.dict.num_values;
+      hc.dict_len = (uint32_t)block.size();
+      hc.dict_off = stage_append(b, block.data(), (int64_t)block.size());
+      int w = hc.value_width;
+      if (w > 0) {  // fixed width PLAIN dictionary: binary.Read per entry
+        uint64_t need = (uint64_t)w * hc.dict_count;
+        if (need > block.size()) {
+          uint64_t rem = block.size() % (uint64_t)w;
+          if (col->physical_type == T_INT96 && block.size() / 12 + 1 == hc.dict_count && rem)
+            return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "truncated INT96 dictionary entry (nil slot)", err);
+          return chunk_fail(b, hc, id, rem == 0 ? PQ_ERR_EOF : PQ_ERR_UNEXPECTED_EOF, -1,
+                            "expected " + std::to_string(hc.dict_count) + " values", err);
+        }
+      }
+      if (meta->dictionary_page_offset >= 0 && meta->dictionary_page_offset != off) {
+        int64_t np = meta->data_page_offset;
+        if (np < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, -1, "seek: negative position", err);
+        count += np - off;
+        off = np;
+      }
+      continue;
+    }
+    if (ph.type != 0 && ph.type != 3)
+      return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, -1, "DATA_PAGE or DATA_PAGE_V2 type supported", err);
+    int pi = (int)b->pages.size() - (int)hc.first_page;
+    PageDesc pd;
+    memset(&pd, 0, sizeof(pd));
+    pd.chunk = (uint32_t)id;
+    pd.page_in_chunk = (uint32_t)pi;
+    block.clear();
+    uint8_t vk = 0;
+    if (ph.type == 0) {
+      // dataPageReaderV1.init page_v1.go:65-85 then read :87-122
+      if (!ph.has_dph) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "page header is missing data page header", err);
+      if (max_rep > 0 && ph.dph.rep_enc != ENC_RLE)
+        return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "encoding is not supported for definition and repetition level", err);
+      if (max_def > 0 && ph.dph.def_enc != ENC_RLE)
+        return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "encoding is not supported for definition and repetition level", err);
+      if (ph.dph.num_values < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "negative NumValues in DATA_PAGE", err);
+      auto d0 = std::chrono::steady_clock::now();
+      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg);
+      decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+      if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
+      if ((e = pick_vkind(ph.dph.encoding, col->physical_type, col->type_length, &vk, &msg)))
+        return chunk_fail(b, hc, id, e, pi, msg, err);
+      pd.num_slots = (uint32_t)ph.dph.num_values;
+      GoReader r{block.data(), (int64_t)block.size()};
+      if (max_rep > 0) {  // hybridDecoder.initSize: u32 length, LimitReader, ReadAll (buffered)
+        if ((e = r.readfull(4))) return chunk_fail(b, hc, id, e, pi, "read repetition level size", err);
+        uint32_t sz;
+        memcpy(&sz, block.data() + r.i - 4, 4);
+        int64_t take = std::min<int64_t>(sz, r.n - r.i);
+        pd.rep_off = (uint32_t)r.i;
+        pd.rep_len = (uint32_t)take;
+        pd.flags |= PF_REP;
+        r.i += take;
+      }
+      if (max_def > 0) {
+        if ((e = r.readfull(4))) return chunk_fail(b, hc, id, e, pi, "read definition level size", err);
+        uint32_t sz;
+        memcpy(&sz, block.data() + r.i - 4, 4);
+        int64_t take = std::min<int64_t>(sz, r.n - r.i);
+        pd.def_off = (uint32_t)r.i;
+        pd.def_len = (uint32_t)take;
+        pd.flags |= PF_DEF;
+        r.i += take;
+      }
+      if ((e = init_values(block.data(), (int64_t)block.size(), r.i, vk, &pd, &msg)))
+        return chunk_fail(b, hc, id, e, pi, msg, err);
+    } else {
+      // dataPageReaderV2.read page_v2.go:79-131
+      if (!ph.has_dph2) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "null DataPageHeaderV2", err);
+      if (ph.dph2.num_values < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "negative NumValues in DATA_PAGE_V2", err);
+      if (ph.dph2.rep_len < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "invalid RepetitionLevelsByteLength", err);
+      if (ph.dph2.def_len < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "invalid DefinitionLevelsByteLength", err);
+      int e;
+      if ((e = pick_vkind(ph.dph2.encoding, col->physical_type, col->type_length, &vk, &msg)))
+        return chunk_fail(b, hc, id, e, pi, msg, err);
+      int64_t levels = (int64_t)ph.dph2.rep_len + ph.dph2.def_len;
+      auto d0 = std::chrono::steady_clock::now();
+      e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, levels, &msg);
+      decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+      if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
+      pd.num_slots = (uint32_t)ph.dph2.num_values;
+      pd.flags |= PF_V2;
+      if (ph.dph2.rep_len > 0 && max_rep > 0) { pd.rep_off = 0; pd.rep_len = (uint32_t)ph.dph2.rep_len; pd.flags |= PF_REP; }
+      if (ph.dph2.def_len > 0 && max_def > 0) {
+        pd.def_off = (uint32_t)ph.dph2.rep_len;
+        pd.def_len = (uint32_t)ph.dph2.def_len;
+        pd.flags |= PF_DEF;
+      }
+      if ((e = init_values(block.data(), (int64_t)block.size(), levels, vk, &pd, &msg)))
+        return chunk_fail(b, hc, id, e, pi, msg, err);
+    }
+    pd.vkind = vk;
+    pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
+    pd.slot_base = hc.num_slots;
+    hc.num_slots += pd.num_slots;
+    b->pages.push_back(pd);
+    hc.num_pages++;
+  }
+  b->stats.host_decompress_ms += decomp_ms;
+  b->stats.host_plan_ms +=
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - decomp_ms;
+  return PQ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Upload: arena layout, descriptors, work lists
+// ---------------------------------------------------------------------------
+static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
+  const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
+  b->items.clear();
+  b->level_pages.clear();
+  b->scan_pages.clear();
+  b->base_chunks.clear();
+  b->dict_ba_chunks.clear();
+  b->ba_chunks.clear();
+  b->rec_pages.clear();
+  b->run_base.assign(np, 0);
+  b->tile_base.assign(np, 0);
+  b->page_nn_init.assign(np, 0);
+  b->ba_tile_off.clear();
+  b->run_total = b->tile_total = 0;
+  b->ba_tiles_total = 0;
+  b->ba_max_tiles = 0;
+  uint64_t a = 0;
+  auto take = [&](uint64_t bytes) {
+    uint64_t o = align_up(a, 256);
+    a = o + align_up(std::max<uint64_t>(bytes, 1), 16);
+    return o;
+  };
+  int64_t in_bytes = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    HostChunk &hc = b->chunks[c];
+    if (hc.err.code) continue;
+    const int w = hc.value_width;
+    const uint64_t ns = hc.num_slots;
+    bool is_ba = w == 0;
+    hc.o_values = is_ba ? 0 : take(ns * (uint64_t)w);
+    hc.o_def = hc.col.max_def > 1 ? take(ns) : 0;
+    hc.o_rep = hc.col.max_rep > 0 ? take(ns) : 0;
+    hc.o_valid = hc.col.max_def > 0 ? take(((ns + 31) / 32 + 2) * 4) : 0;
+    hc.o_lists = hc.col.max_rep > 0 ? take((ns + 1) * 4) : 0;
+    hc.o_offsets = is_ba ? take((ns + 1) * 4) : 0;
+    hc.o_ba_index = is_ba ? take(ns * 8) : 0;
+    hc.o_dict_offsets = (hc.has_dict && is_ba) ? take((uint64_t)hc.dict_count * 8) : 0;
+    b->base_chunks.push_back(c);
+    if (hc.has_dict) {
+      in_bytes += hc.dict_len;
+      if (is_ba) b->dict_ba_chunks.push_back(c);
+    }
+    if (is_ba) {
+      b->ba_chunks.push_back(c);
+      uint64_t nt = (ns + kBaTile - 1) / kBaTile;
+      b->ba_tile_off.push_back(b->ba_tiles_total);
+      b->ba_tiles_total += std::max<uint64_t>(nt, 1);
+      b->ba_max_tiles = std::max<uint32_t>(b->ba_max_tiles, (uint32_t)std::max<uint64_t>(nt, 1));
+    }
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+      PageDesc &pd = b->pages[p];
+      in_bytes += pd.rep_len + pd.def_len + pd.val_len;
+      if (hc.col.max_def > 0 || hc.col.max_rep > 0) b->level_pages.push_back(p);
+      else b->page_nn_init[p] = pd.num_slots;
+      if (hc.col.max_rep > 0) b->rec_pages.push_back(p);
+      const uint32_t ns_p = pd.num_slots;
+      auto tiles = [&](uint8_t kind, uint32_t tile) {
+        for (uint32_t v0 = 0; v0 < ns_p; v0 += tile) b->items.push_back(WorkItem{p, v0, std::min(v0 + tile, ns_p), kind, {0, 0, 0}});
+      };
+      switch (pd.vkind) {
+        case VK_PLAIN_FIXED: case VK_PLAIN_INT96: tiles(WI_PLAIN, kPlainTile); break;
+        case VK_PLAIN_BOOL: tiles(WI_BOOL, kPlainTile); break;
+        case VK_DICT: case VK_RLE_BOOL: {
+          if (pd.dict_bw > 0 && ns_p > 0) {
+            b->scan_pages.push_back(p);
+            uint64_t cap = std::min<uint64_t>(ns_p, (uint64_t)pd.val_len / 2 + 1) + 1;
+            b->run_base[p] = b->run_total;
+            b->run_total += cap;
+            b->tile_base[p] = b->tile_total;
+            b->tile_total += (ns_p + kDictTile - 1) / kDictTile;
+          }
+          tiles(WI_DICT, kDictTile);
+          break;
+        }
+        case VK_DELTA32: case VK_DELTA64:
+          if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_DELTA, {0, 0, 0}});
+          break;
+        case VK_PLAIN_BA:
+          if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_PLAIN_BA, {0, 0, 0}});
+          break;
+      }
+    }
+  }
+  // batch-level arrays
+  b->o_pages = take((uint64_t)np * sizeof(PageDesc));
+  b->o_chunks = take((uint64_t)nc * sizeof(ChunkDesc));
+  b->o_err = take((uint64_t)nc * 8);
+  b->o_nn = take((uint64_t)np * 4);
+  b->o_rec = take((uint64_t)np * 4);
+  b->o_vbase = take((uint64_t)np * 8);
+  b->o_rbase = take((uint64_t)np * 8);
+  b->o_runs = take(b->run_total * sizeof(HybRun));
+  b->o_run_base = take((uint64_t)np * 8);
+  b->o_run_count = take((uint64_t)np * 4);
+  b->o_tile_first = take(b->tile_total * 4);
+  b->o_tile_base = take((uint64_t)np * 8);
+  b->o_items = take(b->items.size() * sizeof(WorkItem));
+  b->o_ba_tile_sum = take(b->ba_tiles_total * 4);
+  b->o_ba_tile_off = take(b->ba_tile_off.size() * 8);
+  b->o_ba_totals = take(b->ba_chunks.size() * 8);
+  b->l_level = take(b->level_pages.size() * 4);
+  b->l_scan = take(b->scan_pages.size() * 4);
+  b->l_base = take(b->base_chunks.size() * 4);
+  b->l_dict_ba = take(b->dict_ba_chunks.size() * 4);
+  b->l_ba = take(b->ba_chunks.size() * 4);
+  b->l_rec = take(b->rec_pages.size() * 4);
+  b->arena_size = a;
+  if (a > b->d_arena_cap) {
+    if (b->d_arena) (void)hipFree(b->d_arena);
+    b->d_arena = nullptr;
+    b->d_arena_cap = 0;
+    HIPCHECK(hipMalloc(&b->d_arena, a), err);
+    b->d_arena_cap = a;
+  }
+  // stage: pinned host copy + device buffer (64 B zero pad)
+  size_t ssz = align_up(b->stage.size(), 16) + 64;
+  if (ssz > b->d_stage_cap) {
+    if (b->d_stage) (void)hipFree(b->d_stage);
+    b->d_stage = nullptr;
+    b->d_stage_cap = 0;
+    HIPCHECK(hipMalloc(&b->d_stage, ssz), err);
+    b->d_stage_cap = ssz;
+  }
+  if (ssz > b->h_pinned_cap) {
+    if (b->h_pinned) (void)hipHostFree(b->h_pinned);
+    b->h_pinned = nullptr;
+    b->h_pinned_cap = 0;
+    HIPCHECK(hipHostMalloc((void **)&b->h_pinned, ssz, hipHostMallocDefault), err);
+    b->h_pinned_cap = ssz;
+  }
+  memcpy(b->h_pinned, b->stage.data(), b->stage.size());
+  memset(b->h_pinned + b->stage.size(), 0, ssz - b->stage.size());
+  HIPCHECK(hipMemcpyAsync(b->d_stage, b->h_pinned, ssz, hipMemcpyHostToDevice, s), err);
+
+  uint8_t *A = b->d_arena;
+  auto dp = [&](uint64_t o) { return (uint64_t)(A + o); };
+  // chunk descriptors
+  b->chunk_desc.assign(nc, ChunkDesc{});
+  for (uint32_t c = 0; c < nc; c++) {
+    HostChunk &hc = b->chunks[c];
+    ChunkDesc &cd = b->chunk_desc[c];
+    memset(&cd, 0, sizeof(cd));
+    cd.type = hc.col.physical_type;
+    cd.type_length = hc.col.type_length;
+    cd.max_def = hc.col.max_def;
+    cd.max_rep = hc.col.max_rep;
+    cd.def_bw = bits_len16(hc.col.max_def);
+    cd.rep_bw = bits_len16(hc.col.max_rep);
+    cd.value_width = hc.value_width;
+    cd.first_page = hc.first_page;
+    cd.num_pages = hc.num_pages;
+    cd.num_slots = hc.num_slots;
+    cd.nn_capacity = hc.num_slots;
+    if (hc.err.code) { cd.flags |= CF_FAILED; continue; }
+    if (hc.has_dict) {
+      cd.flags |= CF_DICT;
+      cd.dict_raw = (uint64_t)(b->d_stage + hc.dict_off);
+      cd.dict_raw_len = hc.dict_len;
+      cd.dict_count = hc.dict_count;
+      cd.dict_values = cd.dict_raw;
+      cd.dict_offsets = hc.o_dict_offsets ? dp(hc.o_dict_offsets) : 0;
+    }
+    cd.values = hc.o_values ? dp(hc.o_values) : 0;
+    cd.def_levels = hc.o_def ? dp(hc.o_def) : 0;
+    cd.rep_levels = hc.o_rep ? dp(hc.o_rep) : 0;
+    cd.validity = hc.o_valid ? dp(hc.o_valid) : 0;
+    cd.list_offsets = hc.o_lists ? dp(hc.o_lists) : 0;
+    cd.offsets = hc.o_offsets ? dp(hc.o_offsets) : 0;
+    cd.ba_index = hc.o_ba_index ? dp(hc.o_ba_index) : 0;
+  }
+  std::vector<PageDesc> pages = b->pages;
+  for (auto &pd : pages) pd.data = (uint64_t)(b->d_stage + pd.data);
+  auto up = [&](uint64_t o, const void *src, size_t n) -> hipError_t {
+    if (!n) return hipSuccess;
+    return hipMemcpyAsync(A + o, src, n, hipMemcpyHostToDevice, s);
+  };
+  HIPCHECK(up(b->o_pages, pages.data(), pages.size() * sizeof(PageDesc)), err);
+  HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
+  HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
+  HIPCHECK(up(b->o_tile_base, b->tile_base.data(), np * 8), err);
+  HIPCHECK(up(b->o_items, b->items.data(), b->items.size() * sizeof(WorkItem)), err);
+  HIPCHECK(up(b->o_ba_tile_off, b->ba_tile_off.data(), b->ba_tile_off.size() * 8), err);
+  HIPCHECK(up(b->l_level, b->level_pages.data(), b->level_pages.size() * 4), err);
+  HIPCHECK(up(b->l_scan, b->scan_pages.data(), b->scan_pages.size() * 4), err);
+  HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
+  HIPCHECK(up(b->l_dict_ba, b->dict_ba_chunks.data(), b->dict_ba_chunks.size() * 4), err);
+  HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
+  HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
+  // the host copies above read from std::vector memory: wait before those vectors change
+  HIPCHECK(hipStreamSynchronize(s), err);
+  b->stats.num_chunks = nc;
+  b->stats.num_pages = np;
+  b->stats.input_bytes = in_bytes;
+  b->stats.staged_bytes = (int64_t)b->stage.size();
+  b->uploaded = true;
+  return PQ_OK;
+}
+
+static BatchDev batch_dev(pqgpu_batch *b) {
+  uint8_t *A = b->d_arena;
+  BatchDev d;
+  d.pages = (const PageDesc *)(A + b->o_pages);
+  d.chunks = (const ChunkDesc *)(A + b->o_chunks);
+  d.chunk_err = (unsigned long long *)(A + b->o_err);
+  d.page_nn = (uint32_t *)(A + b->o_nn);
+  d.page_rec = (uint32_t *)(A + b->o_rec);
+  d.page_vbase = (uint64_t *)(A + b->o_vbase);
+  d.page_rbase = (uint64_t *)(A + b->o_rbase);
+  d.runs = (HybRun *)(A + b->o_runs);
+  d.run_base = (const uint64_t *)(A + b->o_run_base);
+  d.run_count = (uint32_t *)(A + b->o_run_count);
+  d.tile_first = (uint32_t *)(A + b->o_tile_first);
+  d.tile_base = (const uint64_t *)(A + b->o_tile_base);
+  d.ba_tile_sum = (uint32_t *)(A + b->o_ba_tile_sum);
+  d.npages = (uint32_t)b->pages.size();
+  d.nchunks = (uint32_t)b->chunks.size();
+  return d;
+}
+
+static LaunchLists launch_lists(pqgpu_batch *b) {
+  uint8_t *A = b->d_arena;
+  LaunchLists l;
+  l.level_pages = (const uint32_t *)(A + b->l_level);
+  l.n_level_pages = (uint32_t)b->level_pages.size();
+  l.scan_pages = (const uint32_t *)(A + b->l_scan);
+  l.n_scan_pages = (uint32_t)b->scan_pages.size();
+  l.base_chunks = (const uint32_t *)(A + b->l_base);
+  l.n_base_chunks = (uint32_t)b->base_chunks.size();
+  l.items = (const WorkItem *)(A + b->o_items);
+  l.n_items = (uint32_t)b->items.size();
+  l.dict_ba_chunks = (const uint32_t *)(A + b->l_dict_ba);
+  l.n_dict_ba = (uint32_t)b->dict_ba_chunks.size();
+  l.ba_chunks = (const uint32_t *)(A + b->l_ba);
+  l.n_ba_chunks = (uint32_t)b->ba_chunks.size();
+  l.rec_pages = (const uint32_t *)(A + b->l_rec);
+  l.n_rec_pages = (uint32_t)b->rec_pages.size();
+  return l;
+}
+
+// Launch with optional event timing on the launch stream.
+template <class F>
+static hipError_t timed(pqgpu_batch *b, int slot, hipStream_t s, F f) {
+  KernelTimer &t = b->timer;
+  if (!t.enabled) return f();
+  hipEvent_t ea = t.get(), eb = t.get();
+  if (!ea || !eb) return hipErrorOutOfMemory;
+  hipError_t e = hipEventRecord(ea, s);
+  if (e != hipSuccess) return e;
+  e = f();
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(eb, s);
+  t.recs.push_back(KernelTimer::Rec{slot, ea, eb});
+  return e;
+}
+
+static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
+  if (!b->uploaded) {
+    int e = build_and_upload(b, s, err);
+    if (e) return e;
+  }
+  uint8_t *A = b->d_arena;
+  const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
+  // per-decode state
+  HIPCHECK(hipMemsetAsync(A + b->o_err, 0xff, (size_t)nc * 8, s), err);
+  HIPCHECK(hipMemcpyAsync(A + b->o_nn, b->page_nn_init.data(), (size_t)np * 4, hipMemcpyHostToDevice, s), err);
+  HIPCHECK(hipMemsetAsync(A + b->o_rec, 0, (size_t)np * 4, s), err);
+  HIPCHECK(hipMemsetAsync(A + b->o_run_count, 0, (size_t)np * 4, s), err);
+  if (b->tile_total) HIPCHECK(hipMemsetAsync(A + b->o_tile_first, 0xff, b->tile_total * 4, s), err);
+  for (auto &hc : b->chunks) {
+    if (hc.err.code) continue;
+    if (hc.o_valid) HIPCHECK(hipMemsetAsync(A + hc.o_valid, 0, ((hc.num_slots + 31) / 32 + 2) * 4, s), err);
+  }
+  BatchDev d = batch_dev(b);
+  LaunchLists l = launch_lists(b);
+  HIPCHECK(timed(b, 4, s, [&] { return launch_dict_ba(d, l, s); }), err);
+  HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
+  HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
+  HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
+  HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l, s); }), err);
+  if (!b->ba_chunks.empty()) {
+    HIPCHECK(timed(b, 5, s, [&] {
+               return launch_ba_offsets_impl(d, l.ba_chunks, l.n_ba_chunks, (const uint64_t *)(A + b->o_ba_tile_off),
+                                             b->ba_max_tiles, (uint64_t *)(A + b->o_ba_totals), s);
+             }),
+             err);
+    std::vector<uint64_t> totals(b->ba_chunks.size());
+    HIPCHECK(hipMemcpyAsync(totals.data(), A + b->o_ba_totals, totals.size() * 8, hipMemcpyDeviceToHost, s), err);
+    HIPCHECK(hipStreamSynchronize(s), err);
+    bool changed = false;
+    for (size_t k = 0; k < b->ba_chunks.size(); k++) {
+      HostChunk &hc = b->chunks[b->ba_chunks[k]];
+      if (totals[k] > 0x7fffffffULL) {
+        set_err(&hc.err, PQ_ERR_UNSUPPORTED, (int)b->ba_chunks[k], -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
+        continue;
+      }
+      hc.payload_bytes = (int64_t)totals[k];
+      if ((uint64_t)hc.payload_bytes + 64 > hc.payload_cap) {
+        if (hc.payload) (void)hipFree(hc.payload);
+        hc.payload = nullptr;
+        hc.payload_cap = 0;
+        HIPCHECK(hipMalloc(&hc.payload, (size_t)hc.payload_bytes + 64), err);
+        hc.payload_cap = (uint64_t)hc.payload_bytes + 64;
+      }
+      b->chunk_desc[b->ba_chunks[k]].payload = (uint64_t)hc.payload;
+      changed = true;
+    }
+    if (changed) {
+      for (uint32_t c : b->ba_chunks)
+        HIPCHECK(hipMemcpyAsync(A + b->o_chunks + (uint64_t)c * sizeof(ChunkDesc), &b->chunk_desc[c], sizeof(ChunkDesc),
+                                hipMemcpyHostToDevice, s),
+                 err);
+    }
+    uint64_t maxnn = 0;
+    for (uint32_t c : b->ba_chunks) maxnn = std::max<uint64_t>(maxnn, b->chunks[c].num_slots);
+    uint32_t gx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((maxnn + 255) / 256, 1), 4096);
+    HIPCHECK(timed(b, 6, s, [&] { return launch_ba_gather_impl(d, l.ba_chunks, l.n_ba_chunks, gx, s); }), err);
+    if (changed) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc host copies stay valid until here
+  }
+  HIPCHECK(timed(b, 7, s, [&] { return launch_records(d, l, s); }), err);
+  b->decoded = true;
+  return PQ_OK;
+}
+
+// Key -> pqgpu_error (see err_key in pq_device.h).
+static void decode_key(uint64_t key, int chunk, pqgpu_error *e) {
+  uint32_t phase = (uint32_t)(key >> 62);
+  uint32_t page = (uint32_t)((key >> 40) & 0x3fffff);
+  uint32_t stage = (uint32_t)((key >> 36) & 15);
+  uint32_t pos = (uint32_t)((key >> 4) & 0xffffffffu);
+  uint32_t code = (uint32_t)(key & 15);
+  static const char *stages[] = {"dictionary", "repetition levels", "definition levels", "values"};
+  char msg[200];
+  if (phase == 0) {
+    snprintf(msg, sizeof(msg), "%s decode failed at entry %u: %s", stages[stage & 3], pos, pqgpu_status_string((int)code));
+    set_err(e, (int)code, chunk, -1, msg);
+  } else {
+    snprintf(msg, sizeof(msg), "read %s from page failed at position %u: %s", stages[stage & 3], pos,
+             pqgpu_status_string((int)code));
+    set_err(e, (int)code, chunk, (int)page, msg);
+  }
+}
+
+static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
+  clear_err(err);
+  HIPCHECK(hipStreamSynchronize(s), err);
+  if (!b->decoded) return PQ_OK;
+  const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
+  std::vector<uint64_t> keys(nc), vbase(np), rbase(np);
+  std::vector<uint32_t> nn(np), rec(np);
+  uint8_t *A = b->d_arena;
+  if (nc) HIPCHECK(hipMemcpy(keys.data(), A + b->o_err, nc * 8, hipMemcpyDeviceToHost), err);
+  if (np) {
+    HIPCHECK(hipMemcpy(vbase.data(), A + b->o_vbase, np * 8, hipMemcpyDeviceToHost), err);
+    HIPCHECK(hipMemcpy(nn.data(), A + b->o_nn, np * 4, hipMemcpyDeviceToHost), err);
+    HIPCHECK(hipMemcpy(rbase.data(), A + b->o_rbase, np * 8, hipMemcpyDeviceToHost), err);
+    HIPCHECK(hipMemcpy(rec.data(), A + b->o_rec, np * 4, hipMemcpyDeviceToHost), err);
+  }
+  int first = PQ_OK;
+  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    HostChunk &hc = b->chunks[c];
+    clear_err(&hc.dev_err);
+    hc.dev_err.chunk = (int)c;
+    if (!hc.err.code && keys[c] != ~0ull) decode_key(keys[c], (int)c, &hc.dev_err);
+    if (hc.num_pages) {
+      uint32_t lp = hc.first_page + hc.num_pages - 1;
+      hc.nn = (int64_t)(vbase[lp] + nn[lp]);
+      hc.records = (int64_t)(rbase[lp] + rec[lp]);
+    } else {
+      hc.nn = 0;
+      hc.records = 0;
+    }
+    const pqgpu_error &e = hc.err.code ? hc.err : hc.dev_err;
+    if (e.code && !first) {
+      first = e.code;
+      if (err) *err = e;
+    }
+    if (!e.code) {
+      slots += (int64_t)hc.num_slots;
+      values += hc.nn;
+      int w = hc.value_width;
+      out_bytes += w ? hc.nn * w : (hc.nn + 1) * 4 + hc.payload_bytes;
+      if (hc.o_def) out_bytes += (int64_t)hc.num_slots;
+      if (hc.o_rep) out_bytes += (int64_t)hc.num_slots;
+      if (hc.o_valid) out_bytes += (int64_t)(hc.num_slots + 7) / 8;
+      if (hc.o_lists) out_bytes += (hc.records + 1) * 4;
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+        lvl_bytes += b->pages[p].rep_len + b->pages[p].def_len;
+        val_bytes += b->pages[p].val_len;
+      }
+      if (hc.o_def) lvl_bytes += (int64_t)hc.num_slots;
+      if (hc.o_rep) lvl_bytes += (int64_t)hc.num_slots;
+      if (hc.o_valid) lvl_bytes += (int64_t)(hc.num_slots + 7) / 8;
+      val_bytes += w ? hc.nn * w : (hc.nn + 1) * 4;
+    }
+  }
+  b->stats.levels_kernel_bytes = lvl_bytes;
+  b->stats.values_kernel_bytes = val_bytes;
+  b->stats.output_bytes = out_bytes;
+  b->stats.num_slots = slots;
+  b->stats.num_values = values;
+  b->timer.resolve();
+  return first;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int pqgpu_abi_version(void) { return PQGPU_ABI_VERSION; }
+
+const char *pqgpu_status_string(int code) {
+  switch (code) {
+    case PQ_OK: return "ok";
+    case PQ_ERR_EOF: return "EOF";
+    case PQ_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+    case PQ_ERR_INVALID: return "invalid data";
+    case PQ_ERR_UNSUPPORTED: return "unsupported";
+    case PQ_ERR_DICT_INDEX: return "dict: invalid index";
+    case PQ_ERR_CRC: return "CRC32 check failed";
+    case PQ_ERR_DECOMPRESS: return "decompression failed";
+    case PQ_ERR_THRIFT: return "thrift decode error";
+    case PQ_ERR_RANGE: return "int32 out of range";
+    case PQ_ERR_NOMEM: return "out of memory";
+    case PQ_ERR_ARG: return "invalid argument";
+    case PQ_ERR_HIP: return "HIP runtime error";
+  }
+  return "unknown";
+}
+
+int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
+  clear_err(err);
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= device || device < 0) {
+    set_err(err, PQ_ERR_HIP, -1, -1, "no HIP device available for the MI355X decoder");
+    return PQ_ERR_HIP;
+  }
+  HIPCHECK(hipSetDevice(device), err);
+  pqgpu_ctx *c = new pqgpu_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    set_err(err, PQ_ERR_HIP, -1, -1, hipGetErrorString(e));
+    return PQ_ERR_HIP;
+  }
+  *out = c;
+  return PQ_OK;
+}
+
+void pqgpu_ctx_destroy(pqgpu_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int pqgpu_file_open(const uint8_t *buf, size_t len, pqgpu_file **out, pqgpu_error *err) {
+  clear_err(err);
+  *out = nullptr;
+  pqgpu_file *f = new pqgpu_file();
+  Status st = OpenFile(buf, (int64_t)len, &f->meta);
+  if (!st.ok()) {
+    set_err(err, st.code, -1, -1, "reading file meta data failed: " + st.msg);
+    delete f;
+    return st.code;
+  }
+  f->buf = buf;
+  f->len = (int64_t)len;
+  *out = f;
+  return PQ_OK;
+}
+
+void pqgpu_file_close(pqgpu_file *f) { delete f; }
+int pqgpu_file_num_row_groups(const pqgpu_file *f) { return (int)f->meta.row_groups.size(); }
+int pqgpu_file_num_columns(const pqgpu_file *f) { return (int)f->meta.leaves.size(); }
+int64_t pqgpu_file_row_group_num_rows(const pqgpu_file *f, int rg) {
+  if (rg < 0 || rg >= (int)f->meta.row_groups.size()) return -1;
+  return f->meta.row_groups[(size_t)rg].num_rows;
+}
+
+int pqgpu_file_column(const pqgpu_file *f, int col, pqgpu_column_info *out) {
+  if (col < 0 || col >= (int)f->meta.leaves.size()) return PQ_ERR_ARG;
+  const Leaf &l = f->meta.leaves[(size_t)col];
+  memset(out, 0, sizeof(*out));
+  out->physical_type = l.type;
+  out->type_length = l.type_length;
+  out->max_def = l.max_def;
+  out->max_rep = l.max_rep;
+  out->repetition = l.rep;
+  snprintf(out->path, sizeof(out->path), "%s", l.path.c_str());
+  return PQ_OK;
+}
+
+int pqgpu_file_chunk_meta(const pqgpu_file *f, int rg, int col, pqgpu_chunk_meta *out, pqgpu_error *err) {
+  clear_err(err);
+  if (rg < 0 || rg >= (int)f->meta.row_groups.size() || col < 0 || col >= (int)f->meta.leaves.size()) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "row group or column out of range");
+    return PQ_ERR_ARG;
+  }
+  const RowGroup &g = f->meta.row_groups[(size_t)rg];
+  if ((int)g.cols.size() <= col) {  // readRowGroupData chunk_reader.go:383-385
+    set_err(err, PQ_ERR_INVALID, -1, -1, "column index is out of bounds");
+    return PQ_ERR_INVALID;
+  }
+  const ColumnChunkMeta &c = g.cols[(size_t)col];
+  if (!c.has_meta) {
+    set_err(err, PQ_ERR_INVALID, -1, -1, "missing meta data for Column");
+    return PQ_ERR_INVALID;
+  }
+  memset(out, 0, sizeof(*out));
+  out->physical_type = c.type;
+  out->codec = c.codec;
+  out->num_values = c.num_values;
+  out->total_compressed_size = c.total_compressed;
+  out->data_page_offset = c.data_page_offset;
+  out->dictionary_page_offset = c.has_dict_offset ? c.dict_offset : -1;
+  out->has_file_path = c.has_file_path;
+  return PQ_OK;
+}
+
+int pqgpu_batch_create(pqgpu_ctx *ctx, pqgpu_batch **out, pqgpu_error *err) {
+  clear_err(err);
+  // ctx == NULL gives a plan-only batch: page headers are walked and
+  // validated (add_chunk) but upload/decode report PQ_ERR_HIP.
+  pqgpu_batch *b = new pqgpu_batch();
+  b->ctx = ctx;
+  *out = b;
+  return PQ_OK;
+}
+
+static void free_payloads(pqgpu_batch *b) {
+  for (auto &hc : b->chunks)
+    if (hc.payload) { (void)hipFree(hc.payload); hc.payload = nullptr; hc.payload_cap = 0; }
+}
+
+void pqgpu_batch_destroy(pqgpu_batch *b) {
+  if (!b) return;
+  if (!b->ctx) { delete b; return; }
+  (void)hipSetDevice(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  free_payloads(b);
+  if (b->d_arena) (void)hipFree(b->d_arena);
+  if (b->d_stage) (void)hipFree(b->d_stage);
+  if (b->h_pinned) (void)hipHostFree(b->h_pinned);
+  b->timer.destroy();
+  delete b;
+}
+
+int pqgpu_batch_reset(pqgpu_batch *b) {
+  if (b->ctx) {
+    (void)hipStreamSynchronize(b->ctx->stream);
+    free_payloads(b);
+  }
+  b->chunks.clear();
+  b->pages.clear();
+  b->stage.clear();
+  b->uploaded = b->decoded = false;
+  b->stats = pqgpu_batch_stats{};
+  return PQ_OK;
+}
+
+int pqgpu_batch_add_chunk(pqgpu_batch *b, const uint8_t *file_bytes, size_t file_len, const pqgpu_column_info *col,
+                          const pqgpu_chunk_meta *meta, int validate_crc, int32_t *chunk_id, pqgpu_error *err) {
+  if (!b || !file_bytes || !col || !meta) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "null argument");
+    return PQ_ERR_ARG;
+  }
+  return add_chunk_impl(b, file_bytes, (int64_t)file_len, col, meta, validate_crc, chunk_id, err);
+}
+
+int pqgpu_batch_add_file_chunk(pqgpu_batch *b, const pqgpu_file *f, int rg, int col, int validate_crc,
+                               int32_t *chunk_id, pqgpu_error *err) {
+  pqgpu_column_info ci;
+  pqgpu_chunk_meta cm;
+  if (pqgpu_file_column(f, col, &ci)) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "column out of range");
+    return PQ_ERR_ARG;
+  }
+  int e = pqgpu_file_chunk_meta(f, rg, col, &cm, err);
+  if (e) {
+    // still assign a chunk id so the caller can query the error in batch order
+    int32_t id = (int32_t)b->chunks.size();
+    if (chunk_id) *chunk_id = id;
+    b->chunks.emplace_back();
+    HostChunk &hc = b->chunks.back();
+    hc.col = ci;
+    hc.first_page = (uint32_t)b->pages.size();
+    if (err) { err->chunk = id; hc.err = *err; }
+    return e;
+  }
+  return add_chunk_impl(b, f->buf, f->len, &ci, &cm, validate_crc, chunk_id, err);
+}
+
+#define NEED_CTX(b, err)                                                              \
+  do {                                                                                \
+    if (!(b)->ctx) {                                                                  \
+      set_err(err, PQ_ERR_HIP, -1, -1, "plan-only batch: no device context");        \
+      return PQ_ERR_HIP;                                                              \
+    }                                                                                 \
+  } while (0)
+
+static hipStream_t pick_stream(pqgpu_batch *b, void *stream) {
+  return stream ? (hipStream_t)stream : b->ctx->stream;
+}
+
+int pqgpu_batch_upload(pqgpu_batch *b, void *stream, pqgpu_error *err) {
+  clear_err(err);
+  NEED_CTX(b, err);
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  return build_and_upload(b, pick_stream(b, stream), err);
+}
+
+int pqgpu_batch_decode(pqgpu_batch *b, void *stream, pqgpu_error *err) {
+  clear_err(err);
+  NEED_CTX(b, err);
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  return decode_impl(b, pick_stream(b, stream), err);
+}
+
+int pqgpu_batch_sync(pqgpu_batch *b, void *stream, pqgpu_error *err) {
+  if (!b->ctx) {  // plan-only: report the first host-side (readPages) error
+    clear_err(err);
+    for (auto &hc : b->chunks)
+      if (hc.err.code) { if (err) *err = hc.err; return hc.err.code; }
+    return PQ_OK;
+  }
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  return sync_impl(b, pick_stream(b, stream), err);
+}
+
+int pqgpu_batch_num_chunks(const pqgpu_batch *b) { return (int)b->chunks.size(); }
+
+int pqgpu_batch_chunk_status(const pqgpu_batch *b, int32_t id, pqgpu_error *err) {
+  if (id < 0 || id >= (int32_t)b->chunks.size()) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "chunk id out of range");
+    return PQ_ERR_ARG;
+  }
+  const HostChunk &hc = b->chunks[(size_t)id];
+  const pqgpu_error &e = hc.err.code ? hc.err : hc.dev_err;
+  if (err) *err = e;
+  return e.code;
+}
+
+int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_result *out, pqgpu_error *err) {
+  int e = pqgpu_batch_chunk_status(b, id, err);
+  memset(out, 0, sizeof(*out));
+  if (e) return e;
+  const HostChunk &hc = b->chunks[(size_t)id];
+  uint8_t *A = b->d_arena;
+  out->num_slots = (int64_t)hc.num_slots;
+  out->num_values = hc.nn;
+  out->num_records = hc.records;
+  out->payload_bytes = hc.payload_bytes;
+  out->physical_type = hc.col.physical_type;
+  out->value_width = hc.value_width;
+  out->max_def = hc.col.max_def;
+  out->max_rep = hc.col.max_rep;
+  out->values = hc.o_values ? A + hc.o_values : nullptr;
+  out->offsets = hc.o_offsets ? (int32_t *)(A + hc.o_offsets) : nullptr;
+  out->payload = hc.payload;
+  out->def_levels = hc.o_def ? A + hc.o_def : nullptr;
+  out->rep_levels = hc.o_rep ? A + hc.o_rep : nullptr;
+  out->validity = hc.o_valid ? (uint32_t *)(A + hc.o_valid) : nullptr;
+  out->list_offsets = hc.o_lists ? (int32_t *)(A + hc.o_lists) : nullptr;
+  return PQ_OK;
+}
+
+int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32_t *offsets, uint8_t *payload,
+                           uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
+                           pqgpu_error *err) {
+  pqgpu_chunk_result r;
+  int e = pqgpu_batch_chunk_result(b, id, &r, err);
+  if (e) return e;
+  NEED_CTX(b, err);
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  auto cp = [&](void *dst, const void *src, size_t n) -> hipError_t {
+    if (!dst || !src || !n) return hipSuccess;
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
+  };
+  HIPCHECK(cp(values, r.values, (size_t)r.num_values * (size_t)r.value_width), err);
+  HIPCHECK(cp(offsets, r.offsets, r.offsets ? (size_t)(r.num_values + 1) * 4 : 0), err);
+  HIPCHECK(cp(payload, r.payload, (size_t)r.payload_bytes), err);
+  HIPCHECK(cp(def_levels, r.def_levels, (size_t)r.num_slots), err);
+  HIPCHECK(cp(rep_levels, r.rep_levels, (size_t)r.num_slots), err);
+  HIPCHECK(cp(validity, r.validity, (size_t)((r.num_slots + 31) / 32) * 4), err);
+  HIPCHECK(cp(list_offsets, r.list_offsets, r.list_offsets ? (size_t)(r.num_records + 1) * 4 : 0), err);
+  return PQ_OK;
+}
+
+int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out) {
+  *out = b->stats;
+  return PQ_OK;
+}
+
+int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable) {
+  if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
+  b->timer.resolve();
+  b->timer.enabled = enable != 0;
+  for (int k = 0; k < 8; k++) { b->timer.total_ms[k] = 0; b->timer.launches[k] = 0; }
+  return PQ_OK;
+}
+
+int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len) {
+  (void)hipDeviceSynchronize();
+  b->timer.resolve();
+  const KernelTimer &t = b->timer;
+  int best = -1;
+  for (int k = 0; k < 8; k++)
+    if (t.launches[k] && (best < 0 || t.total_ms[k] > t.total_ms[best])) best = k;
+  if (best < 0) {
+    if (avg_ms) *avg_ms = 0;
+    if (launches) *launches = 0;
+    if (name && name_len) name[0] = 0;
+    return PQ_OK;
+  }
+  if (avg_ms) *avg_ms = t.total_ms[best] / (double)t.launches[best];
+  if (launches) *launches = t.launches[best];
+  if (name && name_len) snprintf(name, name_len, "%s", kTimerNames[best]);
+  return PQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// kernels.h — launch interface of the gfx950 decode kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pq_device.h"
+
+namespace pq {
+
+// Device view of one batch; passed by value to every kernel.
+struct BatchDev {
+  const PageDesc *pages;
+  const ChunkDesc *chunks;
+  unsigned long long *chunk_err;  // [nchunks] first-error key (atomicMin), init ~0
+  uint32_t *page_nn;              // [npages] decoded non-null count
+  uint32_t *page_rec;             // [npages] records (rep == 0) per page
+  uint64_t *page_vbase;           // [npages] value base within chunk
+  uint64_t *page_rbase;           // [npages] record base within chunk
+  HybRun *runs;                   // run tables of hybrid value streams
+  const uint64_t *run_base;       // [npages] first entry of each page's run table
+  uint32_t *run_count;            // [npages]
+  uint32_t *tile_first;           // dict tiles: first run index per tile
+  const uint64_t *tile_base;      // [npages] first tile-table entry per page
+  uint32_t *ba_tile_sum;          // BYTE_ARRAY: per 4096-value tile payload sum
+  uint32_t npages, nchunks;
+};
+
+constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
+constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
+constexpr uint32_t kBaTile = 4096;     // values per BYTE_ARRAY scan tile
+
+struct LaunchLists {
+  const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams
+  const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
+  const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
+  const WorkItem *items; uint32_t n_items;               // values work items
+  const uint32_t *dict_ba_chunks; uint32_t n_dict_ba;    // chunks with a BYTE_ARRAY dictionary page
+  const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with BYTE_ARRAY output
+  const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
+};
+
+hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_ba_offsets(const BatchDev &b, const LaunchLists &l, uint64_t *payload_totals_dev, hipStream_t s);
+hipError_t launch_ba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+
+// Names of the kernels, for the timing hook.
+extern const char *kValuesKernelName;
+
+}  // namespace pq

@@ -1,0 +1,131 @@
+// pq_device.h — descriptor tables shared by the host planner and the gfx950
+// kernels. Plain structs (no pointers to host memory); device pointers are
+// stored as uint64_t so the layout is identical on both sides.
+//
+// HBM layout of one batch (see DESIGN.md "Data layout in HBM"):
+//   stage    : every page's (decompressed) payload, each page 16-B aligned,
+//              followed by 64 B of zero padding so unaligned dword reads at a
+//              section end stay in bounds;
+//   pages[]  : PageDesc, one per data page, grouped by chunk;
+//   chunks[] : ChunkDesc, one per column chunk;
+//   outputs  : per chunk values / levels / validity / offsets / payload.
+#pragma once
+#include <stdint.h>
+
+namespace pq {
+
+// parquet.Encoding
+enum : uint8_t {
+  ENC_PLAIN = 0, ENC_PLAIN_DICTIONARY = 2, ENC_RLE = 3, ENC_BIT_PACKED = 4, ENC_DELTA_BINARY_PACKED = 5,
+  ENC_DELTA_LENGTH_BYTE_ARRAY = 6, ENC_DELTA_BYTE_ARRAY = 7, ENC_RLE_DICTIONARY = 8,
+};
+// parquet.Type
+enum : int32_t { T_BOOLEAN = 0, T_INT32 = 1, T_INT64 = 2, T_INT96 = 3, T_FLOAT = 4, T_DOUBLE = 5,
+                 T_BYTE_ARRAY = 6, T_FLBA = 7 };
+
+// Value-decoder kind chosen by getValuesDecoder (chunk_reader.go:106-159).
+enum : uint8_t {
+  VK_PLAIN_FIXED = 0,  // INT32/INT64/FLOAT/DOUBLE/FLBA PLAIN: byte copy
+  VK_PLAIN_INT96 = 1,  // INT96 PLAIN (12-B copy)
+  VK_PLAIN_BOOL = 2,   // BOOLEAN PLAIN: LSB-first bits -> 1 B per value
+  VK_RLE_BOOL = 3,     // BOOLEAN RLE: hybrid bw=1
+  VK_DICT = 4,         // RLE_DICTIONARY / PLAIN_DICTIONARY: hybrid indices -> gather
+  VK_DELTA32 = 5,      // DELTA_BINARY_PACKED INT32
+  VK_DELTA64 = 6,      // DELTA_BINARY_PACKED INT64
+  VK_PLAIN_BA = 7,     // BYTE_ARRAY PLAIN (length-prefixed)
+};
+
+// Page flags
+enum : uint16_t {
+  PF_REP = 1,        // rep stream present (V1 with maxR>0, or V2 rep length > 0)
+  PF_DEF = 2,        // def stream present
+  PF_V2 = 4,
+  PF_BASE_KNOWN = 8, // value_base computed on host (required column or V2 num_nulls)
+  PF_DELTA_SLOW = 16,// DELTA page whose miniblock size is not a multiple of 8: exact scalar path
+};
+
+// Error staging key (64 bit, smaller = reported first):
+//   [63:62] phase   0 = readPages (chunk-level, e.g. dictionary decode), 1 = readValues
+//   [61:40] page    data-page index within chunk (0 for phase 0)
+//   [39:36] stage   0 = dictionary, 1 = rep levels, 2 = def levels, 3 = values
+//   [35:4]  pos     value / slot position within the stage
+//   [3:0]   code    pqgpu_status error class
+__host__ __device__ inline uint64_t err_key(uint32_t phase, uint32_t page, uint32_t stage, uint32_t pos,
+                                            uint32_t code) {
+  return ((uint64_t)(phase & 3) << 62) | ((uint64_t)(page & 0x3fffff) << 40) | ((uint64_t)(stage & 15) << 36) |
+         ((uint64_t)pos << 4) | (uint64_t)(code & 15);
+}
+enum : uint32_t { ST_DICT = 0, ST_REP = 1, ST_DEF = 2, ST_VALUES = 3 };
+
+struct PageDesc {        // 96 B
+  uint64_t data;         // device address of the page payload (decompressed)
+  uint32_t rep_off, rep_len;  // hybrid streams, relative to data (no length prefix)
+  uint32_t def_off, def_len;
+  uint32_t val_off, val_len;  // values section (dict: after the bit-width byte)
+  uint32_t num_slots;    // DataPageHeader(V2).num_values
+  uint32_t chunk;        // owning chunk index
+  uint32_t page_in_chunk;
+  uint16_t flags;
+  uint8_t vkind;         // VK_*
+  uint8_t dict_bw;       // VK_DICT: index bit width (0..32); VK_RLE_BOOL: 1
+  uint64_t slot_base;    // first level slot of this page within its chunk
+  uint64_t value_base;   // first non-null value index within its chunk
+  uint32_t expect_nn;    // non-null count the host expects (PF_BASE_KNOWN), else 0
+  uint32_t delta_first_mb; // DELTA: offset (rel. to data) of the first miniblock header
+  int64_t delta_first;   // DELTA: first value from the block header
+  int32_t delta_count;   // DELTA: valuesCount from the block header
+  uint16_t delta_mbc;    // DELTA: miniblocks per block
+  uint16_t pad0;
+  uint32_t delta_mbvc;   // DELTA: values per miniblock
+  uint32_t pad1;
+};
+
+struct ChunkDesc {       // 192 B
+  int32_t type, type_length, max_def, max_rep;
+  int32_t def_bw, rep_bw, value_width, flags;
+  uint32_t first_page, num_pages;
+  uint64_t num_slots;
+  uint64_t nn_capacity;  // values buffer capacity (values)
+  // dictionary (decoded on device into an aligned buffer)
+  uint64_t dict_raw;     // device address of the dictionary page payload
+  uint32_t dict_raw_len, dict_count;
+  uint64_t dict_values;  // aligned fixed-width values, or BYTE_ARRAY payload (== dict_raw + 4 offsets)
+  uint64_t dict_offsets; // BYTE_ARRAY: int32[dict_count+1] positions of each entry's bytes in dict_raw
+  // outputs
+  uint64_t values;       // fixed width
+  uint64_t def_levels;   // uint8 or 0
+  uint64_t rep_levels;   // uint8 or 0
+  uint64_t validity;     // uint32 words or 0
+  uint64_t offsets;      // BYTE_ARRAY int32[nn+1]
+  uint64_t payload;      // BYTE_ARRAY bytes
+  uint64_t list_offsets; // int32[records+1]
+  uint64_t ba_index;     // scratch: int32 dictionary index per value (BYTE_ARRAY dict)
+  uint64_t payload_capacity;
+  uint64_t page_nn;      // device uint32[num_pages]: decoded non-null counts
+  uint64_t page_rec;     // device uint32[num_pages]: records (rep==0) per page
+  uint64_t page_vbase;   // device uint64[num_pages]: value bases (copied from / checked against PageDesc)
+  uint64_t page_rbase;   // device uint64[num_pages]: record bases
+  uint64_t pad[2];
+};
+
+// Chunk flags
+enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8 };
+
+// Work items of the values kernel.
+enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5 };
+struct WorkItem {        // 16 B
+  uint32_t page;         // global page index
+  uint32_t v0;           // first value (within page) of this tile
+  uint32_t v1;           // end value bound (clamped to the decoded NN in kernel)
+  uint8_t kind;
+  uint8_t pad[3];
+};
+
+// Hybrid run table entry written by the scan kernel for dictionary-index streams.
+struct HybRun {          // 12 B
+  uint32_t value_start;  // index of the run's first value within the stream
+  uint32_t payload_off;  // byte offset of the run payload (after the header) within the stream
+  uint32_t info;         // bit 31: bit-packed; bits 0..30: RLE value (bit-packed: 0)
+};
+
+}  // namespace pq

@@ -1,0 +1,398 @@
+"""pqgpu — Python mirror of parquet-go's read path over the MI355X decoder.
+
+Binds the C ABI in include/pqgpu.h (libpqgpu.so, built in-tree by
+`make -C parquet-go-1_amd`) with ctypes and mirrors the reference's reader
+interface for the decode path:
+
+    reference (Go, package goparquet)              here
+    ------------------------------------------    ---------------------------------
+    NewFileReader(r, columns...)  file_reader.go:154   NewFileReader(data, *columns)
+    FileReader.NumRowGroups / NumRows                  FileReader.NumRowGroups / NumRows
+    FileReader.readRowGroupData  chunk_reader.go:375   FileReader.ReadRowGroupData(rg)
+    readChunk + pageReader.readValues (every page)     -> ColumnData per selected leaf
+    ColumnStore dLevels / rLevels packedArray          ColumnData.dLevels / rLevels
+    []interface{} values (non-null only)               ColumnData.values (ndarray / list of bytes)
+
+Errors are raised as DecodeError carrying the reference's error class
+(io.EOF, io.ErrUnexpectedEOF, ...) and the failing page, like
+readValues' "read values from page failed" wrapping (page_v1.go:57).
+
+There is no CPU fallback: every decode runs on the GPU; without a GPU (or
+without libpqgpu.so) the constructors raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "lib", "libpqgpu.so")
+
+# Error classes (include/pqgpu.h)
+PQ_OK, PQ_ERR_EOF, PQ_ERR_UNEXPECTED_EOF, PQ_ERR_INVALID, PQ_ERR_UNSUPPORTED, PQ_ERR_DICT_INDEX = 0, 1, 2, 3, 4, 5
+PQ_ERR_CRC, PQ_ERR_DECOMPRESS, PQ_ERR_THRIFT, PQ_ERR_RANGE, PQ_ERR_NOMEM, PQ_ERR_ARG, PQ_ERR_HIP = 6, 7, 8, 9, 10, 11, 12
+ERROR_NAMES = {0: "ok", 1: "io.EOF", 2: "io.ErrUnexpectedEOF", 3: "invalid", 4: "unsupported", 5: "dict index",
+               6: "crc", 7: "decompress", 8: "thrift", 9: "range", 10: "nomem", 11: "arg", 12: "hip"}
+
+# parquet.Type
+BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
+_DTYPES = {BOOLEAN: np.uint8, INT32: np.int32, INT64: np.int64, FLOAT: np.uint32, DOUBLE: np.uint64}
+
+
+class Error(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("chunk", ctypes.c_int32), ("page", ctypes.c_int32),
+                ("msg", ctypes.c_char * 244)]
+
+
+class ColumnInfo(ctypes.Structure):
+    _fields_ = [("physical_type", ctypes.c_int32), ("type_length", ctypes.c_int32), ("max_def", ctypes.c_int32),
+                ("max_rep", ctypes.c_int32), ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 236)]
+
+
+class ChunkMeta(ctypes.Structure):
+    _fields_ = [("physical_type", ctypes.c_int32), ("codec", ctypes.c_int32), ("num_values", ctypes.c_int64),
+                ("total_compressed_size", ctypes.c_int64), ("data_page_offset", ctypes.c_int64),
+                ("dictionary_page_offset", ctypes.c_int64), ("has_file_path", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+class ChunkResult(ctypes.Structure):
+    _fields_ = [("num_slots", ctypes.c_int64), ("num_values", ctypes.c_int64), ("num_records", ctypes.c_int64),
+                ("payload_bytes", ctypes.c_int64), ("physical_type", ctypes.c_int32),
+                ("value_width", ctypes.c_int32), ("max_def", ctypes.c_int32), ("max_rep", ctypes.c_int32),
+                ("values", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("payload", ctypes.c_void_p),
+                ("def_levels", ctypes.c_void_p), ("rep_levels", ctypes.c_void_p), ("validity", ctypes.c_void_p),
+                ("list_offsets", ctypes.c_void_p)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("num_chunks", ctypes.c_int64), ("num_pages", ctypes.c_int64), ("num_slots", ctypes.c_int64),
+                ("num_values", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
+                ("staged_bytes", ctypes.c_int64), ("host_plan_ms", ctypes.c_double),
+                ("host_decompress_ms", ctypes.c_double), ("levels_kernel_bytes", ctypes.c_int64),
+                ("values_kernel_bytes", ctypes.c_int64)]
+
+
+_LIB = None
+_EXPORTS = [
+    "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
+    "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
+    "pqgpu_file_column", "pqgpu_file_chunk_meta", "pqgpu_batch_create", "pqgpu_batch_destroy", "pqgpu_batch_reset",
+    "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
+    "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
+    "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
+]
+
+
+def lib():
+    """Load libpqgpu.so (raises if it was not built: there is no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libpqgpu.so not built at {LIB_PATH}: run `make -C {_PKG}` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, E = ctypes.c_void_p, ctypes.POINTER(Error)
+    sig = {
+        "pqgpu_abi_version": ([], ctypes.c_int),
+        "pqgpu_status_string": ([ctypes.c_int], ctypes.c_char_p),
+        "pqgpu_ctx_create": ([ctypes.c_int, ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_ctx_destroy": ([P], None),
+        "pqgpu_file_open": ([P, ctypes.c_size_t, ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_file_close": ([P], None),
+        "pqgpu_file_num_row_groups": ([P], ctypes.c_int),
+        "pqgpu_file_num_columns": ([P], ctypes.c_int),
+        "pqgpu_file_row_group_num_rows": ([P, ctypes.c_int], ctypes.c_int64),
+        "pqgpu_file_column": ([P, ctypes.c_int, ctypes.POINTER(ColumnInfo)], ctypes.c_int),
+        "pqgpu_file_chunk_meta": ([P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ChunkMeta), E], ctypes.c_int),
+        "pqgpu_batch_create": ([P, ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_batch_destroy": ([P], None),
+        "pqgpu_batch_reset": ([P], ctypes.c_int),
+        "pqgpu_batch_add_chunk": ([P, P, ctypes.c_size_t, ctypes.POINTER(ColumnInfo), ctypes.POINTER(ChunkMeta),
+                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
+        "pqgpu_batch_add_file_chunk": ([P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
+        "pqgpu_batch_upload": ([P, P, E], ctypes.c_int),
+        "pqgpu_batch_decode": ([P, P, E], ctypes.c_int),
+        "pqgpu_batch_sync": ([P, P, E], ctypes.c_int),
+        "pqgpu_batch_num_chunks": ([P], ctypes.c_int),
+        "pqgpu_batch_chunk_status": ([P, ctypes.c_int32, E], ctypes.c_int),
+        "pqgpu_batch_chunk_result": ([P, ctypes.c_int32, ctypes.POINTER(ChunkResult), E], ctypes.c_int),
+        "pqgpu_batch_copy_chunk": ([P, ctypes.c_int32, P, P, P, P, P, P, P, E], ctypes.c_int),
+        "pqgpu_batch_stats_get": ([P, ctypes.POINTER(BatchStats)], ctypes.c_int),
+        "pqgpu_batch_kernel_timing": ([P, ctypes.c_int], ctypes.c_int),
+        "pqgpu_batch_kernel_time": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+class DecodeError(Exception):
+    """A reader error with the reference's error class (see ERROR_NAMES)."""
+
+    def __init__(self, err):
+        self.code = int(err.code)
+        self.chunk = int(err.chunk)
+        self.page = int(err.page)
+        self.msg = err.msg.decode(errors="replace")
+        super().__init__(f"[{ERROR_NAMES.get(self.code, self.code)}] chunk {self.chunk} page {self.page}: {self.msg}")
+
+
+def _check(rc, err):
+    if rc:
+        raise DecodeError(err)
+
+
+class Context:
+    """One MI355X device (pqgpu_ctx). HIP device visibility follows HIP_VISIBLE_DEVICES."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_ctx_create(device, ctypes.byref(self._h), ctypes.byref(err)), err)
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().pqgpu_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class File:
+    """Parsed footer + schema (ReadFileMetaData + makeSchema). Keeps `data` alive."""
+
+    def __init__(self, data):
+        self.data = bytes(data)
+        self._buf = ctypes.create_string_buffer(self.data, len(self.data))
+        self._h = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_file_open(ctypes.addressof(self._buf), len(self.data), ctypes.byref(self._h),
+                                     ctypes.byref(err)), err)
+
+    def close(self):
+        if self._h:
+            lib().pqgpu_file_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_row_groups(self):
+        return lib().pqgpu_file_num_row_groups(self._h)
+
+    @property
+    def num_columns(self):
+        return lib().pqgpu_file_num_columns(self._h)
+
+    def row_group_num_rows(self, rg):
+        return lib().pqgpu_file_row_group_num_rows(self._h, rg)
+
+    def column(self, col):
+        ci = ColumnInfo()
+        if lib().pqgpu_file_column(self._h, col, ctypes.byref(ci)):
+            raise IndexError(col)
+        return ci
+
+    def column_paths(self):
+        return [self.column(i).path.decode() for i in range(self.num_columns)]
+
+
+class ColumnData:
+    """One decoded column chunk, in the reference's terms plus Arrow-style extras."""
+
+    def __init__(self, info, res, values, offsets, payload, dlev, rlev, validity, lists):
+        self.path = info.path.decode()
+        self.physical_type = info.physical_type
+        self.max_def, self.max_rep = info.max_def, info.max_rep
+        self.num_slots, self.num_values, self.num_records = res.num_slots, res.num_values, res.num_records
+        self.values_raw = values     # fixed width: ndarray (INT96: (n,12) uint8)
+        self.offsets = offsets       # BYTE_ARRAY: int32[n+1]
+        self.payload = payload       # BYTE_ARRAY: bytes
+        self.validity = validity     # uint32 words or None
+        self.list_offsets = lists    # int32[records+1] or None
+        n = self.num_slots
+        if dlev is not None:
+            self.dLevels = dlev.astype(np.int32)
+        elif self.max_def == 1:      # validity bits ARE the def levels when maxD == 1
+            self.dLevels = self.validity_bits().astype(np.int32)
+        else:
+            self.dLevels = np.zeros(n, np.int32)
+        self.rLevels = rlev.astype(np.int32) if rlev is not None else np.zeros(n, np.int32)
+
+    def validity_bits(self):
+        if self.validity is None:
+            return np.ones(self.num_slots, np.uint8)
+        b = np.unpackbits(self.validity.view(np.uint8), bitorder="little")
+        return b[: self.num_slots]
+
+    @property
+    def values(self):
+        """Non-null values in order; byte arrays as a list of bytes."""
+        if self.offsets is not None:
+            o = self.offsets
+            return [self.payload[o[i]:o[i + 1]] for i in range(self.num_values)]
+        return self.values_raw
+
+
+class Batch:
+    """pqgpu_batch: chunks decoded together with one set of kernel launches."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_batch_create(ctx._h if ctx is not None else None, ctypes.byref(self._h),
+                                        ctypes.byref(err)), err)
+        self._files = []
+        self._infos = []
+
+    def close(self):
+        if self._h:
+            lib().pqgpu_batch_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        lib().pqgpu_batch_reset(self._h)
+        self._files, self._infos = [], []
+
+    def add_file_chunk(self, f, rg, col, validate_crc=False):
+        """readRowGroupData for one (row group, column). Returns (chunk_id, error or None)."""
+        cid = ctypes.c_int32(-1)
+        err = Error()
+        rc = lib().pqgpu_batch_add_file_chunk(self._h, f._h, rg, col, int(validate_crc), ctypes.byref(cid),
+                                              ctypes.byref(err))
+        self._files.append(f)
+        self._infos.append(f.column(col))
+        return cid.value, (DecodeError(err) if rc else None)
+
+    def upload(self):
+        err = Error()
+        _check(lib().pqgpu_batch_upload(self._h, None, ctypes.byref(err)), err)
+
+    def decode(self):
+        err = Error()
+        _check(lib().pqgpu_batch_decode(self._h, None, ctypes.byref(err)), err)
+
+    def sync(self):
+        """Wait; returns the first error (DecodeError) or None."""
+        err = Error()
+        rc = lib().pqgpu_batch_sync(self._h, None, ctypes.byref(err))
+        return DecodeError(err) if rc else None
+
+    def status(self, cid):
+        err = Error()
+        rc = lib().pqgpu_batch_chunk_status(self._h, cid, ctypes.byref(err))
+        return DecodeError(err) if rc else None
+
+    def stats(self):
+        s = BatchStats()
+        lib().pqgpu_batch_stats_get(self._h, ctypes.byref(s))
+        return s
+
+    def kernel_timing(self, enable=True):
+        lib().pqgpu_batch_kernel_timing(self._h, int(enable))
+
+    def kernel_time(self):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        name = ctypes.create_string_buffer(64)
+        lib().pqgpu_batch_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n), name, 64)
+        return ms.value, n.value, name.value.decode()
+
+    def result(self, cid, copy=True):
+        """ColumnData for chunk `cid` (raises DecodeError if that chunk failed)."""
+        err = Error()
+        r = ChunkResult()
+        _check(lib().pqgpu_batch_chunk_result(self._h, cid, ctypes.byref(r), ctypes.byref(err)), err)
+        if not copy:
+            return r
+        info = self._infos[cid]
+        ns, nv = r.num_slots, r.num_values
+        t = r.physical_type
+        vals = offs = pay = dl = rl = valid = lists = None
+        if r.value_width:
+            if t == INT96 or (t == FIXED_LEN_BYTE_ARRAY):
+                vals = np.zeros((nv, r.value_width), np.uint8)
+            else:
+                vals = np.zeros(nv, _DTYPES[t])
+        else:
+            offs = np.zeros(nv + 1, np.int32)
+            pay = np.zeros(max(r.payload_bytes, 1), np.uint8)
+        if r.def_levels:
+            dl = np.zeros(ns, np.uint8)
+        if r.rep_levels:
+            rl = np.zeros(ns, np.uint8)
+        if r.validity:
+            valid = np.zeros((ns + 31) // 32, np.uint32)
+        if r.list_offsets:
+            lists = np.zeros(r.num_records + 1, np.int32)
+
+        def ptr(a):
+            return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+        _check(lib().pqgpu_batch_copy_chunk(self._h, cid, ptr(vals), ptr(offs), ptr(pay), ptr(dl), ptr(rl),
+                                            ptr(valid), ptr(lists), ctypes.byref(err)), err)
+        payload = pay[: r.payload_bytes].tobytes() if pay is not None else None
+        return ColumnData(info, r, vals, offs, payload, dl, rl, valid, lists)
+
+
+class FileReader:
+    """Mirror of goparquet.FileReader for the decode path (file_reader.go)."""
+
+    def __init__(self, data, *columns, ctx=None, validate_crc=False):
+        self.file = File(data)
+        self.ctx = ctx or Context(0)
+        self.validate_crc = validate_crc
+        paths = self.file.column_paths()
+        self.selected = [i for i, p in enumerate(paths) if not columns or p in columns or p.split(".")[0] in columns]
+        self.rowGroupPosition = 0
+
+    def NumRowGroups(self):
+        return self.file.num_row_groups
+
+    def NumRows(self):
+        return sum(self.file.row_group_num_rows(i) for i in range(self.file.num_row_groups))
+
+    def ReadRowGroupData(self, rg):
+        """readRowGroupData (chunk_reader.go:375-404): decode every selected column chunk of row group rg.
+        Returns {path: ColumnData}; raises DecodeError with the first error in column order."""
+        b = Batch(self.ctx)
+        try:
+            ids = []
+            for c in self.selected:
+                cid, e = b.add_file_chunk(self.file, rg, c, self.validate_crc)
+                if e is not None:
+                    raise e
+                ids.append((c, cid))
+            b.decode()
+            e = b.sync()
+            if e is not None:
+                raise e
+            return {self.file.column(c).path.decode(): b.result(cid) for c, cid in ids}
+        finally:
+            b.close()
+
+
+def NewFileReader(data, *columns, **kw):
+    return FileReader(data, *columns, **kw)

@@ -1,0 +1,26 @@
+"""Test configuration: markers and import paths.
+
+`-m "not gpu"` runs everywhere (oracle vs golden vectors, host planning,
+C-ABI symbols); `-m gpu` needs an MI355X and exercises the HIP kernels
+through the C ABI.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "parquet-go-1_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950) and the built libpqgpu.so")
+    config.addinivalue_line("markers", "slow: larger inputs (still seconds)")
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import pqgpu
+    return pqgpu.Context(0)

@@ -1,0 +1,80 @@
+"""GPU parity: every fixture decoded by the MI355X kernels (through the C ABI)
+must equal the CPU oracle bit for bit — values, def/rep levels, validity,
+byte-array offsets and payload, record offsets — and fail with the same
+error class on the same page where the reference fails."""
+import numpy as np
+import pytest
+
+import pqgpu
+import pqtest
+import py_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_decode(ctx, data):
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(ctx)
+    ids = {}
+    host_err = {}
+    for rg in range(f.num_row_groups):
+        for col in range(f.num_columns):
+            cid, e = b.add_file_chunk(f, rg, col)
+            ids[(rg, col)] = cid
+            host_err[(rg, col)] = e
+    b.decode()
+    b.sync()
+    out = {}
+    for k, cid in ids.items():
+        e = b.status(cid)
+        out[k] = e if e is not None else b.result(cid)
+    b.close()
+    return out
+
+
+@pytest.mark.parametrize("name", pqtest.ALL)
+def test_fixture_parity(gpu_ctx, name):
+    data = pqtest.load(name)
+    try:
+        orc = pqtest.oracle_decode(data)
+    except O.OracleError:
+        pytest.skip("footer-level error: covered by CPU tests")
+    gpu = _gpu_decode(gpu_ctx, data)
+    for rg, col, r in orc:
+        g = gpu[(rg, col)]
+        where = f"{name} rg{rg} col{col}"
+        if isinstance(r, O.OracleError):
+            assert isinstance(g, pqgpu.DecodeError), f"{where}: oracle error {r} but GPU decoded"
+            assert (g.code, g.page) == (r.code, r.page), f"{where}: {g} vs {r}"
+        else:
+            assert not isinstance(g, pqgpu.DecodeError), f"{where}: GPU error {g}"
+            pqtest.assert_chunk_equal(g, r, where)
+
+
+@pytest.mark.parametrize("name,expected", sorted(pqtest.EXPECTED_ERRORS.items()))
+def test_expected_errors(gpu_ctx, name, expected):
+    gpu = _gpu_decode(gpu_ctx, pqtest.load(name))
+    errs = [v for k, v in sorted(gpu.items()) if isinstance(v, pqgpu.DecodeError)]
+    assert errs and (errs[0].code, errs[0].page) == expected, (name, errs[:1])
+
+
+def test_must_not_crash_gpu(gpu_ctx):
+    import os
+    d = os.path.join(pqtest.GOLDEN, "must_not_crash")
+    for fn in sorted(os.listdir(d)):
+        data = open(os.path.join(d, fn), "rb").read()
+        try:
+            _gpu_decode(gpu_ctx, data)
+        except pqgpu.DecodeError:
+            pass
+
+
+def test_file_reader_mirror(gpu_ctx):
+    """FileReader.ReadRowGroupData mirrors readRowGroupData for the selected columns."""
+    data = pqtest.load("cfg2_v2_small")
+    r = pqgpu.NewFileReader(data, "a", ctx=gpu_ctx)
+    assert r.NumRowGroups() == 2
+    cols = r.ReadRowGroupData(1)
+    assert list(cols) == ["a"]
+    orc = O.File(data).read_chunk(1, 0)
+    pqtest.assert_chunk_equal(cols["a"], orc, "reader")
