@@ -540,6 +540,8 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       if ((e = init_values(block.data(), (int64_t)block.size(), levels, vk, &pd, &msg)))
         return chunk_fail(b, hc, id, e, pi, msg, err);
     }
+    if (hc.num_slots + pd.num_slots > 0x7fffffffULL)
+      return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "more than 2^31-1 level slots in one chunk", err);
     pd.vkind = vk;
     pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
     pd.slot_base = hc.num_slots;
@@ -572,7 +574,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->run_total = b->tile_total = 0;
   b->ba_tiles_total = 0;
   b->ba_max_tiles = 0;
-  uint64_t a = 0;
+  uint64_t a = 256;  // offset 0 is reserved: a zero offset means "not allocated"
   auto take = [&](uint64_t bytes) {
     uint64_t o = align_up(a, 256);
     a = o + align_up(std::max<uint64_t>(bytes, 1), 16);
@@ -841,12 +843,15 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                                              b->ba_max_tiles, (uint64_t *)(A + b->o_ba_totals), s);
              }),
              err);
-    std::vector<uint64_t> totals(b->ba_chunks.size());
+    std::vector<uint64_t> totals(b->ba_chunks.size()), keys(nc);
     HIPCHECK(hipMemcpyAsync(totals.data(), A + b->o_ba_totals, totals.size() * 8, hipMemcpyDeviceToHost, s), err);
+    HIPCHECK(hipMemcpyAsync(keys.data(), A + b->o_err, (size_t)nc * 8, hipMemcpyDeviceToHost, s), err);
     HIPCHECK(hipStreamSynchronize(s), err);
     bool changed = false;
+    std::vector<uint32_t> gather;  // chunks without a decode error: their lengths and sources are all set
     for (size_t k = 0; k < b->ba_chunks.size(); k++) {
       HostChunk &hc = b->chunks[b->ba_chunks[k]];
+      if (keys[b->ba_chunks[k]] != ~0ull) continue;
       if (totals[k] > 0x7fffffffULL) {
         set_err(&hc.err, PQ_ERR_UNSUPPORTED, (int)b->ba_chunks[k], -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
         continue;
@@ -861,6 +866,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
       b->chunk_desc[b->ba_chunks[k]].payload = (uint64_t)hc.payload;
       changed = true;
+      gather.push_back(b->ba_chunks[k]);
     }
     if (changed) {
       for (uint32_t c : b->ba_chunks)
@@ -869,10 +875,17 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                  err);
     }
     uint64_t maxnn = 0;
-    for (uint32_t c : b->ba_chunks) maxnn = std::max<uint64_t>(maxnn, b->chunks[c].num_slots);
+    for (uint32_t c : gather) maxnn = std::max<uint64_t>(maxnn, b->chunks[c].num_slots);
     uint32_t gx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((maxnn + 255) / 256, 1), 4096);
-    HIPCHECK(timed(b, 6, s, [&] { return launch_ba_gather_impl(d, l.ba_chunks, l.n_ba_chunks, gx, s); }), err);
-    if (changed) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc host copies stay valid until here
+    if (!gather.empty()) {
+      // the offsets kernels are done with the BYTE_ARRAY list: reuse its slot for the gather list
+      HIPCHECK(hipMemcpyAsync(A + b->l_ba, gather.data(), gather.size() * 4, hipMemcpyHostToDevice, s), err);
+      HIPCHECK(timed(b, 6, s, [&] {
+                 return launch_ba_gather_impl(d, (const uint32_t *)(A + b->l_ba), (uint32_t)gather.size(), gx, s);
+               }),
+               err);
+    }
+    HIPCHECK(hipStreamSynchronize(s), err);  // host vectors above stay valid until here
   }
   HIPCHECK(timed(b, 7, s, [&] { return launch_records(d, l, s); }), err);
   b->decoded = true;

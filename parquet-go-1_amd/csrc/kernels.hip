@@ -787,14 +787,17 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     uint64_t sum = 0;
     uint32_t gerr = 0, gerr_pos = 0;
     bool valid = bi < nb && d0 < stop;
+    uint32_t goff = 0, wbits = 0;
     if (valid) {
       uint32_t inb = (g % gpb) * 8;
       uint32_t m = inb / mbvc, o = inb % mbvc;
-      uint32_t wbits = L.mb_w[bi][m];
-      uint32_t goff = L.mb_off[bi][m] + (o / 8) * wbits;  // group byte offset
+      wbits = L.mb_w[bi][m];
+      goff = L.mb_off[bi][m] + (o / 8) * wbits;  // group byte offset
       // io.ReadFull(w bytes) of the group
       if (wbits > 0 && goff >= n) { gerr = PQ_ERR_EOF; gerr_pos = d0; }
-      else if (goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
+      else if ((uint64_t)goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
+    }
+    if (valid && !gerr) {
       uint64_t md = (uint64_t)L.min_delta[bi];
 #pragma unroll
       for (int j = 0; j < 8; j++) {

@@ -12,4 +12,7 @@ for step in "$@"; do
   echo "=== $name rc=$rc"
   tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  if grep -qiE "illegal memory access|memory access fault|hipErrorLaunchFailure|HSA_STATUS_ERROR|core dumped" "gpurun_out/$name.log"; then
+    echo "stopping after $name: GPU fault reported"; exit 3
+  fi
 done
