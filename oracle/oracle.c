@@ -1468,7 +1468,7 @@ int or_read_chunk(const or_file *f, int rg, int col, int validate_crc, or_chunk_
   const leaf_col *c = &f->leaves[col];
   out->value_width = (c->physical_type == T_BYTE_ARRAY || c->physical_type == T_FLBA) ? 0 : fixed_width(c->physical_type);
   int e = OR_OK;
-  page_t *pages = NULL;
+  page_t **pages = NULL; /* individually allocated: decoders keep pointers into their page */
   int npages = 0, cap = 0;
   dict_t dict = {0};
   int64_t *dict_offs = NULL;
@@ -1567,12 +1567,13 @@ int or_read_chunk(const or_file *f, int rg, int col, int validate_crc, or_chunk_
     if (ph.type != 0 && ph.type != 3) FAIL(OR_ERR_UNSUPPORTED, -1, "DATA_PAGE or DATA_PAGE_V2 type supported");
     if (npages == cap) {
       cap = cap ? cap * 2 : 16;
-      page_t *np = (page_t *)realloc(pages, sizeof(page_t) * (size_t)cap);
+      page_t **np = (page_t **)realloc(pages, sizeof(page_t *) * (size_t)cap);
       if (!np) FAIL(OR_ERR_NOMEM, -1, "nomem");
       pages = np;
     }
-    page_t *p = &pages[npages];
-    memset(p, 0, sizeof(*p));
+    page_t *p = (page_t *)calloc(1, sizeof(page_t));
+    if (!p) FAIL(OR_ERR_NOMEM, -1, "nomem");
+    pages[npages] = p;
     p->vd.col = c;
     p->vd.dict = &dict;
     npages++;
@@ -1642,7 +1643,7 @@ int or_read_chunk(const or_file *f, int rg, int col, int validate_crc, or_chunk_
   }
   /* readPageData + ColumnStore.get -> readNextPage, every page in order */
   for (int i = 0; i < npages; i++) {
-    if ((e = page_read_values(&pages[i], c, &a))) {
+    if ((e = page_read_values(pages[i], c, &a))) {
       out->err_page = i;
       snprintf(out->err_msg, sizeof(out->err_msg), "read values from page failed");
       goto done;
@@ -1650,7 +1651,7 @@ int or_read_chunk(const or_file *f, int rg, int col, int validate_crc, or_chunk_
   }
 done:
 #undef FAIL
-  for (int i = 0; i < npages; i++) page_free(&pages[i]);
+  for (int i = 0; i < npages; i++) { page_free(pages[i]); free(pages[i]); }
   free(pages);
   free(dict_offs);
   free(dacc.vals); free(dacc.offs); free(dacc.def); free(dacc.rep);

@@ -86,7 +86,13 @@ def assert_chunk_equal(gpu, orc, where=""):
     if gpu.max_def > 0:
         np.testing.assert_array_equal(gpu.validity_bits(), (orc.def_levels == gpu.max_def).astype(np.uint8),
                                       err_msg=f"{where}: validity")
-    if orc.offsets is not None:
+    if orc.offsets is not None and gpu.offsets is None:
+        # FIXED_LEN_BYTE_ARRAY: the oracle keeps the reference's []byte values, the GPU a fixed-width array
+        g = np.asarray(gpu.values_raw)
+        w = g.shape[1] if g.ndim == 2 else 0
+        assert np.all(np.diff(orc.offsets) == w), f"{where}: FLBA lengths"
+        assert g.tobytes() == orc.values, f"{where}: FLBA bytes differ"
+    elif orc.offsets is not None:
         assert gpu.offsets is not None, where
         np.testing.assert_array_equal(gpu.offsets.astype(np.int64), orc.offsets, err_msg=f"{where}: offsets")
         assert gpu.payload == orc.values, f"{where}: payload differs"
