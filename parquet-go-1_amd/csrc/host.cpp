@@ -263,6 +263,7 @@ struct pqgpu_batch {
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
+  uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   std::vector<ChunkDesc> chunk_desc;
   bool uploaded = false, decoded = false;
   pqgpu_batch_stats stats{};
@@ -390,7 +391,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     pd->delta_mbc = (uint16_t)std::min<int32_t>(mbc, 65535);
     pd->delta_mbvc = (uint32_t)mbvc;
     pd->delta_first_mb = (uint32_t)(vstart + mb_start);
-    if (mbvc % 8 != 0 || (int64_t)bs / 8 > 256 || mbc > 64) pd->flags |= PF_DELTA_SLOW;
+    if (mbvc % 8 != 0 || bs > 1024 || mbc > 64) pd->flags |= PF_DELTA_SLOW;
     if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
     return PQ_OK;
   }
@@ -581,6 +582,15 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     return o;
   };
   int64_t in_bytes = 0;
+  // Region zeroed before every decode: all validity bitmaps, then per-page record/run counters.
+  b->z_begin = align_up(a, 256);
+  for (uint32_t c = 0; c < nc; c++) {
+    HostChunk &hc = b->chunks[c];
+    hc.o_valid = (!hc.err.code && hc.col.max_def > 0) ? take(((hc.num_slots + 31) / 32 + 2) * 4) : 0;
+  }
+  b->o_rec = take((uint64_t)np * 4);
+  b->o_run_count = take((uint64_t)np * 4);
+  b->z_end = a;
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
     if (hc.err.code) continue;
@@ -590,7 +600,6 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     hc.o_values = is_ba ? 0 : take(ns * (uint64_t)w);
     hc.o_def = hc.col.max_def > 1 ? take(ns) : 0;
     hc.o_rep = hc.col.max_rep > 0 ? take(ns) : 0;
-    hc.o_valid = hc.col.max_def > 0 ? take(((ns + 31) / 32 + 2) * 4) : 0;
     hc.o_lists = hc.col.max_rep > 0 ? take((ns + 1) * 4) : 0;
     hc.o_offsets = is_ba ? take((ns + 1) * 4) : 0;
     hc.o_ba_index = is_ba ? take(ns * 8) : 0;
@@ -641,18 +650,19 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
     }
   }
+  // Region set to 0xff before every decode: chunk error keys, dictionary tile table.
+  b->o_err = take((uint64_t)nc * 8);
+  b->f_begin = b->o_err;
+  b->o_tile_first = take(b->tile_total * 4);
+  b->f_end = a;
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
   b->o_chunks = take((uint64_t)nc * sizeof(ChunkDesc));
-  b->o_err = take((uint64_t)nc * 8);
   b->o_nn = take((uint64_t)np * 4);
-  b->o_rec = take((uint64_t)np * 4);
   b->o_vbase = take((uint64_t)np * 8);
   b->o_rbase = take((uint64_t)np * 8);
   b->o_runs = take(b->run_total * sizeof(HybRun));
   b->o_run_base = take((uint64_t)np * 8);
-  b->o_run_count = take((uint64_t)np * 4);
-  b->o_tile_first = take(b->tile_total * 4);
   b->o_tile_base = take((uint64_t)np * 8);
   b->o_items = take(b->items.size() * sizeof(WorkItem));
   b->o_ba_tile_sum = take(b->ba_tiles_total * 4);
@@ -737,6 +747,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->o_pages, pages.data(), pages.size() * sizeof(PageDesc)), err);
   HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
   HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
+  HIPCHECK(up(b->o_nn, b->page_nn_init.data(), np * 4), err);
   HIPCHECK(up(b->o_tile_base, b->tile_base.data(), np * 8), err);
   HIPCHECK(up(b->o_items, b->items.data(), b->items.size() * sizeof(WorkItem)), err);
   HIPCHECK(up(b->o_ba_tile_off, b->ba_tile_off.data(), b->ba_tile_off.size() * 8), err);
@@ -820,16 +831,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   uint8_t *A = b->d_arena;
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
-  // per-decode state
-  HIPCHECK(hipMemsetAsync(A + b->o_err, 0xff, (size_t)nc * 8, s), err);
-  HIPCHECK(hipMemcpyAsync(A + b->o_nn, b->page_nn_init.data(), (size_t)np * 4, hipMemcpyHostToDevice, s), err);
-  HIPCHECK(hipMemsetAsync(A + b->o_rec, 0, (size_t)np * 4, s), err);
-  HIPCHECK(hipMemsetAsync(A + b->o_run_count, 0, (size_t)np * 4, s), err);
-  if (b->tile_total) HIPCHECK(hipMemsetAsync(A + b->o_tile_first, 0xff, b->tile_total * 4, s), err);
-  for (auto &hc : b->chunks) {
-    if (hc.err.code) continue;
-    if (hc.o_valid) HIPCHECK(hipMemsetAsync(A + hc.o_valid, 0, ((hc.num_slots + 31) / 32 + 2) * 4, s), err);
-  }
+  // per-decode state: two contiguous fills (validity bitmaps + counters; error keys + tile table).
+  // page_nn of pages without level streams is constant and was uploaded with the descriptors.
+  (void)np;
+  HIPCHECK(hipMemsetAsync(A + b->z_begin, 0, b->z_end - b->z_begin, s), err);
+  HIPCHECK(hipMemsetAsync(A + b->f_begin, 0xff, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
   HIPCHECK(timed(b, 4, s, [&] { return launch_dict_ba(d, l, s); }), err);

@@ -532,18 +532,19 @@ __global__ void __launch_bounds__(64) k_scan_runs(BatchDev b, const uint32_t *pa
 struct DictLDS {
   HybRun runs[1024];
 };
+constexpr uint32_t kDeltaWin = 16384;  // bytes of a DELTA stream staged in LDS at a time
 struct DeltaLDS {
-  uint32_t mb_off[8][64];   // payload offset of each miniblock (rel. to stream), per block in batch
+  uint32_t win[kDeltaWin / 4 + 8];  // stream bytes [win0, win0 + kDeltaWin), zero past the stream end
+  uint32_t mb_off[8][64];           // miniblock payload offset (stream-relative) per block of the batch
   uint8_t mb_w[8][64];
   int64_t min_delta[8];
-  uint64_t sums[256];
-  uint32_t nblocks;
-  uint32_t err_code, err_pos, stop_val;
-  uint32_t next_hdr;
+  uint64_t wsum[4];                 // per-wave totals of the batch scan
+  uint32_t nblocks, err_code, err_pos, stop_val, next_hdr, reload;
 };
 union ValuesLDS {
   DictLDS dict;
   DeltaLDS delta;
+  uint8_t slow_widths[256];
 };
 
 // Reference fixed-width PLAIN error: binary.Read/io.ReadFull of w bytes per value
@@ -551,31 +552,60 @@ union ValuesLDS {
 // no byte of it is left, else ErrUnexpectedEOF.
 DEV uint32_t plain_err(uint64_t have, uint32_t w) { return (have % w) == 0 ? PQ_ERR_EOF : PQ_ERR_UNEXPECTED_EOF; }
 
-// Byte-range copy dst[0..n) = src[0..n) with arbitrary alignments: 16 B per lane.
+// Byte-range copy dst[0..n) = src[0..n) with arbitrary alignments. The destination is
+// walked in 16-B aligned pieces, one per lane; each piece is assembled from the two
+// 16-B aligned source blocks that cover it (dwordx4 loads; the second block is the
+// next lane's first, so the pair costs no extra HBM traffic) with v_alignbyte funnel
+// shifts. Four pieces per lane are kept in flight.
+DEV uint4 funnel16(uint4 a, uint4 b, uint32_t s) {  // bytes [s, s+16) of the 32-byte pair (a, b)
+  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t q = s >> 2, r = s & 3;
+  uint4 o;
+  switch (q) {  // wave-uniform (same source alignment for every lane)
+    case 0: o.x = __builtin_amdgcn_alignbyte(w[1], w[0], r); o.y = __builtin_amdgcn_alignbyte(w[2], w[1], r);
+            o.z = __builtin_amdgcn_alignbyte(w[3], w[2], r); o.w = __builtin_amdgcn_alignbyte(w[4], w[3], r); break;
+    case 1: o.x = __builtin_amdgcn_alignbyte(w[2], w[1], r); o.y = __builtin_amdgcn_alignbyte(w[3], w[2], r);
+            o.z = __builtin_amdgcn_alignbyte(w[4], w[3], r); o.w = __builtin_amdgcn_alignbyte(w[5], w[4], r); break;
+    case 2: o.x = __builtin_amdgcn_alignbyte(w[3], w[2], r); o.y = __builtin_amdgcn_alignbyte(w[4], w[3], r);
+            o.z = __builtin_amdgcn_alignbyte(w[5], w[4], r); o.w = __builtin_amdgcn_alignbyte(w[6], w[5], r); break;
+    default: o.x = __builtin_amdgcn_alignbyte(w[4], w[3], r); o.y = __builtin_amdgcn_alignbyte(w[5], w[4], r);
+             o.z = __builtin_amdgcn_alignbyte(w[6], w[5], r); o.w = __builtin_amdgcn_alignbyte(w[7], w[6], r); break;
+  }
+  return o;
+}
+
 DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
   if (n == 0) return;
   uintptr_t da = (uintptr_t)dst;
   uint64_t head = (16 - (da & 15)) & 15;
   if (head > n) head = n;
   if (tid < head) dst[tid] = src[tid];
-  uint64_t body = (n - head) & ~(uint64_t)15;
-  uint8_t *d = dst + head;
+  const uint64_t body = (n - head) & ~(uint64_t)15;
+  uint4 *d = (uint4 *)(dst + head);
   const uint8_t *sp = src + head;
-  for (uint64_t o = (uint64_t)tid * 16; o < body; o += (uint64_t)nt * 16) {
-    const uint8_t *q = sp + o;
-    uintptr_t a = (uintptr_t)q;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-    uint32_t s = (uint32_t)(a & 3);
-    uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-    uint4 v;
-    v.x = __builtin_amdgcn_alignbyte(w1, w0, s);
-    v.y = __builtin_amdgcn_alignbyte(w2, w1, s);
-    v.z = __builtin_amdgcn_alignbyte(w3, w2, s);
-    v.w = __builtin_amdgcn_alignbyte(w4, w3, s);
-    *(uint4 *)(d + o) = v;
+  const uint32_t sa = (uint32_t)((uintptr_t)sp & 15);
+  const uint4 *sb = (const uint4 *)((uintptr_t)sp & ~(uintptr_t)15);
+  const uint64_t pieces = body >> 4;
+  uint64_t i = tid;
+  if (sa == 0) {
+    for (; i + 3 * (uint64_t)nt < pieces; i += 4 * (uint64_t)nt) {
+      uint4 v0 = sb[i], v1 = sb[i + nt], v2 = sb[i + 2 * nt], v3 = sb[i + 3 * nt];
+      d[i] = v0; d[i + nt] = v1; d[i + 2 * nt] = v2; d[i + 3 * nt] = v3;
+    }
+    for (; i < pieces; i += nt) d[i] = sb[i];
+  } else {
+    for (; i + 3 * (uint64_t)nt < pieces; i += 4 * (uint64_t)nt) {
+      uint4 a0 = sb[i], b0 = sb[i + 1], a1 = sb[i + nt], b1 = sb[i + nt + 1];
+      uint4 a2 = sb[i + 2 * nt], b2 = sb[i + 2 * nt + 1], a3 = sb[i + 3 * nt], b3 = sb[i + 3 * nt + 1];
+      d[i] = funnel16(a0, b0, sa);
+      d[i + nt] = funnel16(a1, b1, sa);
+      d[i + 2 * nt] = funnel16(a2, b2, sa);
+      d[i + 3 * nt] = funnel16(a3, b3, sa);
+    }
+    for (; i < pieces; i += nt) d[i] = funnel16(sb[i], sb[i + 1], sa);
   }
-  uint64_t tail = n - head - body;
-  if (tid < tail) d[body + tid] = sp[body + tid];
+  const uint64_t tail = n - head - body;
+  if (tid < tail) dst[head + body + tid] = sp[body + tid];
 }
 
 // PLAIN fixed width (INT32/INT64/FLOAT/DOUBLE/INT96/FLBA): byte copy.
@@ -695,19 +725,38 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, first_err_code);
 }
 
-// DELTA_BINARY_PACKED (deltabp_decoder.go:113-174 / :272-333), one workgroup per page.
-// Wave 0 walks up to 8 block headers (lane 0, scalar), then all 256 threads
-// unpack one group of 8 deltas each and a block-wide scan with a carried
-// running value produces the outputs. Requires miniblock sizes that are
-// multiples of 8 (else PF_DELTA_SLOW).
-DEV bool delta_hdr(const uint8_t *s, uint32_t n, uint32_t pos, bool is64, uint32_t mbc, int64_t *min_delta,
-                   uint8_t *w, uint32_t *hdr_len, uint32_t *err) {
+// DELTA_BINARY_PACKED (deltabp_decoder.go:113-174 / :272-333), one workgroup per page,
+// single pass over the stream: the stream is staged through a 16 KiB LDS window
+// (coalesced dwordx4 loads); thread 0 walks up to 8 block headers inside the window
+// (minDelta zigzag varint + miniblock widths -> miniblock offsets); then every thread
+// unpacks one group of 8 deltas from LDS, a wave64 shuffle scan plus a 4-entry
+// cross-wave combine gives the running sums, and each thread writes its 8 values
+// (64 contiguous bytes). Requires miniblock sizes that are multiples of 8 and at most
+// 2048 values per block (else PF_DELTA_SLOW).
+//
+// Reference semantics reproduced exactly:
+//  * value[i] = first + sum of (delta[k] + minDelta[block(k)]) for k < i, with the
+//    look-ahead: returning value i reads the group holding delta i (Q1);
+//  * next() at position p fails when p >= the header's valuesCount (io.EOF);
+//  * a block header is read by next() at the block's first position; its errors
+//    (varint EOF/overflow/range, short width bytes, width > 32/64) surface there;
+//  * a group is read with io.ReadFull at its first position (EOF / ErrUnexpectedEOF).
+// `s` may be an LDS view of the stream that is valid for 10 + mbc bytes from pos; `gs`
+// is the stream in global memory, read only for varints longer than 10 bytes.
+DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64, uint32_t mbc,
+                   int64_t *min_delta, uint8_t *w, uint32_t *hdr_len, uint32_t *err) {
   // minDelta: zigzag varint (readVariant32 / readVariant64), then mbc width bytes (io.ReadFull)
   uint64_t x = 0;
   unsigned sh = 0;
   uint32_t k = 0;
   for (;; k++) {
     if (pos + k >= n) { *err = PQ_ERR_EOF; return false; }
+    if (k == 10) {  // Go keeps reading: a later terminator is an overflow, none is EOF
+      for (uint32_t q = pos + 10; q < n; q++)
+        if (gs[q] < 0x80) { *err = PQ_ERR_RANGE; return false; }
+      *err = PQ_ERR_EOF;
+      return false;
+    }
     uint32_t by = s[pos + k];
     if (by < 0x80) {
       if (k > 9 || (k == 9 && by > 1)) { *err = PQ_ERR_RANGE; return false; }
@@ -733,6 +782,26 @@ DEV bool delta_hdr(const uint8_t *s, uint32_t n, uint32_t pos, bool is64, uint32
   return true;
 }
 
+DEV uint64_t wave_incl_scan64(uint64_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  return v;
+}
+
+// bits at bit offset `bo` (< 2^32) of the LDS window, width <= 64
+DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
+  if (w == 0) return 0;
+  uint32_t wi = bo >> 5, sh = bo & 31;
+  uint64_t lo = (uint64_t)win[wi] | ((uint64_t)win[wi + 1] << 32);
+  uint64_t x = lo >> sh;
+  if (sh && w > 64 - sh) x |= (uint64_t)win[wi + 2] << (64 - sh);
+  return w >= 64 ? x : x & ((1ull << w) - 1ull);
+}
+
 DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                   DeltaLDS &L) {
   if (nn == 0) return;
@@ -740,32 +809,54 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   const uint32_t n = pd.val_len;
   const bool is64 = pd.vkind == VK_DELTA64;
   const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint64_t vb = b.page_vbase[wi.page];
-  // values decodable before the decoder's own valuesCount (next() returns EOF at position >= valuesCount)
-  uint32_t limit = nn;
+  uint32_t limit = nn;  // next() returns EOF at positions >= the header's valuesCount
   uint32_t final_err = 0, final_pos = 0;
   if ((uint32_t)pd.delta_count < nn) { limit = (uint32_t)pd.delta_count; final_err = PQ_ERR_EOF; final_pos = limit; }
   uint64_t carry = (uint64_t)pd.delta_first;
-  uint32_t hdr = pd.delta_first_mb - pd.val_off;  // first miniblock header (relative to stream)
+  uint32_t hdr = pd.delta_first_mb - pd.val_off;  // next miniblock header (stream-relative)
   const uint32_t gpb = bs / 8;                      // groups per block
-  const uint32_t blocks_per_batch = max(1u, min(8u, 256u / gpb));
-  for (uint32_t blk0 = 0; (uint64_t)blk0 * bs < limit; blk0 += blocks_per_batch) {
-    // ---- header walk (thread 0)
-    if (threadIdx.x == 0) {
+  const uint32_t bpb = max(1u, min(8u, 256u / gpb)); // blocks per batch
+  const uint32_t max_blk = 10 + mbc + bs * 8;       // upper bound of one block's bytes (widths <= 64)
+  uint32_t win0 = 0xffffffffu;
+  uint32_t blk = 0;                                 // index of the next block
+  uint8_t *wb = (uint8_t *)L.win;
+  while ((uint64_t)blk * bs < limit) {
+    // ---- (re)stage the window so that it starts at the next header
+    if (win0 == 0xffffffffu || (hdr + max_blk > win0 + kDeltaWin && win0 + kDeltaWin < n)) {
+      __syncthreads();
+      win0 = hdr & ~3u;
+      const uint8_t *src = s + win0;
+      uint32_t lim = n > win0 ? n - win0 : 0;  // stream bytes left
+      for (uint32_t k = tid; k < kDeltaWin / 4 + 8; k += blockDim.x) {
+        uint32_t o = 4 * k;
+        uint32_t v = o + 4 <= lim ? ld32(src + o) : (o < lim ? ld32(src + o) & ((1u << (8 * (lim - o))) - 1u) : 0u);
+        L.win[k] = v;
+      }
+      __syncthreads();
+    }
+    // ---- header walk (thread 0), inside the window
+    if (tid == 0) {
       L.err_code = 0;
       L.stop_val = limit;
       uint32_t nb = 0;
-      for (; nb < blocks_per_batch && (uint64_t)(blk0 + nb) * bs < limit; nb++) {
+      const uint32_t wend = win0 + kDeltaWin;
+      for (; nb < bpb && (uint64_t)(blk + nb) * bs < limit; nb++) {
+        if (hdr + 10 + mbc > wend && wend < n) break;  // header not entirely staged: next window
         uint32_t hl = 0, e = 0;
         int64_t md;
-        if (!delta_hdr(s, n, hdr, is64, mbc, &md, L.mb_w[nb], &hl, &e)) {
+        // parse from LDS: bytes past n read as 0 but delta_hdr bounds-checks against n
+        if (!delta_hdr(wb - win0, s, n, hdr, is64, mbc, &md, L.mb_w[nb], &hl, &e)) {
           L.err_code = e;
-          L.err_pos = (blk0 + nb) * bs;  // next() at the block's first position reads the header
+          L.err_pos = (blk + nb) * bs;
           L.stop_val = L.err_pos;
           break;
         }
+        uint32_t off = hdr + hl, end = off;
+        for (uint32_t m = 0; m < mbc; m++) end += (mbvc / 8) * L.mb_w[nb][m];
+        if (end > wend && wend < n && nb > 0) break;  // block body not entirely staged (always take >= 1)
         L.min_delta[nb] = md;
-        uint32_t off = hdr + hl;
         for (uint32_t m = 0; m < mbc; m++) {
           L.mb_off[nb][m] = off;
           off += (mbvc / 8) * L.mb_w[nb][m];
@@ -780,78 +871,102 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     const uint32_t nb = L.nblocks;
     uint32_t stop = L.stop_val;
     // ---- unpack: thread t -> group t of the batch (8 deltas)
-    const uint32_t g = threadIdx.x;
+    const uint32_t g = tid;
     const uint32_t bi = g / gpb;
-    const uint32_t d0 = (blk0 * bs) + g * 8;  // first delta index of the group
+    const uint32_t d0 = (blk + bi) * bs + (g % gpb) * 8;  // first delta index of the group
     uint64_t d[8];
     uint64_t sum = 0;
     uint32_t gerr = 0, gerr_pos = 0;
-    bool valid = bi < nb && d0 < stop;
+    const bool valid = bi < nb && d0 < stop;
     uint32_t goff = 0, wbits = 0;
     if (valid) {
       uint32_t inb = (g % gpb) * 8;
       uint32_t m = inb / mbvc, o = inb % mbvc;
       wbits = L.mb_w[bi][m];
-      goff = L.mb_off[bi][m] + (o / 8) * wbits;  // group byte offset
-      // io.ReadFull(w bytes) of the group
+      goff = L.mb_off[bi][m] + (o / 8) * wbits;  // group byte offset (stream-relative)
       if (wbits > 0 && goff >= n) { gerr = PQ_ERR_EOF; gerr_pos = d0; }
       else if ((uint64_t)goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
     }
     if (valid && !gerr) {
-      uint64_t md = (uint64_t)L.min_delta[bi];
+      const uint64_t md = (uint64_t)L.min_delta[bi];
+      const uint32_t bo = (goff - win0) * 8;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        uint64_t u = is64 ? bits64(s + goff, (uint64_t)j * wbits, wbits)
-                          : (uint64_t)(int64_t)(int32_t)bits32(s + goff, (uint64_t)j * wbits, wbits);
+        uint64_t u = lds_bits64(L.win, bo + j * wbits, wbits);
+        if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
         d[j] = u + md;
         sum += d[j];
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j++) d[j] = 0;
     }
-    // error handling: the first failing group decides where decoding stops
     if (gerr) atomicMin(&L.stop_val, gerr_pos);
     __syncthreads();
-    if (gerr && gerr_pos == L.stop_val && L.stop_val < stop) {
-      L.err_code = gerr;
-      L.err_pos = gerr_pos;
-    }
-    stop = L.stop_val;
-    // ---- block-wide exclusive scan of group sums (only groups fully before `stop` contribute)
-    L.sums[g] = valid ? sum : 0;
+    const uint32_t stop2 = L.stop_val;
+    if (gerr && gerr_pos == stop2 && stop2 < stop) { L.err_code = gerr; L.err_pos = gerr_pos; }
+    stop = stop2;
+    const uint64_t contrib = (valid && d0 < stop) ? sum : 0;
+    // ---- block-wide exclusive scan of group sums: wave shuffle scan + 4-way combine
+    const uint64_t incl = wave_incl_scan64(contrib);
+    if (lane == 63) L.wsum[wv] = incl;
     __syncthreads();
-    for (uint32_t dd = 1; dd < 256; dd <<= 1) {
-      uint64_t a = g >= dd ? L.sums[g - dd] : 0;
-      __syncthreads();
-      L.sums[g] += a;
-      __syncthreads();
+    uint64_t before = 0, total = 0;
+    for (uint32_t k = 0; k < (blockDim.x >> 6); k++) {
+      uint64_t t = L.wsum[k];
+      if (k < wv) before += t;
+      total += t;
     }
-    uint64_t excl = L.sums[g] - (valid ? sum : 0);
-    uint64_t run = carry + excl;
-    if (valid) {
-      // value at position d0+j is first + sum of deltas before it (one delta of look-ahead)
+    uint64_t run = carry + before + incl - contrib;
+    if (valid && d0 < stop) {
+      uint64_t out[8];
+#pragma unroll
       for (int j = 0; j < 8; j++) {
-        uint32_t pos = d0 + j;
-        if (pos < stop) {
-          if (is64) ((uint64_t *)cd.values)[vb + pos] = run;
-          else ((uint32_t *)cd.values)[vb + pos] = (uint32_t)run;
-        }
+        out[j] = run;
         run += d[j];
       }
+      if (d0 + 8 <= stop) {
+        if (is64) {
+          uint64_t *o = (uint64_t *)cd.values + vb + d0;  // 8-B aligned; 16-B aligned when vb is even
+          if (((uintptr_t)o & 15) == 0) {
+            uint4 *o4 = (uint4 *)o;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              o4[j] = make_uint4((uint32_t)out[2 * j], (uint32_t)(out[2 * j] >> 32), (uint32_t)out[2 * j + 1],
+                                 (uint32_t)(out[2 * j + 1] >> 32));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = out[j];
+          }
+        } else {
+          uint32_t *o = (uint32_t *)cd.values + vb + d0;
+#pragma unroll
+          for (int j = 0; j < 8; j++) o[j] = (uint32_t)out[j];
+        }
+      } else {
+        for (int j = 0; j < 8; j++) {
+          if (d0 + j < stop) {
+            if (is64) ((uint64_t *)cd.values)[vb + d0 + j] = out[j];
+            else ((uint32_t *)cd.values)[vb + d0 + j] = (uint32_t)out[j];
+          }
+        }
+      }
     }
-    carry += L.sums[255];
+    carry += total;
+    blk += nb;
     __syncthreads();
-    if (L.err_code || stop < limit) {
-      if (threadIdx.x == 0 && L.err_code)
-        report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, L.err_pos, L.err_code);
+    if (L.err_code || stop < limit || nb == 0) {
+      if (tid == 0 && L.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, L.err_pos, L.err_code);
       return;
     }
-    __syncthreads();
   }
-  if (final_err && threadIdx.x == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, final_pos, final_err);
+  if (final_err && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, final_pos, final_err);
 }
 
 // Exact scalar restatement of deltaBitPackDecoder.next for pages whose miniblock
 // value count is not a multiple of 8 (deltabp_decoder.go:113-174).
-DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
+DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
+                       uint8_t *widths) {
   if (threadIdx.x != 0 || nn == 0) return;
   const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
   const uint32_t n = pd.val_len;
@@ -859,12 +974,11 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
   const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc;
   const uint64_t vb = b.page_vbase[wi.page];
   uint32_t rpos = pd.delta_first_mb - pd.val_off;
-  uint8_t widths[256];
   int64_t md = 0;
   uint32_t hl, e = 0;
   if (mbc > 256) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, 0, PQ_ERR_UNSUPPORTED); return; }
   // init(): the first miniblock header was validated on the host; re-read it here
-  if (!delta_hdr(s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
+  if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
     report(b, pd.chunk, 0, 0, ST_VALUES, 0, e);
     return;
   }
@@ -878,7 +992,7 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     if (pos % 8 == 0) {
       if (pos % mbvc == 0) {
         if (cur_mb >= mbc) {
-          if (!delta_hdr(s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
+          if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
             report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, e);
             return;
           }
@@ -941,7 +1055,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *item
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
     case WI_DELTA:
-      if (pd.flags & PF_DELTA_SLOW) do_delta_slow(b, wi, pd, cd, nn);
+      if (pd.flags & PF_DELTA_SLOW) do_delta_slow(b, wi, pd, cd, nn, lds.slow_widths);
       else do_delta(b, wi, pd, cd, nn, lds.delta);
       break;
     case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
