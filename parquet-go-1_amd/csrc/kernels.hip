@@ -94,6 +94,15 @@ DEV uint32_t wave_excl_scan(uint32_t v) {
   }
   return x - v;
 }
+DEV uint64_t wave_incl_scan64(uint64_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  return v;
+}
 DEV uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -143,7 +152,7 @@ DEV void stage_load(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n) {
 }
 
 template <class Sink>
-DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
+__device__ __attribute__((noinline)) uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
   const uint32_t lane = lane_id();
   const uint32_t rs = (bw + 7) >> 3;
   uint32_t pos = 0, done = 0;
@@ -263,10 +272,6 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegSlots = 65536;  // bitmap slots staged in LDS per page
 
-struct LevelLDS {
-  WalkLDS walk;
-  uint32_t bits[kSegSlots / 32];
-};
 
 struct LevelSink {
   const uint8_t *s;
@@ -357,6 +362,257 @@ struct LevelSink {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Speculative segment decoder for LEVEL streams (short runs: a V2 def section of
+// 64K slots holds ~3,700 runs). The stream (<= kLvlStage bytes) is staged in LDS
+// and cut into 64 segments, one per lane.
+//  A. every lane follows the header chain from its segment start (as if a run
+//     header started there), marking each visited position inside its segment;
+//  B. every lane continues its chain past its segment until it reaches a position
+//     marked by a later lane (the chains have merged: "next header" is a function
+//     of the position alone) and records the positions it visited on the way;
+//  C. lane 0 starts at the true stream start, so the lanes reached by following
+//     merge targets from lane 0 are exactly the lanes whose chains are true;
+//  D. each true lane clears the (false) marks between its segment end and its
+//     merge point and sets its recorded positions: the marks are now exactly the
+//     run headers of the reference's sequential walk (hybrid_decoder.go:81-165);
+//  E. every lane decodes the runs whose headers lie in its segment; a wave scan
+//     of the per-lane value counts gives each run's first slot; runs are expanded
+//     into levels / validity bits (short runs per lane, long runs by the wave).
+// Streams larger than kLvlStage, or a true lane whose record list overflows, use
+// the windowed walker (hyb_walk). Errors are reported at the slot where the
+// reference's next() would fail, as in hyb_walk.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLvlStage = 12288;  // bytes of a level stream decoded speculatively
+constexpr uint32_t kExtMax = 24;       // recorded chain positions per lane past its segment
+
+struct SpecLDS {
+  uint32_t stage[kLvlStage / 4 + 8];
+  uint32_t marks[kLvlStage / 32 + 4];
+  uint16_t ext[64][kExtMax];
+};
+struct LevelLDS {
+  union {
+    WalkLDS walk;
+    SpecLDS spec;
+  } u;
+  uint32_t bits[kSegSlots / 32];
+};
+
+struct Hdr {
+  uint32_t err, nvals, okvals, value, adv, bp;
+};
+
+// Decode the run header that would start at stream position c (stage holds [sb, ...)).
+DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t c, uint32_t n, uint32_t bw,
+                   uint32_t rs) {
+  Hdr r{0, 0, 0, 0, 1, 0};
+  if (c >= n) { r.err = PQ_ERR_EOF; return r; }
+  uint32_t off = c - sb;
+  uint32_t w0 = lds_ld32(stg, off), w1 = lds_ld32(stg, off + 4), w2 = lds_ld32(stg, off + 8);
+  uint64_t h = 0;
+  unsigned sh = 0;
+  bool term = false;
+  uint32_t k = 0;
+  for (; k < 12; k++) {
+    if (c + k >= n) { r.err = PQ_ERR_EOF; break; }
+    uint32_t wv = k < 4 ? w0 : (k < 8 ? w1 : w2);
+    uint32_t by = (wv >> (8 * (k & 3))) & 0xffu;
+    if (by < 0x80u) {
+      if (k > 9 || (k == 9 && by > 1)) r.err = PQ_ERR_RANGE;
+      else if (sh < 64) h |= (uint64_t)by << sh;
+      term = true;
+      break;
+    }
+    if (sh < 64) h |= (uint64_t)(by & 0x7f) << sh;
+    sh += 7;
+  }
+  if (!r.err && !term) {  // > 12-byte varint: Go keeps reading until a terminator (overflow) or EOF
+    r.err = PQ_ERR_EOF;
+    for (uint32_t q = c + 12; q < n; q++)
+      if (s[q] < 0x80) { r.err = PQ_ERR_RANGE; break; }
+  }
+  const uint32_t hl = k + 1;
+  if (!r.err && h > 0x7fffffffull) r.err = PQ_ERR_RANGE;
+  if (r.err) return r;
+  const uint32_t cnt = (uint32_t)(h >> 1);
+  r.bp = (uint32_t)(h & 1);
+  if (cnt == 0) { r.err = PQ_ERR_INVALID; return r; }
+  const uint32_t pay = c + hl;
+  if (r.bp) {
+    uint64_t nv = (uint64_t)cnt * 8;
+    r.nvals = nv > 0x7fffffffull ? 0x7fffffffu : (uint32_t)nv;
+    uint64_t pb = (uint64_t)cnt * bw;
+    uint64_t a = hl + pb;
+    r.adv = a > 0x3fffffffull ? 0x3fffffffu : (uint32_t)a;
+    if ((uint64_t)pay + pb > n) {
+      uint64_t g = pay >= n ? 0 : ((uint64_t)(n - pay) + bw - 1) / bw;  // groups that start before EOF
+      uint64_t ok = g * 8;
+      r.okvals = ok > r.nvals ? r.nvals : (uint32_t)ok;
+    } else {
+      r.okvals = r.nvals;
+    }
+    r.value = pay;
+  } else {
+    r.nvals = cnt;
+    r.okvals = cnt;
+    r.adv = hl + rs;
+    if (pay >= n) r.err = PQ_ERR_EOF;
+    else if (pay + rs > n) r.err = PQ_ERR_UNEXPECTED_EOF;
+    else {
+      uint32_t v = lds_ld32(stg, pay - sb);
+      r.value = rs >= 4 ? v : (v & ((1u << (8 * rs)) - 1u));
+      if (bw < 32 && (r.value >> bw) != 0) r.err = PQ_ERR_INVALID;
+    }
+  }
+  return r;
+}
+
+DEV bool mark_test(const uint32_t *m, uint32_t p) { return (m[p >> 5] >> (p & 31)) & 1u; }
+
+// Clear marks in [lo, hi).
+DEV void mark_clear(uint32_t *m, uint32_t lo, uint32_t hi) {
+  if (lo >= hi) return;
+  uint32_t w0 = lo >> 5, w1 = (hi - 1) >> 5;
+  for (uint32_t w = w0; w <= w1; w++) {
+    uint32_t keep = 0;
+    if (w == w0) keep |= (1u << (lo & 31)) - 1u;
+    if (w == w1 && ((hi & 31) != 0)) keep |= ~((1u << (hi & 31)) - 1u);
+    atomicAnd(&m[w], keep);
+  }
+}
+
+// Returns the number of values the stream supplied (< need only on error).
+template <class Sink>
+DEV uint32_t lvl_decode(LevelLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
+  if (need == 0) return 0;
+  if (n > kLvlStage) return hyb_walk(L.u.walk, s, n, bw, need, sink);
+  SpecLDS &S = L.u.spec;
+  const uint32_t lane = lane_id();
+  const uint32_t rs = (bw + 7) >> 3;
+  // ---- stage the whole stream, zero the marks
+  for (uint32_t k = lane; k < kLvlStage / 4 + 8; k += 64) {
+    uint32_t o = 4 * k;
+    S.stage[k] = o + 4 <= n ? ld32(s + o) : (o < n ? ld32(s + o) & ((1u << (8 * (n - o))) - 1u) : 0u);
+  }
+  const uint32_t nmw = (n + 31) / 32 + 2;
+  for (uint32_t k = lane; k < nmw; k += 64) S.marks[k] = 0;
+  __syncthreads();
+  const uint32_t seg = max(16u, (n + 63) / 64);
+  const uint32_t lo = lane * seg, hi = min(n, lo + seg);
+  const bool active = lo < n;
+  // ---- A: speculative chains inside the own segment
+  uint32_t p = lo;
+  if (active) {
+    while (p < hi) {
+      atomicOr(&S.marks[p >> 5], 1u << (p & 31));
+      Hdr h = decode_hdr(S.stage, 0, s, p, n, bw, rs);
+      p += h.err ? 1u : h.adv;
+    }
+  }
+  __syncthreads();
+  // ---- B: continue past the segment until merging with a later lane's chain
+  uint32_t target = 64, conv = n, cnt = 0;
+  if (active) {
+    uint32_t q = p;
+    while (q < n) {
+      if (mark_test(S.marks, q)) { target = q / seg; conv = q; break; }
+      if (cnt < kExtMax) S.ext[lane][cnt] = (uint16_t)q;
+      cnt++;
+      Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
+      q += h.err ? 1u : h.adv;
+    }
+  }
+  // ---- C: true lanes (scalar)
+  uint64_t tmask = 0;
+  bool overflow = false;
+  for (uint32_t t = 0; t < 64;) {
+    tmask |= 1ull << t;
+    if (rdlane(cnt, t) > kExtMax) overflow = true;
+    uint32_t nt = rdlane(target, t);
+    if (nt <= t) break;  // cannot happen (merge points lie past the lane's segment)
+    t = nt;
+  }
+  if (overflow) {
+    __syncthreads();
+    return hyb_walk(L.u.walk, s, n, bw, need, sink);
+  }
+  const bool is_true = (tmask >> lane) & 1ull;
+  // ---- D: patch marks between each true lane's segment end and its merge point
+  if (is_true && active) mark_clear(S.marks, hi, conv);
+  __syncthreads();
+  if (is_true && active)
+    for (uint32_t k = 0; k < cnt; k++) atomicOr(&S.marks[S.ext[lane][k] >> 5], 1u << (S.ext[lane][k] & 31));
+  __syncthreads();
+  // ---- E1: per-lane value counts up to the first error in chain order
+  uint32_t tvals = 0, ecode = 0;
+  const uint32_t mw0 = lo >> 5, mw1 = active ? (hi - 1) >> 5 : 0;
+  auto first_bits = [&](uint32_t w) -> uint32_t {
+    uint32_t m = S.marks[w];
+    if (w == mw0) m &= ~((1u << (lo & 31)) - 1u);
+    if (w == mw1 && (hi & 31)) m &= (1u << (hi & 31)) - 1u;
+    return m;
+  };
+  if (active) {
+    for (uint32_t w = mw0; w <= mw1 && !ecode; w++) {
+      uint32_t m = first_bits(w);
+      while (m) {
+        uint32_t q = w * 32 + __builtin_ctz(m);
+        m &= m - 1;
+        Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
+        if (h.err) { ecode = h.err; break; }
+        if (h.okvals < h.nvals) { tvals = min(0x7fffffffu, tvals + h.okvals); ecode = PQ_ERR_EOF; break; }
+        tvals = min(0x7fffffffu, tvals + h.nvals);
+      }
+    }
+  }
+  const uint64_t emask = __ballot(ecode != 0);
+  const uint32_t elane = emask ? (uint32_t)__builtin_ctzll(emask) : 64u;
+  if (lane > elane) tvals = 0;
+  uint64_t incl = wave_incl_scan64(tvals);
+  const uint64_t start = incl - tvals;
+  const uint64_t total = __shfl(incl, 63, 64);
+  uint32_t eff = need;
+  if (elane < 64) {
+    uint64_t epos = __shfl(incl, (int)elane, 64);
+    uint32_t ec = rdlane(ecode, elane);
+    if (epos < need) { sink.error((uint32_t)epos, ec); eff = (uint32_t)epos; }
+  } else if (total < need) {
+    sink.error((uint32_t)total, PQ_ERR_EOF);  // the chain reached the stream end: next header is EOF
+    eff = (uint32_t)total;
+  }
+  // ---- E2: expansion
+  uint64_t slot = start;
+  uint32_t cw = mw0, cm = (active && lane <= elane) ? first_bits(mw0) : 0u;
+  bool more = active && lane <= elane;
+  for (;;) {
+    // next marked header of this lane
+    uint32_t q = 0;
+    bool have = false;
+    if (more) {
+      while (!cm && cw < mw1) cm = first_bits(++cw);
+      if (cm) {
+        q = cw * 32 + __builtin_ctz(cm);
+        cm &= cm - 1;
+        have = slot < eff;
+      }
+      if (!have) more = false;
+    }
+    if (!__ballot(have)) break;
+    uint32_t cnt2 = 0, value = 0;
+    bool bp = false;
+    if (have) {
+      Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
+      cnt2 = (uint32_t)min((uint64_t)h.nvals, (uint64_t)eff - slot);
+      bp = h.bp != 0;
+      value = h.value;
+    }
+    sink.window(have && cnt2 > 0, (uint32_t)slot, cnt2, bp, value, q);
+    slot += cnt2;
+  }
+  return (uint32_t)min((uint64_t)eff, total);
+}
+
 // One wave per page with level streams (rep and/or def).
 // Reference: page_v1.go:42-48 / page_v2.go:40-46 readValues -> decodePackedArray.
 __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages) {
@@ -370,12 +626,12 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
 
   // ---- repetition levels (counted: records start where rep == 0)
   if (cd.max_rep > 0) {
-    LevelSink rs{base + pd.rep_off, pd.rep_len, (uint32_t)cd.rep_bw, (uint8_t *)cd.rep_levels + pd.slot_base, nullptr, nullptr,
-                 pd.slot_base, 0u, 0u, 0u, 0u};
+    LevelSink rs{base + pd.rep_off, pd.rep_len, (uint32_t)cd.rep_bw, (uint8_t *)cd.rep_levels + pd.slot_base, nullptr,
+                 nullptr, pd.slot_base, 0u, 0u, 0u, 0u};
     if (!(pd.flags & PF_REP)) {
       if (ns) rs.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
     } else {
-      hyb_walk(lds.walk, base + pd.rep_off, pd.rep_len, cd.rep_bw, ns, rs);
+      lvl_decode(lds, base + pd.rep_off, pd.rep_len, cd.rep_bw, ns, rs);
     }
     uint64_t recs = wave_sum64(rs.count);
     if (lane == 0) {
@@ -386,11 +642,12 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
       if (lane == 0) b.page_nn[pi] = 0;
       return;
     }
+    __syncthreads();
   }
   // ---- definition levels
   if (cd.max_def > 0) {
     for (uint32_t k = lane; k < kSegSlots / 32; k += 64) lds.bits[k] = 0;
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     uint32_t *vbits = (uint32_t *)cd.validity;
     LevelSink ds{base + pd.def_off,
                  pd.def_len,
@@ -404,9 +661,8 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
     if (!(pd.flags & PF_DEF)) {
       if (ns) ds.error(0, PQ_ERR_INVALID);
     } else {
-      hyb_walk(lds.walk, base + pd.def_off, pd.def_len, cd.def_bw, ns, ds);
+      lvl_decode(lds, base + pd.def_off, pd.def_len, cd.def_bw, ns, ds);
     }
-    __builtin_amdgcn_wave_barrier();
     __syncthreads();
     // flush the LDS bitmap segment to the chunk bitmap
     const uint32_t seg = min(ns, kSegSlots);
@@ -782,15 +1038,6 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
   return true;
 }
 
-DEV uint64_t wave_incl_scan64(uint64_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t y = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += y;
-  }
-  return v;
-}
 
 // bits at bit offset `bo` (< 2^32) of the LDS window, width <= 64
 DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
