@@ -132,6 +132,7 @@ DEV void report(const BatchDev &b, uint32_t chunk, uint32_t phase, uint32_t page
 //   bit-packed group starting at EOF      -> io.EOF (a short group zero-fills)
 // ---------------------------------------------------------------------------
 constexpr uint32_t kStage = 4096;
+constexpr uint32_t kSegSlots = 65536;  // bitmap slots staged in LDS per page
 
 struct WalkLDS {
   uint32_t stage[kStage / 4 + 8];
@@ -141,263 +142,30 @@ DEV uint32_t lds_ld32(const uint32_t *stg, uint32_t off) {
   uint32_t w = off >> 2, s = off & 3;
   return __builtin_amdgcn_alignbyte(stg[w + 1], stg[w], s);
 }
+DEV uint32_t sgpr(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// Restage [sb, sb+kStage) of the stream into LDS (bytes past n read as padding).
+// Stage stream bytes [sb, sb + kStage + 32) into LDS; bytes at or past n read as 0
+// (the zero fill of a short final bit-packed group, hybrid_decoder.go:132-140).
 DEV void stage_load(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n) {
   const uint32_t lane = lane_id();
   const uint8_t *src = s + sb;
-  const uint32_t lim = n > sb ? n - sb + 16 : 16;  // never read past the stream + 24 B (buffer pad is 64 B)
+  const uint32_t lim = n > sb ? n - sb : 0;
 #pragma unroll 4
-  for (uint32_t k = lane; k < kStage / 4 + 8; k += 64) stg[k] = 4 * k < lim ? ld32(src + 4 * k) : 0u;
+  for (uint32_t k = lane; k < kStage / 4 + 8; k += 64) {
+    uint32_t o = 4 * k;
+    stg[k] = o + 4 <= lim ? ld32(src + o) : (o < lim ? ld32(src + o) & ((1u << (8 * (lim - o))) - 1u) : 0u);
+  }
 }
 
-template <class Sink>
-__device__ __attribute__((noinline)) uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
-  const uint32_t lane = lane_id();
-  const uint32_t rs = (bw + 7) >> 3;
-  uint32_t pos = 0, done = 0;
-  uint32_t sb = 0;
-  stage_load(L.stage, s, 0, n);
-  __builtin_amdgcn_wave_barrier();
-  while (done < need) {
-    if (pos + 80 > sb + kStage) {
-      sb = pos & ~3u;
-      __builtin_amdgcn_wave_barrier();
-      stage_load(L.stage, s, sb, n);
-      __builtin_amdgcn_wave_barrier();
-    }
-    // ---- speculative header decode at c = pos + lane
-    const uint32_t c = pos + lane;
-    uint32_t err = 0, hl = 0, nvals = 0, okvals = 0, value = 0, adv = 0, bp = 0;
-    uint64_t h = 0;
-    if (c >= n) {
-      err = PQ_ERR_EOF;
-    } else {
-      uint32_t off = c - sb;
-      uint32_t w0 = lds_ld32(L.stage, off), w1 = lds_ld32(L.stage, off + 4), w2 = lds_ld32(L.stage, off + 8);
-      unsigned sh = 0;
-      bool term = false;
-      uint32_t k = 0;
-      for (; k < 12; k++) {
-        if (c + k >= n) { err = PQ_ERR_EOF; break; }
-        uint32_t wv = k < 4 ? w0 : (k < 8 ? w1 : w2);
-        uint32_t by = (wv >> (8 * (k & 3))) & 0xffu;
-        if (by < 0x80u) {
-          if (k > 9 || (k == 9 && by > 1)) err = PQ_ERR_RANGE;
-          else if (sh < 64) h |= (uint64_t)by << sh;
-          term = true;
-          break;
-        }
-        if (sh < 64) h |= (uint64_t)(by & 0x7f) << sh;
-        sh += 7;
-      }
-      if (!err && !term) {  // > 12-byte varint: Go keeps reading until a terminator (overflow) or EOF
-        err = PQ_ERR_EOF;
-        for (uint32_t q = c + 12; q < n; q++)
-          if (s[q] < 0x80) { err = PQ_ERR_RANGE; break; }
-      }
-      hl = k + 1;
-      if (!err && h > 0x7fffffffull) err = PQ_ERR_RANGE;
-      if (!err) {
-        uint32_t cnt = (uint32_t)(h >> 1);
-        bp = (uint32_t)(h & 1);
-        if (cnt == 0) err = PQ_ERR_INVALID;
-        uint32_t pay = c + hl;
-        if (!err && bp) {
-          uint64_t nv = (uint64_t)cnt * 8;
-          nvals = nv > 0x7fffffffull ? 0x7fffffffu : (uint32_t)nv;
-          uint64_t pb = (uint64_t)cnt * bw;
-          uint64_t a = hl + pb;
-          adv = a > 0x3fffffffull ? 0x3fffffffu : (uint32_t)a;
-          if ((uint64_t)pay + pb > n) {
-            uint64_t g = pay >= n ? 0 : ((uint64_t)(n - pay) + bw - 1) / bw;  // groups that start before EOF
-            uint64_t ok = g * 8;
-            okvals = ok > nvals ? nvals : (uint32_t)ok;
-          } else {
-            okvals = nvals;
-          }
-          value = pay;
-        } else if (!err) {
-          nvals = cnt;
-          okvals = cnt;
-          adv = hl + rs;
-          if (pay >= n) err = PQ_ERR_EOF;
-          else if (pay + rs > n) err = PQ_ERR_UNEXPECTED_EOF;
-          else {
-            uint32_t off2 = pay - sb;
-            uint32_t v = lds_ld32(L.stage, off2);
-            value = rs >= 4 ? v : (v & ((1u << (8 * rs)) - 1u));
-            if (bw < 32 && (value >> bw) != 0) err = PQ_ERR_INVALID;
-          }
-        }
-      }
-    }
-    // ---- follow the true chain (scalar)
-    uint64_t mask = 0;
-    uint32_t cum = 0, p = 0, next_pos = pos;
-    bool stop = false;
-    uint32_t stop_err = 0, stop_pos = 0;
-    for (;;) {
-      uint32_t e = rdlane(err, p);
-      if (e) { stop = true; stop_err = e; stop_pos = done + cum; break; }
-      uint32_t nv = rdlane(nvals, p), ok = rdlane(okvals, p);
-      mask |= 1ull << p;
-      uint32_t rem = need - done - cum;
-      if (ok < nv && ok < rem) { cum += ok; stop = true; stop_err = PQ_ERR_EOF; stop_pos = done + cum; break; }
-      if (nv >= rem) { cum += rem; stop = true; break; }
-      cum += nv;
-      uint32_t q = p + rdlane(adv, p);
-      if (q >= 64) { next_pos = pos + q; break; }
-      p = q;
-    }
-    // ---- expansion
-    const bool mine = (mask >> lane) & 1ull;
-    uint32_t first = wave_excl_scan(mine ? nvals : 0u);
-    uint32_t cnt = 0;
-    if (mine && first < cum) cnt = min(nvals, cum - first);
-    sink.window(mine && cnt > 0, done + first, cnt, bp != 0, value, c);
-    done += cum;
-    if (stop) {
-      if (stop_err) sink.error(stop_pos, stop_err);
-      break;
-    }
-    pos = next_pos;
-  }
-  return done;
+// bits at bit offset bo (relative to the stage start) of the LDS stage, width <= 64
+DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
+  if (w == 0) return 0;
+  uint32_t wi = bo >> 5, sh = bo & 31;
+  uint64_t lo = (uint64_t)win[wi] | ((uint64_t)win[wi + 1] << 32);
+  uint64_t x = lo >> sh;
+  if (sh && w > 64 - sh) x |= (uint64_t)win[wi + 2] << (64 - sh);
+  return w >= 64 ? x : x & ((1ull << w) - 1ull);
 }
-
-// ---------------------------------------------------------------------------
-// Level sink: rep/def levels -> uint8 levels, validity bits, counts.
-// decodePackedArray helpers.go:133-149 (notNull = count(level == maxD)).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSegSlots = 65536;  // bitmap slots staged in LDS per page
-
-
-struct LevelSink {
-  const uint8_t *s;
-  uint32_t n;  // stream length
-  uint32_t bw;
-  uint8_t *out;          // uint8 levels at page start, or null
-  uint32_t *bits_lds;    // LDS bitmap (page-relative slots [0, kSegSlots)) or null
-  uint32_t *bits_glob;   // global bitmap of the chunk (slot_base applied by caller) or null
-  uint64_t slot_base;    // chunk-relative slot of page start
-  uint32_t cmp;          // level value that counts (maxD for def, 0 for rep)
-  uint32_t count;        // lane-local count of (level == cmp)
-  uint32_t err_code, err_pos;
-
-  DEV void set_bits(uint32_t slot, uint64_t m, uint32_t nb) {
-    if (!m) return;
-    if (bits_lds && slot < kSegSlots && slot + nb > kSegSlots) {  // split at the LDS segment end
-      uint32_t lo = kSegSlots - slot;
-      set_bits(slot, m & ((1ull << lo) - 1ull), lo);
-      set_bits(kSegSlots, m >> lo, nb - lo);
-      return;
-    }
-    if (bits_lds && slot + nb <= kSegSlots) {
-      uint32_t w = slot >> 5, sh = slot & 31;
-      atomicOr(&bits_lds[w], (uint32_t)(m << sh));
-      uint64_t rest = sh ? (m >> (32 - sh)) : (m >> 32);
-      if (rest) {
-        atomicOr(&bits_lds[w + 1], (uint32_t)rest);
-        if (rest >> 32) atomicOr(&bits_lds[w + 2], (uint32_t)(rest >> 32));
-      }
-    } else if (bits_glob) {
-      uint64_t g = slot_base + slot;
-      uint32_t w = (uint32_t)(g >> 5), sh = (uint32_t)(g & 31);
-      atomicOr(&bits_glob[w], (uint32_t)(m << sh));
-      uint64_t rest = sh ? (m >> (32 - sh)) : (m >> 32);
-      if (rest) {
-        atomicOr(&bits_glob[w + 1], (uint32_t)rest);
-        if (rest >> 32) atomicOr(&bits_glob[w + 2], (uint32_t)(rest >> 32));
-      }
-    }
-  }
-
-  // Up to 64 values of one run starting at value k of the run.
-  DEV void piece(bool bp, uint32_t value, uint32_t pay, uint32_t slot, uint32_t k, uint32_t nb) {
-    uint64_t eq;
-    if (bp) {
-      if (bw == 1) {
-        uint64_t raw = nb > 56 ? (bits64c(s, n, (uint64_t)pay * 8 + k, 32) |
-                                  (bits64c(s, n, (uint64_t)pay * 8 + k + 32, nb - 32) << 32))
-                               : bits64c(s, n, (uint64_t)pay * 8 + k, nb);
-        eq = cmp ? raw : (~raw & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
-        if (out)
-          for (uint32_t j = 0; j < nb; j++) out[slot + j] = (uint8_t)((raw >> j) & 1);
-      } else {
-        eq = 0;
-        for (uint32_t j = 0; j < nb; j++) {
-          uint32_t lv = bits32c(s, n, (uint64_t)pay * 8 + (uint64_t)(k + j) * bw, bw);
-          if (out) out[slot + j] = (uint8_t)lv;
-          eq |= (uint64_t)(lv == cmp) << j;
-        }
-      }
-    } else {
-      eq = value == cmp ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1)) : 0;
-      if (out)
-        for (uint32_t j = 0; j < nb; j++) out[slot + j] = (uint8_t)value;
-    }
-    count += __popcll(eq);
-    set_bits(slot, eq, nb);
-  }
-
-  DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t) {
-    // short runs: one lane per run
-    if (active && cnt <= 64) piece(bp, value, value, first, 0, cnt);
-    // long runs: the whole wave, 64 values per lane-step
-    uint64_t big = __ballot(active && cnt > 64);
-    while (big) {
-      uint32_t r = __builtin_ctzll(big);
-      big &= big - 1;
-      uint32_t rf = rdlane(first, r), rc = rdlane(cnt, r), rv = rdlane(value, r);
-      bool rbp = rdlane(bp ? 1u : 0u, r) != 0;
-      for (uint32_t k = lane_id() * 64; k < rc; k += 64 * 64) {
-        uint32_t nb = min(64u, rc - k);
-        piece(rbp, rv, rv, rf + k, k, nb);
-      }
-    }
-  }
-  DEV void error(uint32_t pos, uint32_t code) {
-    if (!err_code) { err_code = code; err_pos = pos; }
-  }
-};
-
-// ---------------------------------------------------------------------------
-// Speculative segment decoder for LEVEL streams (short runs: a V2 def section of
-// 64K slots holds ~3,700 runs). The stream (<= kLvlStage bytes) is staged in LDS
-// and cut into 64 segments, one per lane.
-//  A. every lane follows the header chain from its segment start (as if a run
-//     header started there), marking each visited position inside its segment;
-//  B. every lane continues its chain past its segment until it reaches a position
-//     marked by a later lane (the chains have merged: "next header" is a function
-//     of the position alone) and records the positions it visited on the way;
-//  C. lane 0 starts at the true stream start, so the lanes reached by following
-//     merge targets from lane 0 are exactly the lanes whose chains are true;
-//  D. each true lane clears the (false) marks between its segment end and its
-//     merge point and sets its recorded positions: the marks are now exactly the
-//     run headers of the reference's sequential walk (hybrid_decoder.go:81-165);
-//  E. every lane decodes the runs whose headers lie in its segment; a wave scan
-//     of the per-lane value counts gives each run's first slot; runs are expanded
-//     into levels / validity bits (short runs per lane, long runs by the wave).
-// Streams larger than kLvlStage, or a true lane whose record list overflows, use
-// the windowed walker (hyb_walk). Errors are reported at the slot where the
-// reference's next() would fail, as in hyb_walk.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kLvlStage = 12288;  // bytes of a level stream decoded speculatively
-constexpr uint32_t kExtMax = 24;       // recorded chain positions per lane past its segment
-
-struct SpecLDS {
-  uint32_t stage[kLvlStage / 4 + 8];
-  uint32_t marks[kLvlStage / 32 + 4];
-  uint16_t ext[64][kExtMax];
-};
-struct LevelLDS {
-  union {
-    WalkLDS walk;
-    SpecLDS spec;
-  } u;
-  uint32_t bits[kSegSlots / 32];
-};
 
 struct Hdr {
   uint32_t err, nvals, okvals, value, adv, bp;
@@ -468,152 +236,160 @@ DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t 
   return r;
 }
 
-DEV bool mark_test(const uint32_t *m, uint32_t p) { return (m[p >> 5] >> (p & 31)) & 1u; }
 
-// Clear marks in [lo, hi).
-DEV void mark_clear(uint32_t *m, uint32_t lo, uint32_t hi) {
-  if (lo >= hi) return;
-  uint32_t w0 = lo >> 5, w1 = (hi - 1) >> 5;
-  for (uint32_t w = w0; w <= w1; w++) {
-    uint32_t keep = 0;
-    if (w == w0) keep |= (1u << (lo & 31)) - 1u;
-    if (w == w1 && ((hi & 31) != 0)) keep |= ~((1u << (hi & 31)) - 1u);
-    atomicAnd(&m[w], keep);
-  }
-}
-
-// Returns the number of values the stream supplied (< need only on error).
 template <class Sink>
-DEV uint32_t lvl_decode(LevelLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
-  if (need == 0) return 0;
-  if (n > kLvlStage) return hyb_walk(L.u.walk, s, n, bw, need, sink);
-  SpecLDS &S = L.u.spec;
+DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
   const uint32_t lane = lane_id();
+  n = sgpr(n);
+  bw = sgpr(bw);
+  need = sgpr(need);
   const uint32_t rs = (bw + 7) >> 3;
-  // ---- stage the whole stream, zero the marks
-  for (uint32_t k = lane; k < kLvlStage / 4 + 8; k += 64) {
-    uint32_t o = 4 * k;
-    S.stage[k] = o + 4 <= n ? ld32(s + o) : (o < n ? ld32(s + o) & ((1u << (8 * (n - o))) - 1u) : 0u);
-  }
-  const uint32_t nmw = (n + 31) / 32 + 2;
-  for (uint32_t k = lane; k < nmw; k += 64) S.marks[k] = 0;
+  uint32_t pos = 0, done = 0, sb = 0;
+  stage_load(L.stage, s, 0, n);
   __syncthreads();
-  const uint32_t seg = max(16u, (n + 63) / 64);
-  const uint32_t lo = lane * seg, hi = min(n, lo + seg);
-  const bool active = lo < n;
-  // ---- A: speculative chains inside the own segment
-  uint32_t p = lo;
-  if (active) {
-    while (p < hi) {
-      atomicOr(&S.marks[p >> 5], 1u << (p & 31));
-      Hdr h = decode_hdr(S.stage, 0, s, p, n, bw, rs);
-      p += h.err ? 1u : h.adv;
+  while (done < need) {
+    // keep the candidate headers (pos .. pos+76) and short-run payloads staged
+    if (pos + 208 > sb + kStage) {
+      sb = sgpr(pos & ~3u);
+      __syncthreads();
+      stage_load(L.stage, s, sb, n);
+      __syncthreads();
     }
-  }
-  __syncthreads();
-  // ---- B: continue past the segment until merging with a later lane's chain
-  uint32_t target = 64, conv = n, cnt = 0;
-  if (active) {
-    uint32_t q = p;
-    while (q < n) {
-      if (mark_test(S.marks, q)) { target = q / seg; conv = q; break; }
-      if (cnt < kExtMax) S.ext[lane][cnt] = (uint16_t)q;
-      cnt++;
-      Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
-      q += h.err ? 1u : h.adv;
+    // ---- speculative header decode at c = pos + lane
+    const uint32_t c = pos + lane;
+    const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+    // ---- follow the true chain lane to lane (scalar registers)
+    uint64_t mask = 0;
+    uint32_t cum = 0, p = 0, next_pos = pos;
+    uint32_t stop = 0, stop_err = 0, stop_pos = 0;
+    for (;;) {
+      const uint32_t e = rdlane(h.err, p);
+      if (e) { stop = 1; stop_err = e; stop_pos = done + cum; break; }
+      const uint32_t nv = rdlane(h.nvals, p), ok = rdlane(h.okvals, p);
+      mask |= 1ull << p;
+      const uint32_t rem = need - done - cum;
+      if (ok < nv && ok < rem) { cum += ok; stop = 1; stop_err = PQ_ERR_EOF; stop_pos = done + cum; break; }
+      if (nv >= rem) { cum += rem; stop = 1; break; }
+      cum += nv;
+      const uint32_t q = p + rdlane(h.adv, p);
+      if (q >= 64) { next_pos = pos + q; break; }
+      p = q;
     }
-  }
-  // ---- C: true lanes (scalar)
-  uint64_t tmask = 0;
-  bool overflow = false;
-  for (uint32_t t = 0; t < 64;) {
-    tmask |= 1ull << t;
-    if (rdlane(cnt, t) > kExtMax) overflow = true;
-    uint32_t nt = rdlane(target, t);
-    if (nt <= t) break;  // cannot happen (merge points lie past the lane's segment)
-    t = nt;
-  }
-  if (overflow) {
-    __syncthreads();
-    return hyb_walk(L.u.walk, s, n, bw, need, sink);
-  }
-  const bool is_true = (tmask >> lane) & 1ull;
-  // ---- D: patch marks between each true lane's segment end and its merge point
-  if (is_true && active) mark_clear(S.marks, hi, conv);
-  __syncthreads();
-  if (is_true && active)
-    for (uint32_t k = 0; k < cnt; k++) atomicOr(&S.marks[S.ext[lane][k] >> 5], 1u << (S.ext[lane][k] & 31));
-  __syncthreads();
-  // ---- E1: per-lane value counts up to the first error in chain order
-  uint32_t tvals = 0, ecode = 0;
-  const uint32_t mw0 = lo >> 5, mw1 = active ? (hi - 1) >> 5 : 0;
-  auto first_bits = [&](uint32_t w) -> uint32_t {
-    uint32_t m = S.marks[w];
-    if (w == mw0) m &= ~((1u << (lo & 31)) - 1u);
-    if (w == mw1 && (hi & 31)) m &= (1u << (hi & 31)) - 1u;
-    return m;
-  };
-  if (active) {
-    for (uint32_t w = mw0; w <= mw1 && !ecode; w++) {
-      uint32_t m = first_bits(w);
-      while (m) {
-        uint32_t q = w * 32 + __builtin_ctz(m);
-        m &= m - 1;
-        Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
-        if (h.err) { ecode = h.err; break; }
-        if (h.okvals < h.nvals) { tvals = min(0x7fffffffu, tvals + h.okvals); ecode = PQ_ERR_EOF; break; }
-        tvals = min(0x7fffffffu, tvals + h.nvals);
-      }
+    // ---- expansion
+    const bool mine = (mask >> lane) & 1ull;
+    const uint32_t first = wave_excl_scan(mine ? h.nvals : 0u);
+    uint32_t cnt = 0;
+    if (mine && first < cum) cnt = min(h.nvals, cum - first);
+    sink.window(mine && cnt > 0, done + first, cnt, h.bp != 0, h.value, c, L.stage, sb);
+    done = sgpr(done + cum);
+    if (stop) {
+      if (stop_err) sink.error(stop_pos, stop_err);
+      break;
     }
+    pos = sgpr(next_pos);
   }
-  const uint64_t emask = __ballot(ecode != 0);
-  const uint32_t elane = emask ? (uint32_t)__builtin_ctzll(emask) : 64u;
-  if (lane > elane) tvals = 0;
-  uint64_t incl = wave_incl_scan64(tvals);
-  const uint64_t start = incl - tvals;
-  const uint64_t total = __shfl(incl, 63, 64);
-  uint32_t eff = need;
-  if (elane < 64) {
-    uint64_t epos = __shfl(incl, (int)elane, 64);
-    uint32_t ec = rdlane(ecode, elane);
-    if (epos < need) { sink.error((uint32_t)epos, ec); eff = (uint32_t)epos; }
-  } else if (total < need) {
-    sink.error((uint32_t)total, PQ_ERR_EOF);  // the chain reached the stream end: next header is EOF
-    eff = (uint32_t)total;
-  }
-  // ---- E2: expansion
-  uint64_t slot = start;
-  uint32_t cw = mw0, cm = (active && lane <= elane) ? first_bits(mw0) : 0u;
-  bool more = active && lane <= elane;
-  for (;;) {
-    // next marked header of this lane
-    uint32_t q = 0;
-    bool have = false;
-    if (more) {
-      while (!cm && cw < mw1) cm = first_bits(++cw);
-      if (cm) {
-        q = cw * 32 + __builtin_ctz(cm);
-        cm &= cm - 1;
-        have = slot < eff;
-      }
-      if (!have) more = false;
-    }
-    if (!__ballot(have)) break;
-    uint32_t cnt2 = 0, value = 0;
-    bool bp = false;
-    if (have) {
-      Hdr h = decode_hdr(S.stage, 0, s, q, n, bw, rs);
-      cnt2 = (uint32_t)min((uint64_t)h.nvals, (uint64_t)eff - slot);
-      bp = h.bp != 0;
-      value = h.value;
-    }
-    sink.window(have && cnt2 > 0, (uint32_t)slot, cnt2, bp, value, q);
-    slot += cnt2;
-  }
-  return (uint32_t)min((uint64_t)eff, total);
+  return done;
 }
 
-// One wave per page with level streams (rep and/or def).
+// ---------------------------------------------------------------------------
+// Level sink: rep/def levels -> uint8 levels, validity bits, counts.
+// decodePackedArray helpers.go:133-149 (notNull = count(level == maxD)).
+// ---------------------------------------------------------------------------
+struct LevelSink {
+  const uint8_t *s;
+  uint32_t n;            // stream length
+  uint32_t bw;
+  uint8_t *out;          // uint8 levels at page start, or null
+  uint32_t *bits_lds;    // LDS bitmap (page-relative slots [0, kSegSlots)) or null
+  uint32_t *bits_glob;   // global bitmap of the chunk (slot_base applied by caller) or null
+  uint64_t slot_base;    // chunk-relative slot of page start
+  uint32_t cmp;          // level value that counts (maxD for def, 0 for rep)
+  uint32_t count;        // lane-local count of (level == cmp)
+  uint32_t err_code, err_pos;
+
+  DEV static void or_bits(uint32_t *dst, uint64_t g, uint64_t m) {
+    if (!m) return;
+    uint32_t w = (uint32_t)(g >> 5), sh = (uint32_t)(g & 31);
+    atomicOr(&dst[w], (uint32_t)(m << sh));
+    uint64_t rest = sh ? (m >> (32 - sh)) : (m >> 32);
+    if (rest) {
+      atomicOr(&dst[w + 1], (uint32_t)rest);
+      if (rest >> 32) atomicOr(&dst[w + 2], (uint32_t)(rest >> 32));
+    }
+  }
+  // bits [slot, slot+nb) of the page: LDS segment for slots < kSegSlots, chunk bitmap beyond
+  DEV void set_bits(uint32_t slot, uint64_t m, uint32_t nb) {
+    if (!m) return;
+    if (!bits_lds) {
+      if (bits_glob) or_bits(bits_glob, slot_base + slot, m);
+      return;
+    }
+    if (slot + nb <= kSegSlots) { or_bits(bits_lds, slot, m); return; }
+    if (slot >= kSegSlots) { or_bits(bits_glob, slot_base + slot, m); return; }
+    const uint32_t lo = kSegSlots - slot;  // split at the LDS segment end
+    or_bits(bits_lds, slot, m & ((1ull << lo) - 1ull));
+    or_bits(bits_glob, slot_base + kSegSlots, m >> lo);
+  }
+
+  // Up to 64 values of one run, starting at value k of the run. `stg`/`sb`: the LDS stage.
+  DEV void piece(bool bp, uint32_t value, uint32_t slot, uint32_t k, uint32_t nb, const uint32_t *stg, uint32_t sb) {
+    uint64_t eq;
+    if (bp) {
+      const uint64_t bo = (uint64_t)value * 8 + (uint64_t)k * bw;   // stream bit offset
+      const uint64_t be = bo + (uint64_t)nb * bw;
+      const bool staged = stg && value >= sb && be + 64 <= (uint64_t)(sb + kStage) * 8;
+      if (bw == 1) {
+        uint64_t raw;
+        if (staged) raw = lds_bits64(stg, (uint32_t)(bo - (uint64_t)sb * 8), nb);
+        else raw = nb > 56 ? (bits64c(s, n, bo, 32) | (bits64c(s, n, bo + 32, nb - 32) << 32)) : bits64c(s, n, bo, nb);
+        eq = cmp ? raw : (~raw & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
+        if (out)
+          for (uint32_t j = 0; j < nb; j++) out[slot + j] = (uint8_t)((raw >> j) & 1);
+      } else {
+        eq = 0;
+        for (uint32_t j = 0; j < nb; j++) {
+          const uint64_t b0 = bo + (uint64_t)j * bw;
+          uint32_t lv = staged ? (uint32_t)lds_bits64(stg, (uint32_t)(b0 - (uint64_t)sb * 8), bw) : bits32c(s, n, b0, bw);
+          if (out) out[slot + j] = (uint8_t)lv;
+          eq |= (uint64_t)(lv == cmp) << j;
+        }
+      }
+    } else {
+      eq = value == cmp ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1)) : 0;
+      if (out)
+        for (uint32_t j = 0; j < nb; j++) out[slot + j] = (uint8_t)value;
+    }
+    count += __popcll(eq);
+    set_bits(slot, eq, nb);
+  }
+
+  DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t, const uint32_t *stg,
+                  uint32_t sb) {
+    // short runs: one lane per run
+    if (active && cnt <= 64) piece(bp, value, first, 0, cnt, stg, sb);
+    // long runs: the whole wave, 64 values per lane-step (payload read from global memory)
+    uint64_t big = __ballot(active && cnt > 64);
+    while (big) {
+      const uint32_t r = __builtin_ctzll(big);
+      big &= big - 1;
+      const uint32_t rf = rdlane(first, r), rc = rdlane(cnt, r), rv = rdlane(value, r);
+      const bool rbp = rdlane(bp ? 1u : 0u, r) != 0;
+      for (uint32_t k = lane_id() * 64; k < rc; k += 64 * 64) piece(rbp, rv, rf + k, k, min(64u, rc - k), nullptr, 0);
+    }
+  }
+  DEV void error(uint32_t pos, uint32_t code) {
+    if (!err_code) { err_code = code; err_pos = pos; }
+  }
+};
+
+struct LevelLDS {
+  WalkLDS walk;
+  uint32_t bits[kSegSlots / 32];
+};
+
+// One wave per page with level streams: repetition levels (counted: records start
+// where rep == 0), then definition levels (validity bitmap built in LDS, flushed with
+// coalesced stores). One call site of the walker for both streams.
 // Reference: page_v1.go:42-48 / page_v2.go:40-46 readValues -> decodePackedArray.
 __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages) {
   __shared__ LevelLDS lds;
@@ -623,46 +399,47 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
   const uint8_t *base = (const uint8_t *)pd.data;
   const uint32_t lane = lane_id();
   const uint32_t ns = pd.num_slots;
-
-  // ---- repetition levels (counted: records start where rep == 0)
-  if (cd.max_rep > 0) {
-    LevelSink rs{base + pd.rep_off, pd.rep_len, (uint32_t)cd.rep_bw, (uint8_t *)cd.rep_levels + pd.slot_base, nullptr,
-                 nullptr, pd.slot_base, 0u, 0u, 0u, 0u};
-    if (!(pd.flags & PF_REP)) {
-      if (ns) rs.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
-    } else {
-      lvl_decode(lds, base + pd.rep_off, pd.rep_len, cd.rep_bw, ns, rs);
-    }
-    uint64_t recs = wave_sum64(rs.count);
-    if (lane == 0) {
-      b.page_rec[pi] = (uint32_t)recs;
-      if (rs.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_REP, rs.err_pos, rs.err_code);
-    }
-    if (rs.err_code) {
-      if (lane == 0) b.page_nn[pi] = 0;
-      return;
-    }
+  uint32_t *vbits = (uint32_t *)cd.validity;
+  for (uint32_t k = lane; k < kSegSlots / 32; k += 64) lds.bits[k] = 0;
+  uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
+  for (uint32_t which = 0; which < 2; which++) {
+    const bool rep = which == 0;
+    if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
+    LevelSink sk;
+    sk.s = base + (rep ? pd.rep_off : pd.def_off);
+    sk.n = rep ? pd.rep_len : pd.def_len;
+    sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+    sk.out = rep ? (uint8_t *)cd.rep_levels + pd.slot_base
+                 : (cd.def_levels ? (uint8_t *)cd.def_levels + pd.slot_base : nullptr);
+    sk.bits_lds = rep ? nullptr : lds.bits;
+    sk.bits_glob = rep ? nullptr : vbits;
+    sk.slot_base = pd.slot_base;
+    sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
+    sk.count = 0;
+    sk.err_code = 0;
+    sk.err_pos = 0;
     __syncthreads();
+    if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+      if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+    } else {
+      hyb_walk(lds.walk, sk.s, sk.n, sk.bw, ns, sk);
+    }
+    const uint64_t cntv = wave_sum64(sk.count);
+    if (sk.err_code) {
+      if (lane == 0) {
+        report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
+        b.page_nn[pi] = 0;
+        if (rep) b.page_rec[pi] = (uint32_t)cntv;
+      }
+      return;  // the reference fails the page at the first level error
+    }
+    if (rep) {
+      if (lane == 0) b.page_rec[pi] = (uint32_t)cntv;
+    } else {
+      nn = (uint32_t)cntv;
+    }
   }
-  // ---- definition levels
   if (cd.max_def > 0) {
-    for (uint32_t k = lane; k < kSegSlots / 32; k += 64) lds.bits[k] = 0;
-    __syncthreads();
-    uint32_t *vbits = (uint32_t *)cd.validity;
-    LevelSink ds{base + pd.def_off,
-                 pd.def_len,
-                 (uint32_t)cd.def_bw,
-                 cd.def_levels ? (uint8_t *)cd.def_levels + pd.slot_base : nullptr,
-                 lds.bits,
-                 vbits,
-                 pd.slot_base,
-                 (uint32_t)cd.max_def,
-                 0u, 0u, 0u};
-    if (!(pd.flags & PF_DEF)) {
-      if (ns) ds.error(0, PQ_ERR_INVALID);
-    } else {
-      lvl_decode(lds, base + pd.def_off, pd.def_len, cd.def_bw, ns, ds);
-    }
     __syncthreads();
     // flush the LDS bitmap segment to the chunk bitmap
     const uint32_t seg = min(ns, kSegSlots);
@@ -675,22 +452,14 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
       if (sh == 0) {
         if (k == 0 || k == nw - 1) atomicOr(&vbits[w0 + k], v);
         else vbits[w0 + k] = v;
-      } else {
-        if (v) {
-          atomicOr(&vbits[w0 + k], v << sh);
-          uint32_t hi = v >> (32 - sh);
-          if (hi) atomicOr(&vbits[w0 + k + 1], hi);
-        }
+      } else if (v) {
+        atomicOr(&vbits[w0 + k], v << sh);
+        uint32_t hi = v >> (32 - sh);
+        if (hi) atomicOr(&vbits[w0 + k + 1], hi);
       }
     }
-    uint64_t nn = wave_sum64(ds.count);
-    if (lane == 0) {
-      if (ds.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_DEF, ds.err_pos, ds.err_code);
-      b.page_nn[pi] = ds.err_code ? 0u : (uint32_t)nn;
-    }
-  } else if (lane == 0) {
-    b.page_nn[pi] = ns;  // constDecoder(0) == maxD(0): every slot is a value
   }
+  if (lane == 0) b.page_nn[pi] = nn;
 }
 
 // ---------------------------------------------------------------------------
@@ -740,7 +509,8 @@ struct RunSink {
   uint32_t stream_base;  // not used
   uint32_t err_code, err_pos;
 
-  DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t c) {
+  DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t c, const uint32_t *,
+                  uint32_t) {
     uint64_t m = __ballot(active);
     uint32_t rank = __popcll(m & ((1ull << lane_id()) - 1ull));
     if (active) {
@@ -1039,15 +809,6 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
 }
 
 
-// bits at bit offset `bo` (< 2^32) of the LDS window, width <= 64
-DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
-  if (w == 0) return 0;
-  uint32_t wi = bo >> 5, sh = bo & 31;
-  uint64_t lo = (uint64_t)win[wi] | ((uint64_t)win[wi + 1] << 32);
-  uint64_t x = lo >> sh;
-  if (sh && w > 64 - sh) x |= (uint64_t)win[wi + 2] << (64 - sh);
-  return w >= 64 ? x : x & ((1ull << w) - 1ull);
-}
 
 DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                   DeltaLDS &L) {
