@@ -209,8 +209,8 @@ struct KernelTimer {
   struct Rec { int slot; hipEvent_t a, b; };
   std::vector<Rec> recs;          // pending launch records
   std::vector<hipEvent_t> pool;   // free events
-  double total_ms[8] = {0};
-  int64_t launches[8] = {0};
+  double total_ms[9] = {0};
+  int64_t launches[9] = {0};
   hipEvent_t get() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e = nullptr;
@@ -234,8 +234,8 @@ struct KernelTimer {
     pool.clear();
   }
 };
-static const char *kTimerNames[8] = {"k_levels", "k_values", "k_scan_runs", "k_bases",
-                                     "k_dict_ba", "k_ba_offsets", "k_ba_gather", "k_records"};
+static const char *kTimerNames[9] = {"k_levels", "k_values", "k_scan_runs", "k_bases", "k_dict_ba",
+                                     "k_ba_offsets", "k_ba_gather", "k_records", "k_values"};
 
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
@@ -264,6 +264,7 @@ struct pqgpu_batch {
            o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
+  uint32_t n_delta_items = 0;
   std::vector<ChunkDesc> chunk_desc;
   bool uploaded = false, decoded = false;
   pqgpu_batch_stats stats{};
@@ -655,6 +656,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_begin = b->o_err;
   b->o_tile_first = take(b->tile_total * 4);
   b->f_end = a;
+  // DELTA pages first (long-running, latency-bound work items), then the bandwidth-bound tiles
+  std::stable_sort(b->items.begin(), b->items.end(), [](const WorkItem &x, const WorkItem &y) {
+    return (x.kind == WI_DELTA) > (y.kind == WI_DELTA);
+  });
+  b->n_delta_items = 0;
+  for (auto &it : b->items) b->n_delta_items += it.kind == WI_DELTA;
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
   b->o_chunks = take((uint64_t)nc * sizeof(ChunkDesc));
@@ -842,7 +849,14 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
   HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
   HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
-  HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l, s); }), err);
+  {  // DELTA work items and the other value work items as two launches (separately profiled)
+    LaunchLists l1 = l, l2 = l;
+    l1.n_items = b->n_delta_items;
+    l2.items = l.items + b->n_delta_items;
+    l2.n_items = l.n_items - b->n_delta_items;
+    HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l1, s); }), err);
+    HIPCHECK(timed(b, 8, s, [&] { return launch_values(d, l2, s); }), err);
+  }
   if (!b->ba_chunks.empty()) {
     HIPCHECK(timed(b, 5, s, [&] {
                return launch_ba_offsets_impl(d, l.ba_chunks, l.n_ba_chunks, (const uint64_t *)(A + b->o_ba_tile_off),
@@ -1277,7 +1291,7 @@ int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable) {
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
   b->timer.resolve();
   b->timer.enabled = enable != 0;
-  for (int k = 0; k < 8; k++) { b->timer.total_ms[k] = 0; b->timer.launches[k] = 0; }
+  for (int k = 0; k < 9; k++) { b->timer.total_ms[k] = 0; b->timer.launches[k] = 0; }
   return PQ_OK;
 }
 
@@ -1286,7 +1300,7 @@ int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, c
   b->timer.resolve();
   const KernelTimer &t = b->timer;
   int best = -1;
-  for (int k = 0; k < 8; k++)
+  for (int k = 0; k < 9; k++)
     if (t.launches[k] && (best < 0 || t.total_ms[k] > t.total_ms[best])) best = k;
   if (best < 0) {
     if (avg_ms) *avg_ms = 0;

@@ -365,10 +365,12 @@ struct LevelSink {
 
   DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t, const uint32_t *stg,
                   uint32_t sb) {
-    // short runs: one lane per run
-    if (active && cnt <= 64) piece(bp, value, first, 0, cnt, stg, sb);
-    // long runs: the whole wave, 64 values per lane-step (payload read from global memory)
-    uint64_t big = __ballot(active && cnt > 64);
+    // runs up to 4096 values: the owning lane, 64 values per step (payload from the LDS stage)
+    const bool mine = active && cnt <= 4096;
+    for (uint32_t k = 0; __ballot(mine && k < cnt); k += 64)
+      if (mine && k < cnt) piece(bp, value, first + k, k, min(64u, cnt - k), stg, sb);
+    // longer runs: the whole wave, 64 values per lane-step (payload read from global memory)
+    uint64_t big = __ballot(active && cnt > 4096);
     while (big) {
       const uint32_t r = __builtin_ctzll(big);
       big &= big - 1;
