@@ -167,6 +167,13 @@ DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
   return w >= 64 ? x : x & ((1ull << w) - 1ull);
 }
 
+constexpr uint32_t kErrLongVarint = 15;  // internal: varint longer than 12 bytes, resolved lazily
+DEV uint32_t resolve_long_varint(const uint8_t *s, uint32_t c, uint32_t n) {
+  for (uint32_t q = c + 12; q < n; q++)
+    if (s[q] < 0x80) return PQ_ERR_RANGE;
+  return PQ_ERR_EOF;
+}
+
 struct Hdr {
   uint32_t err, nvals, okvals, value, adv, bp;
 };
@@ -195,11 +202,10 @@ DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t 
     if (sh < 64) h |= (uint64_t)(by & 0x7f) << sh;
     sh += 7;
   }
-  if (!r.err && !term) {  // > 12-byte varint: Go keeps reading until a terminator (overflow) or EOF
-    r.err = PQ_ERR_EOF;
-    for (uint32_t q = c + 12; q < n; q++)
-      if (s[q] < 0x80) { r.err = PQ_ERR_RANGE; break; }
-  }
+  // > 12-byte varint: Go keeps reading until a terminator (overflow) or EOF. Only a header
+  // the walker actually reaches needs the answer (resolve_long_varint); speculative
+  // candidates inside bit-packed payloads (0xFF bytes) must not scan memory.
+  if (!r.err && !term) r.err = kErrLongVarint;
   const uint32_t hl = k + 1;
   if (!r.err && h > 0x7fffffffull) r.err = PQ_ERR_RANGE;
   if (r.err) return r;
@@ -263,7 +269,8 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
     uint32_t cum = 0, p = 0, next_pos = pos;
     uint32_t stop = 0, stop_err = 0, stop_pos = 0;
     for (;;) {
-      const uint32_t e = rdlane(h.err, p);
+      uint32_t e = rdlane(h.err, p);
+      if (e == kErrLongVarint) e = sgpr(resolve_long_varint(s, pos + p, n));
       if (e) { stop = 1; stop_err = e; stop_pos = done + cum; break; }
       const uint32_t nv = rdlane(h.nvals, p), ok = rdlane(h.okvals, p);
       mask |= 1ull << p;
@@ -812,6 +819,48 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
 
 
 
+// delta_hdr over the LDS window (stream bytes [win0, ...) in `win`), dword reads only.
+DEV bool delta_hdr_lds(const uint32_t *win, uint32_t win0, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64,
+                       uint32_t mbc, int64_t *min_delta, uint8_t *w, uint32_t *hdr_len, uint32_t *err) {
+  const uint32_t off = pos - win0;
+  uint32_t b[4] = {lds_ld32(win, off), lds_ld32(win, off + 4), lds_ld32(win, off + 8), lds_ld32(win, off + 12)};
+  uint64_t x = 0;
+  unsigned sh = 0;
+  uint32_t k = 0;
+  for (;; k++) {
+    if (pos + k >= n) { *err = PQ_ERR_EOF; return false; }
+    if (k == 10) {  // Go keeps reading: a later terminator is an overflow, none is EOF
+      *err = resolve_long_varint(gs, pos - 2, n) == PQ_ERR_RANGE ? PQ_ERR_RANGE : PQ_ERR_EOF;
+      return false;
+    }
+    uint32_t by = (b[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    if (by < 0x80) {
+      if (k == 9 && by > 1) { *err = PQ_ERR_RANGE; return false; }
+      if (sh < 64) x |= (uint64_t)by << sh;
+      break;
+    }
+    if (sh < 64) x |= (uint64_t)(by & 0x7f) << sh;
+    sh += 7;
+  }
+  int64_t v = (int64_t)(x >> 1);
+  if (x & 1) v = ~v;
+  if (!is64 && (v > 2147483647ll || v < -2147483648ll)) { *err = PQ_ERR_RANGE; return false; }
+  *min_delta = v;
+  const uint32_t p = pos + k + 1;
+  if (p >= n && mbc > 0) { *err = PQ_ERR_EOF; return false; }
+  if (p + mbc > n) { *err = PQ_ERR_UNEXPECTED_EOF; return false; }
+  for (uint32_t i = 0; i < mbc; i += 4) {
+    uint32_t ww = lds_ld32(win, p - win0 + i);
+    for (uint32_t j = 0; j < 4 && i + j < mbc; j++) {
+      uint32_t wi = (ww >> (8 * j)) & 0xffu;
+      if (wi > (is64 ? 64u : 32u)) { *err = PQ_ERR_INVALID; return false; }
+      w[i + j] = (uint8_t)wi;
+    }
+  }
+  *hdr_len = k + 1 + mbc;
+  return true;
+}
+
 DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                   DeltaLDS &L) {
   if (nn == 0) return;
@@ -856,8 +905,8 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
         if (hdr + 10 + mbc > wend && wend < n) break;  // header not entirely staged: next window
         uint32_t hl = 0, e = 0;
         int64_t md;
-        // parse from LDS: bytes past n read as 0 but delta_hdr bounds-checks against n
-        if (!delta_hdr(wb - win0, s, n, hdr, is64, mbc, &md, L.mb_w[nb], &hl, &e)) {
+        // parse from the LDS window with typed dword reads (bounds-checked against n)
+        if (!delta_hdr_lds(L.win, win0, s, n, hdr, is64, mbc, &md, L.mb_w[nb], &hl, &e)) {
           L.err_code = e;
           L.err_pos = (blk + nb) * bs;
           L.stop_val = L.err_pos;
