@@ -880,7 +880,6 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   const uint32_t max_blk = 10 + mbc + bs * 8;       // upper bound of one block's bytes (widths <= 64)
   uint32_t win0 = 0xffffffffu;
   uint32_t blk = 0;                                 // index of the next block
-  uint8_t *wb = (uint8_t *)L.win;
   while ((uint64_t)blk * bs < limit) {
     // ---- (re)stage the window so that it starts at the next header
     if (win0 == 0xffffffffu || (hdr + max_blk > win0 + kDeltaWin && win0 + kDeltaWin < n)) {
