@@ -198,6 +198,9 @@ int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values,
                            uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
                            pqgpu_error *err);
 int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out);
+/* Diagnostics: 64 device counters filled by in-kernel phase stamps when the
+ * environment has PQ_DEBUG_STAMPS=1 at upload time. */
+int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
 
 /* Timing hook for the benchmark: average duration (ms) of the dominant
  * decode kernel over the last `pqgpu_batch_decode` calls, measured with HIP

@@ -10,6 +10,7 @@
 // missing, pqgpu_ctx_create fails with PQ_ERR_HIP.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
 
@@ -265,6 +266,8 @@ struct pqgpu_batch {
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   uint32_t n_delta_items = 0;
+  uint64_t o_dbg = 0;
+  bool debug_stamps = getenv("PQ_DEBUG_STAMPS") && atoi(getenv("PQ_DEBUG_STAMPS")) != 0;
   std::vector<ChunkDesc> chunk_desc;
   bool uploaded = false, decoded = false;
   pqgpu_batch_stats stats{};
@@ -675,6 +678,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_tile_sum = take(b->ba_tiles_total * 4);
   b->o_ba_tile_off = take(b->ba_tile_off.size() * 8);
   b->o_ba_totals = take(b->ba_chunks.size() * 8);
+  b->o_dbg = take(64 * 8);
   b->l_level = take(b->level_pages.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
   b->l_base = take(b->base_chunks.size() * 4);
@@ -755,6 +759,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
   HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
   HIPCHECK(up(b->o_nn, b->page_nn_init.data(), np * 4), err);
+  HIPCHECK(hipMemsetAsync(A + b->o_dbg, 0, 64 * 8, s), err);
   HIPCHECK(up(b->o_tile_base, b->tile_base.data(), np * 8), err);
   HIPCHECK(up(b->o_items, b->items.data(), b->items.size() * sizeof(WorkItem)), err);
   HIPCHECK(up(b->o_ba_tile_off, b->ba_tile_off.data(), b->ba_tile_off.size() * 8), err);
@@ -790,6 +795,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.tile_first = (uint32_t *)(A + b->o_tile_first);
   d.tile_base = (const uint64_t *)(A + b->o_tile_base);
   d.ba_tile_sum = (uint32_t *)(A + b->o_ba_tile_sum);
+  d.dbg = b->debug_stamps ? (unsigned long long *)(A + b->o_dbg) : nullptr;
   d.npages = (uint32_t)b->pages.size();
   d.nchunks = (uint32_t)b->chunks.size();
   return d;
@@ -1279,6 +1285,15 @@ int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32
   HIPCHECK(cp(rep_levels, r.rep_levels, (size_t)r.num_slots), err);
   HIPCHECK(cp(validity, r.validity, (size_t)((r.num_slots + 31) / 32) * 4), err);
   HIPCHECK(cp(list_offsets, r.list_offsets, r.list_offsets ? (size_t)(r.num_records + 1) * 4 : 0), err);
+  return PQ_OK;
+}
+
+int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset) {
+  if (!b->ctx || !b->d_arena) return PQ_ERR_ARG;
+  (void)hipSetDevice(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  if (hipMemcpy(out64, b->d_arena + b->o_dbg, 64 * 8, hipMemcpyDeviceToHost) != hipSuccess) return PQ_ERR_HIP;
+  if (reset) (void)hipMemset(b->d_arena + b->o_dbg, 0, 64 * 8);
   return PQ_OK;
 }
 

@@ -22,6 +22,7 @@ struct BatchDev {
   uint32_t *tile_first;           // dict tiles: first run index per tile
   const uint64_t *tile_base;      // [npages] first tile-table entry per page
   uint32_t *ba_tile_sum;          // BYTE_ARRAY: per 4096-value tile payload sum
+  unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
 };
 

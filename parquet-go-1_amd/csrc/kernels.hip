@@ -82,6 +82,21 @@ DEV uint64_t bits64c(const uint8_t *p, uint32_t n, uint64_t bo, uint32_t nb) {  
 }
 
 DEV uint32_t lane_id() { return __lane_id(); }
+
+// Diagnostic phase stamps (PQ_DEBUG_STAMPS=1 only): per-wave cycle sums added to b.dbg.
+DEV uint64_t stamp() { return __builtin_amdgcn_s_memtime(); }
+struct Stamps {
+  unsigned long long *dbg;
+  uint64_t t, acc[8];
+  DEV void begin() { if (dbg) t = stamp(); }
+  DEV void lap(int k) {
+    if (dbg) { uint64_t n = stamp(); acc[k] += n - t; t = n; }
+  }
+  DEV void flush(int base) {
+    if (dbg && __lane_id() == 0)
+      for (int k = 0; k < 8; k++) if (acc[k]) atomicAdd(&dbg[base + k], (unsigned long long)acc[k]);
+  }
+};
 DEV uint32_t rdlane(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
 DEV uint32_t wave_excl_scan(uint32_t v) {
@@ -244,7 +259,8 @@ DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t 
 
 
 template <class Sink>
-DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
+DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink,
+                      Stamps *st = nullptr) {
   const uint32_t lane = lane_id();
   n = sgpr(n);
   bw = sgpr(bw);
@@ -255,15 +271,18 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
   __syncthreads();
   while (done < need) {
     // keep the candidate headers (pos .. pos+76) and short-run payloads staged
+    if (st) st->lap(7);
     if (pos + 208 > sb + kStage) {
       sb = sgpr(pos & ~3u);
       __syncthreads();
       stage_load(L.stage, s, sb, n);
       __syncthreads();
+      if (st) { st->lap(0); st->acc[5]++; }
     }
     // ---- speculative header decode at c = pos + lane
     const uint32_t c = pos + lane;
     const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+    if (st) { (void)__builtin_amdgcn_readfirstlane(h.err + h.adv + h.nvals); st->lap(1); st->acc[6]++; }
     // ---- follow the true chain lane to lane (scalar registers)
     uint64_t mask = 0;
     uint32_t cum = 0, p = 0, next_pos = pos;
@@ -282,12 +301,15 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
       if (q >= 64) { next_pos = pos + q; break; }
       p = q;
     }
+    if (st) st->lap(2);
     // ---- expansion
     const bool mine = (mask >> lane) & 1ull;
     const uint32_t first = wave_excl_scan(mine ? h.nvals : 0u);
     uint32_t cnt = 0;
     if (mine && first < cum) cnt = min(h.nvals, cum - first);
+    if (st) st->lap(3);
     sink.window(mine && cnt > 0, done + first, cnt, h.bp != 0, h.value, c, L.stage, sb);
+    if (st) st->lap(4);
     done = sgpr(done + cum);
     if (stop) {
       if (stop_err) sink.error(stop_pos, stop_err);
@@ -431,7 +453,10 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
     if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
       if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
     } else {
-      hyb_walk(lds.walk, sk.s, sk.n, sk.bw, ns, sk);
+      Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+      st.begin();
+      hyb_walk(lds.walk, sk.s, sk.n, sk.bw, ns, sk, b.dbg ? &st : nullptr);
+      st.flush(0);
     }
     const uint64_t cntv = wave_sum64(sk.count);
     if (sk.err_code) {
@@ -880,6 +905,8 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   const uint32_t max_blk = 10 + mbc + bs * 8;       // upper bound of one block's bytes (widths <= 64)
   uint32_t win0 = 0xffffffffu;
   uint32_t blk = 0;                                 // index of the next block
+  Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+  st.begin();
   while ((uint64_t)blk * bs < limit) {
     // ---- (re)stage the window so that it starts at the next header
     if (win0 == 0xffffffffu || (hdr + max_blk > win0 + kDeltaWin && win0 + kDeltaWin < n)) {
@@ -893,6 +920,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
         L.win[k] = v;
       }
       __syncthreads();
+      st.lap(0);
     }
     // ---- header walk (thread 0), inside the window
     if (tid == 0) {
@@ -925,6 +953,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
       L.next_hdr = hdr;
     }
     __syncthreads();
+    st.lap(1);
     hdr = L.next_hdr;
     const uint32_t nb = L.nblocks;
     uint32_t stop = L.stop_val;
@@ -961,6 +990,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     }
     if (gerr) atomicMin(&L.stop_val, gerr_pos);
     __syncthreads();
+    st.lap(2);
     const uint32_t stop2 = L.stop_val;
     if (gerr && gerr_pos == stop2 && stop2 < stop) { L.err_code = gerr; L.err_pos = gerr_pos; }
     stop = stop2;
@@ -976,6 +1006,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
       total += t;
     }
     uint64_t run = carry + before + incl - contrib;
+    st.lap(3);
     if (valid && d0 < stop) {
       uint64_t out[8];
 #pragma unroll
@@ -1012,12 +1043,17 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     }
     carry += total;
     blk += nb;
+    st.lap(4);
+    st.acc[5]++;
     __syncthreads();
+    st.lap(6);
     if (L.err_code || stop < limit || nb == 0) {
+      st.flush(8);
       if (tid == 0 && L.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, L.err_pos, L.err_code);
       return;
     }
   }
+  st.flush(8);
   if (final_err && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, final_pos, final_err);
 }
 

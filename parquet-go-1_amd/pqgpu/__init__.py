@@ -82,6 +82,7 @@ _EXPORTS = [
     "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
     "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
+    "pqgpu_batch_debug_counters",
 ]
 
 
@@ -122,6 +123,7 @@ def lib():
         "pqgpu_batch_copy_chunk": ([P, ctypes.c_int32, P, P, P, P, P, P, P, E], ctypes.c_int),
         "pqgpu_batch_stats_get": ([P, ctypes.POINTER(BatchStats)], ctypes.c_int),
         "pqgpu_batch_kernel_timing": ([P, ctypes.c_int], ctypes.c_int),
+        "pqgpu_batch_debug_counters": ([P, P, ctypes.c_int], ctypes.c_int),
         "pqgpu_batch_kernel_time": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                      ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
     }
@@ -310,6 +312,11 @@ class Batch:
         s = BatchStats()
         lib().pqgpu_batch_stats_get(self._h, ctypes.byref(s))
         return s
+
+    def debug_counters(self, reset=True):
+        out = np.zeros(64, np.uint64)
+        lib().pqgpu_batch_debug_counters(self._h, out.ctypes.data_as(ctypes.c_void_p), int(reset))
+        return out
 
     def kernel_timing(self, enable=True):
         lib().pqgpu_batch_kernel_timing(self._h, int(enable))

@@ -1,0 +1,36 @@
+"""Diagnostic: per-phase cycle counters of k_levels and the DELTA values path (PQ_DEBUG_STAMPS=1)."""
+import os
+import sys
+import time
+os.environ["PQ_DEBUG_STAMPS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
+import bench  # noqa: E402
+import pqgpu  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4 * 4194304
+data, _ = bench.gen_cfg2(rows)
+ctx = pqgpu.Context(0)
+f = pqgpu.File(data)
+b = pqgpu.Batch(ctx)
+for rg in range(f.num_row_groups):
+    for c in range(f.num_columns):
+        b.add_file_chunk(f, rg, c)
+b.upload()
+b.decode(); b.sync()
+b.debug_counters(reset=True)
+t0 = time.perf_counter()
+b.decode(); b.sync()
+dt = time.perf_counter() - t0
+d = b.debug_counters()
+pages = f.num_row_groups * 64 * 2
+print(f"decode {dt*1e3:.3f} ms for {rows} rows; {pages} level pages, {pages//2} DELTA pages")
+names = ["restage", "decode_hdr", "hop_loop", "scan", "sink_window", "restages#", "windows#", "loop_top"]
+for k, n in enumerate(names):
+    v = int(d[k])
+    print(f"levels {n:12s} total {v:>14d}  per page {v / pages:>12.1f}")
+dn = ["reload", "hdr_walk", "unpack", "scan", "write", "batches#", "end_barrier", "-"]
+for k, n in enumerate(dn):
+    v = int(d[8 + k])
+    print(f"delta  {n:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
