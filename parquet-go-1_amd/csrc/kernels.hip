@@ -593,11 +593,10 @@ struct DictLDS {
   HybRun runs[1024];
 };
 constexpr uint32_t kDeltaWin = 16384;  // bytes of a DELTA stream staged in LDS at a time
+constexpr uint32_t kDeltaBatch = 16;  // blocks per batch (256 groups of 8 deltas at 128 values/block)
 struct DeltaLDS {
-  uint32_t win[kDeltaWin / 4 + 8];  // stream bytes [win0, win0 + kDeltaWin), zero past the stream end
-  uint32_t mb_off[8][64];           // miniblock payload offset (stream-relative) per block of the batch
-  uint8_t mb_w[8][64];
-  int64_t min_delta[8];
+  uint32_t win[kDeltaWin / 4 + 8];  // stream bytes [win0, win0 + kDeltaWin), 16-B aligned in memory
+  uint32_t blk_hdr[kDeltaBatch];      // stream position of each block header of the batch
   uint64_t wsum[4];                 // per-wave totals of the batch scan
   uint32_t nblocks, err_code, err_pos, stop_val, next_hdr, reload;
 };
@@ -844,46 +843,99 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
 
 
 
-// delta_hdr over the LDS window (stream bytes [win0, ...) in `win`), dword reads only.
-DEV bool delta_hdr_lds(const uint32_t *win, uint32_t win0, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64,
-                       uint32_t mbc, int64_t *min_delta, uint8_t *w, uint32_t *hdr_len, uint32_t *err) {
-  const uint32_t off = pos - win0;
-  uint32_t b[4] = {lds_ld32(win, off), lds_ld32(win, off + 4), lds_ld32(win, off + 8), lds_ld32(win, off + 12)};
-  uint64_t x = 0;
-  unsigned sh = 0;
-  uint32_t k = 0;
-  for (;; k++) {
-    if (pos + k >= n) { *err = PQ_ERR_EOF; return false; }
-    if (k == 10) {  // Go keeps reading: a later terminator is an overflow, none is EOF
-      *err = resolve_long_varint(gs, pos - 2, n) == PQ_ERR_RANGE ? PQ_ERR_RANGE : PQ_ERR_EOF;
-      return false;
+// One DELTA block header (minDelta zigzag varint + mbc miniblock widths, the reads of
+// deltabp_decoder.go:125-150) at stream position pos, read from the LDS window that holds
+// stream bytes [win0, ...). Returns the error class (0 = ok) and, on success, minDelta,
+// the width and payload offset (relative to pos) of miniblock m, and the block's total
+// length. The common case (varint <= 8 bytes, <= 4 miniblocks) is branch-free register
+// work on one round of LDS reads; longer headers walk the window byte by byte, and a
+// varint longer than 10 bytes is resolved from global memory (Go overflow vs EOF).
+DEV uint32_t delta_blk(const uint32_t *win, int32_t win0, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64,
+                       uint32_t mbc, uint32_t g8, uint32_t m, int64_t *min_delta, uint32_t *wm, uint32_t *moff,
+                       uint32_t *blen) {
+  const uint32_t off = (uint32_t)((int32_t)pos - win0);
+  const uint32_t a = off >> 2, sh = off & 3;
+  const uint32_t w0 = win[a], w1 = win[a + 1], w2 = win[a + 2], w3 = win[a + 3];
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32);
+  const uint64_t term = ~lo & 0x8080808080808080ull;
+  uint64_t x;
+  uint32_t L;
+  if (term) {
+    L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;  // varint bytes (1..8)
+    if (pos + L > n) return PQ_ERR_EOF;              // stream ends inside the varint
+    uint64_t y = lo & (L == 8 ? ~0ull : ((1ull << (8 * L)) - 1ull)) & 0x7f7f7f7f7f7f7f7full;
+    y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
+    y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
+    x = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
+  } else {
+    x = 0;
+    unsigned shv = 0;
+    for (uint32_t k = 0;; k++) {
+      if (pos + k >= n) return PQ_ERR_EOF;
+      if (k == 10) return resolve_long_varint(gs, pos - 2, n) == PQ_ERR_RANGE ? PQ_ERR_RANGE : PQ_ERR_EOF;
+      const uint32_t by = lds_ld32(win, off + k) & 0xffu;
+      if (by < 0x80) {
+        if (k == 9 && by > 1) return PQ_ERR_RANGE;
+        if (shv < 64) x |= (uint64_t)by << shv;
+        L = k + 1;
+        break;
+      }
+      if (shv < 64) x |= (uint64_t)(by & 0x7f) << shv;
+      shv += 7;
     }
-    uint32_t by = (b[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    if (by < 0x80) {
-      if (k == 9 && by > 1) { *err = PQ_ERR_RANGE; return false; }
-      if (sh < 64) x |= (uint64_t)by << sh;
-      break;
-    }
-    if (sh < 64) x |= (uint64_t)(by & 0x7f) << sh;
-    sh += 7;
   }
   int64_t v = (int64_t)(x >> 1);
   if (x & 1) v = ~v;
-  if (!is64 && (v > 2147483647ll || v < -2147483648ll)) { *err = PQ_ERR_RANGE; return false; }
+  if (!is64 && (v > 2147483647ll || v < -2147483648ll)) return PQ_ERR_RANGE;
   *min_delta = v;
-  const uint32_t p = pos + k + 1;
-  if (p >= n && mbc > 0) { *err = PQ_ERR_EOF; return false; }
-  if (p + mbc > n) { *err = PQ_ERR_UNEXPECTED_EOF; return false; }
-  for (uint32_t i = 0; i < mbc; i += 4) {
-    uint32_t ww = lds_ld32(win, p - win0 + i);
-    for (uint32_t j = 0; j < 4 && i + j < mbc; j++) {
-      uint32_t wi = (ww >> (8 * j)) & 0xffu;
-      if (wi > (is64 ? 64u : 32u)) { *err = PQ_ERR_INVALID; return false; }
-      w[i + j] = (uint8_t)wi;
+  const uint32_t p = pos + L;
+  if (p >= n && mbc > 0) return PQ_ERR_EOF;
+  if (p + mbc > n) return PQ_ERR_UNEXPECTED_EOF;
+  const uint32_t lim = is64 ? 64u : 32u;
+  uint32_t sum = 0, before = 0, wsel = 0;
+  if (mbc <= 4 && L <= 8) {
+    uint32_t ww = L < 8 ? (uint32_t)((lo >> (8 * L)) | ((uint64_t)u2 << (64 - 8 * L))) : u2;
+    if (mbc < 4) ww &= (1u << (8 * mbc)) - 1u;
+    const uint32_t b0 = ww & 0xffu, b1 = (ww >> 8) & 0xffu, b2 = (ww >> 16) & 0xffu, b3 = ww >> 24;
+    if (max(max(b0, b1), max(b2, b3)) > lim) return PQ_ERR_INVALID;
+    sum = b0 + b1 + b2 + b3;
+    before = (m > 0 ? b0 : 0) + (m > 1 ? b1 : 0) + (m > 2 ? b2 : 0);
+    wsel = m == 0 ? b0 : m == 1 ? b1 : m == 2 ? b2 : b3;
+  } else {
+    const uint32_t q = off + L;
+    for (uint32_t i = 0; i < mbc; i++) {
+      const uint32_t wi = lds_ld32(win, q + i) & 0xffu;
+      if (wi > lim) return PQ_ERR_INVALID;
+      if (i < m) before += wi;
+      if (i == m) wsel = wi;
+      sum += wi;
     }
   }
-  *hdr_len = k + 1 + mbc;
-  return true;
+  *wm = wsel;
+  *moff = L + mbc + g8 * before;
+  *blen = L + mbc + g8 * sum;
+  return 0;
+}
+
+// Length of the DELTA block whose header starts at stream position pos, on the serial
+// critical path of the header walk: varint length from a byte mask, width sum with one
+// SAD. No validation (the unpack threads re-parse every header with delta_blk and report
+// its errors); returns 0 when the header needs delta_blk (varint > 8 bytes, mbc > 4).
+DEV uint32_t delta_blk_len(const uint32_t *win, int32_t win0, uint32_t pos, uint32_t mbc, uint32_t g8) {
+  const uint32_t off = (uint32_t)((int32_t)pos - win0);
+  const uint32_t a = off >> 2, sh = off & 3;
+  const uint32_t w0 = win[a], w1 = win[a + 1], w2 = win[a + 2], w3 = win[a + 3];
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32);
+  const uint64_t term = ~lo & 0x8080808080808080ull;
+  if (!term || mbc > 4) return 0;
+  const uint32_t L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;
+  uint32_t ww = L < 8 ? (uint32_t)((lo >> (8 * L)) | ((uint64_t)u2 << (64 - 8 * L))) : u2;
+  ww &= mbc == 4 ? 0xffffffffu : ((1u << (8 * mbc)) - 1u);
+  return L + mbc + g8 * __builtin_amdgcn_sad_u8(ww, 0u, 0u);
 }
 
 DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
@@ -901,53 +953,73 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   uint64_t carry = (uint64_t)pd.delta_first;
   uint32_t hdr = pd.delta_first_mb - pd.val_off;  // next miniblock header (stream-relative)
   const uint32_t gpb = bs / 8;                      // groups per block
-  const uint32_t bpb = max(1u, min(8u, 256u / gpb)); // blocks per batch
+  const uint32_t bpb = max(1u, min(kDeltaBatch, 256u / gpb)); // blocks per batch
   const uint32_t max_blk = 10 + mbc + bs * 8;       // upper bound of one block's bytes (widths <= 64)
-  uint32_t win0 = 0xffffffffu;
+  int32_t win0 = 0;                                 // stream offset of LDS byte 0 (16-B aligned address)
+  bool staged = false;
   uint32_t blk = 0;                                 // index of the next block
+  const uint32_t g8 = mbvc / 8;                     // bytes per bit of miniblock width
+  if (tid == 0) { L.err_code = 0; L.stop_val = limit; }
   Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
   st.begin();
   while ((uint64_t)blk * bs < limit) {
     // ---- (re)stage the window so that it starts at the next header
-    if (win0 == 0xffffffffu || (hdr + max_blk > win0 + kDeltaWin && win0 + kDeltaWin < n)) {
+    if (!staged || ((int64_t)hdr + max_blk > (int64_t)win0 + kDeltaWin && (int64_t)win0 + kDeltaWin < n)) {
       __syncthreads();
-      win0 = hdr & ~3u;
-      const uint8_t *src = s + win0;
-      uint32_t lim = n > win0 ? n - win0 : 0;  // stream bytes left
-      for (uint32_t k = tid; k < kDeltaWin / 4 + 8; k += blockDim.x) {
-        uint32_t o = 4 * k;
-        uint32_t v = o + 4 <= lim ? ld32(src + o) : (o < lim ? ld32(src + o) & ((1u << (8 * (lim - o))) - 1u) : 0u);
-        L.win[k] = v;
+      // window starts at the 16-B aligned address at or below the next header (never below the
+      // 16-B aligned page start); loads stop 16 B past the stream end (page padding)
+      win0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
+      staged = true;
+      const uint4 *src = (const uint4 *)(s + win0);
+      uint4 *dst = (uint4 *)L.win;
+      const int64_t lim = (int64_t)n + 16 - win0;  // bytes worth loading
+      uint4 v[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint32_t k = tid + j * 256;
+        v[j] = (k < kDeltaWin / 16 + 2 && (int64_t)k * 16 < lim) ? src[k] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint32_t k = tid + j * 256;
+        const int64_t o = (int64_t)win0 + 16 * (int64_t)k;  // stream offset of this uint4
+        if (o + 16 > (int64_t)n) {                             // zero the bytes past the stream end
+          uint32_t *e = &v[j].x;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int64_t r = (int64_t)n - (o + 4 * q);
+            e[q] = r >= 4 ? e[q] : (r <= 0 ? 0u : e[q] & ((1u << (8 * r)) - 1u));
+          }
+        }
+        if (k < kDeltaWin / 16 + 2) dst[k] = v[j];
       }
       __syncthreads();
       st.lap(0);
     }
-    // ---- header walk (thread 0), inside the window
+    // ---- header walk (thread 0): block positions only; every unpack thread re-parses its
+    // own block's header in parallel (and reports its errors) below
     if (tid == 0) {
-      L.err_code = 0;
-      L.stop_val = limit;
       uint32_t nb = 0;
-      const uint32_t wend = win0 + kDeltaWin;
+      const int64_t wend = (int64_t)win0 + kDeltaWin;
       for (; nb < bpb && (uint64_t)(blk + nb) * bs < limit; nb++) {
-        if (hdr + 10 + mbc > wend && wend < n) break;  // header not entirely staged: next window
-        uint32_t hl = 0, e = 0;
-        int64_t md;
-        // parse from the LDS window with typed dword reads (bounds-checked against n)
-        if (!delta_hdr_lds(L.win, win0, s, n, hdr, is64, mbc, &md, L.mb_w[nb], &hl, &e)) {
-          L.err_code = e;
-          L.err_pos = (blk + nb) * bs;
-          L.stop_val = L.err_pos;
+        if ((int64_t)hdr + 16 + mbc > wend && wend < n) break;  // header not entirely staged: next window
+        uint32_t bl = delta_blk_len(L.win, win0, hdr, mbc, g8);
+        if (!bl) {
+          int64_t md;
+          uint32_t wm, mo;
+          if (delta_blk(L.win, win0, s, n, hdr, is64, mbc, g8, 0, &md, &wm, &mo, &bl)) {
+            L.blk_hdr[nb++] = hdr;  // the unpack threads report the error
+            break;
+          }
+        }
+        if (hdr + bl > n) {  // the stream ends inside this block (or its header is bad): reported below
+          L.blk_hdr[nb++] = hdr;
+          hdr += bl;
           break;
         }
-        uint32_t off = hdr + hl, end = off;
-        for (uint32_t m = 0; m < mbc; m++) end += (mbvc / 8) * L.mb_w[nb][m];
-        if (end > wend && wend < n && nb > 0) break;  // block body not entirely staged (always take >= 1)
-        L.min_delta[nb] = md;
-        for (uint32_t m = 0; m < mbc; m++) {
-          L.mb_off[nb][m] = off;
-          off += (mbvc / 8) * L.mb_w[nb][m];
-        }
-        hdr = off;
+        if ((int64_t)hdr + bl > wend && wend < n && nb > 0) break;  // block body not staged (always take >= 1)
+        L.blk_hdr[nb] = hdr;
+        hdr += bl;
       }
       L.nblocks = nb;
       L.next_hdr = hdr;
@@ -964,19 +1036,27 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     uint64_t d[8];
     uint64_t sum = 0;
     uint32_t gerr = 0, gerr_pos = 0;
-    const bool valid = bi < nb && d0 < stop;
+    bool valid = bi < nb && d0 < stop;
     uint32_t goff = 0, wbits = 0;
+    int64_t mdl = 0;
     if (valid) {
-      uint32_t inb = (g % gpb) * 8;
-      uint32_t m = inb / mbvc, o = inb % mbvc;
-      wbits = L.mb_w[bi][m];
-      goff = L.mb_off[bi][m] + (o / 8) * wbits;  // group byte offset (stream-relative)
-      if (wbits > 0 && goff >= n) { gerr = PQ_ERR_EOF; gerr_pos = d0; }
-      else if ((uint64_t)goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
+      const uint32_t inb = (g % gpb) * 8;
+      const uint32_t m = inb / mbvc, o = inb % mbvc;
+      const uint32_t bpos = L.blk_hdr[bi];
+      uint32_t mo, bl;
+      const uint32_t he = delta_blk(L.win, win0, s, n, bpos, is64, mbc, g8, m, &mdl, &wbits, &mo, &bl);
+      if (he) {  // header error: surfaces at the block's first position (read by next() there)
+        gerr = he;
+        gerr_pos = (blk + bi) * bs;
+      } else {
+        goff = bpos + mo + (o / 8) * wbits;  // group byte offset (stream-relative)
+        if (wbits > 0 && goff >= n) { gerr = PQ_ERR_EOF; gerr_pos = d0; }
+        else if ((uint64_t)goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
+      }
     }
     if (valid && !gerr) {
-      const uint64_t md = (uint64_t)L.min_delta[bi];
-      const uint32_t bo = (goff - win0) * 8;
+      const uint64_t md = (uint64_t)mdl;
+      const uint32_t bo = (uint32_t)((int32_t)goff - win0) * 8;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         uint64_t u = lds_bits64(L.win, bo + j * wbits, wbits);

@@ -1,0 +1,212 @@
+"""Minimal Parquet writer for hand-built pages (test-fixture tool, not product code).
+
+pyarrow only emits DELTA_BINARY_PACKED with blockSize 256 / 4 miniblocks, so the
+decoder paths for other block shapes (more than 4 miniblocks, blocks > 1024
+values, miniblocks whose value count is not a multiple of 8 or 32), 10-byte
+minDelta varints and arbitrary widths in unneeded trailing miniblocks are
+reached only through streams written here. The encoder follows the format
+specification (parquet-format Encodings.md, DELTA_BINARY_PACKED); the file
+framing is the Thrift compact protocol (parquet.thrift field ids).
+"""
+import struct
+
+import numpy as np
+
+# ---------------------------------------------------------------- thrift compact
+
+
+def uvar(x):
+    out = bytearray()
+    while True:
+        b = x & 0x7F
+        x >>= 7
+        if x:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def zz64(v):
+    return ((v << 1) ^ (v >> 63)) & 0xFFFFFFFFFFFFFFFF
+
+
+I32, I64, BIN, LIST, STRUCT, BOOL = 5, 6, 8, 9, 12, 1
+
+
+def tstruct(fields):
+    """fields: [(id, type, value)] in increasing id order; value of STRUCT is a field list,
+    of LIST is (elem_type, [values])."""
+    out = bytearray()
+    last = 0
+    for fid, t, v in fields:
+        if v is None:
+            continue
+        ct = t
+        if t == BOOL:
+            ct = 1 if v else 2
+        d = fid - last
+        if 0 < d <= 15:
+            out.append((d << 4) | ct)
+        else:
+            out.append(ct)
+            out += uvar(zz64(fid))
+        last = fid
+        out += tvalue(t, v)
+    out.append(0)
+    return bytes(out)
+
+
+def tvalue(t, v):
+    if t in (I32, I64):
+        return uvar(zz64(v))
+    if t == BIN:
+        v = v.encode() if isinstance(v, str) else v
+        return uvar(len(v)) + v
+    if t == STRUCT:
+        return tstruct(v)
+    if t == BOOL:
+        return b""
+    if t == LIST:
+        et, vals = v
+        hdr = bytes([(len(vals) << 4) | et]) if len(vals) < 15 else bytes([0xF0 | et]) + uvar(len(vals))
+        return hdr + b"".join(tvalue(et, x) for x in vals)
+    raise ValueError(t)
+
+
+# ---------------------------------------------------------------- encoders
+
+
+def bitpack(vals, w):
+    """LSB-first bit packing of non-negative ints at width w (len(vals) * w must be a multiple of 8)."""
+    acc = 0
+    for i, v in enumerate(vals):
+        acc |= (int(v) & ((1 << w) - 1)) << (i * w)
+    return acc.to_bytes(len(vals) * w // 8, "little") if w else b""
+
+
+def hybrid_bitpacked(levels, bw):
+    """RLE/bit-packing hybrid with one bit-packed run (levels padded to a multiple of 8)."""
+    n = len(levels)
+    g = (n + 7) // 8
+    padded = list(levels) + [0] * (g * 8 - n)
+    return uvar((g << 1) | 1) + bitpack(padded, bw)
+
+
+def delta_encode(vals, bs=128, mbc=4, bits=64, trailing_width=0, min_delta_override=None):
+    """DELTA_BINARY_PACKED stream of `vals` (python ints, wrapped to `bits`).
+
+    trailing_width: width byte written for miniblocks of the last block that hold no
+    delta (the spec lets writers put anything there). min_delta_override: force every
+    block's minDelta (widths are then computed for the wrapped differences)."""
+    mask = (1 << bits) - 1
+    sign = 1 << (bits - 1)
+
+    def s(v):
+        v &= mask
+        return v - (1 << bits) if v & sign else v
+
+    mbvc = bs // mbc
+    out = bytearray(uvar(bs) + uvar(mbc) + uvar(len(vals)))
+    if not vals:
+        return bytes(out + uvar(0))
+    out += uvar(zz64(s(vals[0])))
+    deltas = [s(vals[i] - vals[i - 1]) for i in range(1, len(vals))]
+    for b0 in range(0, len(deltas), bs):
+        blk = deltas[b0:b0 + bs]
+        md = min(blk) if min_delta_override is None else min_delta_override
+        adj = [(d - md) & mask for d in blk]
+        out += uvar(zz64(md))
+        widths, bodies = [], []
+        for m in range(mbc):
+            mb = adj[m * mbvc:(m + 1) * mbvc]
+            if not mb:
+                widths.append(trailing_width)
+                continue
+            w = max(int(x).bit_length() for x in mb)
+            widths.append(w)
+            mb = mb + [0] * (mbvc - len(mb))
+            if (mbvc * w) % 8:
+                pad = (8 - (mbvc * w) % 8)
+                body = bitpack(mb + [0] * pad, w)  # round up to whole bytes
+                body = body[: (mbvc * w + 7) // 8]
+            else:
+                body = bitpack(mb, w)
+            bodies.append(body)
+        out += bytes(widths)
+        for body in bodies:
+            out += body
+    return bytes(out)
+
+
+# ---------------------------------------------------------------- file framing
+
+TYPES = {"INT32": 1, "INT64": 2, "DOUBLE": 5}
+ENC = {"PLAIN": 0, "RLE": 3, "DELTA_BINARY_PACKED": 5}
+
+
+def page_v1(values_bytes, num_values, encoding, def_bytes=b""):
+    """DATA_PAGE (V1): [def levels with u32 length prefix] + values."""
+    body = (struct.pack("<I", len(def_bytes)) + def_bytes if def_bytes else b"") + values_bytes
+    dph = [(1, I32, num_values), (2, I32, ENC[encoding]), (3, I32, ENC["RLE"]), (4, I32, ENC["RLE"])]
+    hdr = tstruct([(1, I32, 0), (2, I32, len(body)), (3, I32, len(body)), (5, STRUCT, dph)])
+    return hdr + body
+
+
+def page_v2(values_bytes, num_values, num_nulls, num_rows, encoding, def_bytes=b""):
+    body = def_bytes + values_bytes
+    dph = [(1, I32, num_values), (2, I32, num_nulls), (3, I32, num_rows), (4, I32, ENC[encoding]),
+           (5, I32, len(def_bytes)), (6, I32, 0), (7, BOOL, False)]
+    hdr = tstruct([(1, I32, 3), (2, I32, len(body)), (3, I32, len(body)), (8, STRUCT, dph)])
+    return hdr + body
+
+
+def write_file(columns, row_groups):
+    """columns: [(name, type, optional)]; row_groups: [(num_rows, [[page bytes, ...] per column],
+    [num_values per column])]. Returns the file bytes."""
+    out = bytearray(b"PAR1")
+    rgs = []
+    for num_rows, col_pages, col_nv in row_groups:
+        ccs = []
+        total = 0
+        for (name, typ, opt), pages, nv in zip(columns, col_pages, col_nv):
+            off = len(out)
+            for p in pages:
+                out += p
+            size = len(out) - off
+            total += size
+            md = [(1, I32, TYPES[typ]), (2, LIST, (I32, [0, 3, 5])), (3, LIST, (BIN, [name])), (4, I32, 0),
+                  (5, I64, nv), (6, I64, size), (7, I64, size), (9, I64, off)]
+            ccs.append([(2, I64, off), (3, STRUCT, md)])
+        rgs.append([(1, LIST, (STRUCT, ccs)), (2, I64, total), (3, I64, num_rows)])
+    schema = [[(4, BIN, "schema"), (5, I32, len(columns))]]
+    for name, typ, opt in columns:
+        schema.append([(1, I32, TYPES[typ]), (3, I32, 1 if opt else 0), (4, BIN, name)])
+    fmd = tstruct([(1, I32, 1), (2, LIST, (STRUCT, schema)), (3, I64, sum(r[0] for r in row_groups)),
+                   (4, LIST, (STRUCT, rgs)), (6, BIN, "rawpq fixture writer")])
+    out += fmd + struct.pack("<I", len(fmd)) + b"PAR1"
+    return bytes(out)
+
+
+def delta_column_file(pages_vals, bs, mbc, typ="INT64", v2=False, rg_split=None, **kw):
+    """A one-column REQUIRED file whose pages are DELTA streams of the given value lists."""
+    bits = 64 if typ == "INT64" else 32
+    pages = []
+    for vals in pages_vals:
+        st = delta_encode(vals, bs, mbc, bits, **kw)
+        pages.append(page_v2(st, len(vals), 0, len(vals), "DELTA_BINARY_PACKED") if v2
+                     else page_v1(st, len(vals), "DELTA_BINARY_PACKED"))
+    groups = rg_split or [len(pages)]
+    rgs, k = [], 0
+    for g in groups:
+        ps, vs = pages[k:k + g], pages_vals[k:k + g]
+        n = sum(len(v) for v in vs)
+        rgs.append((n, [ps], [n]))
+        k += g
+    return write_file([("a", typ, False)], rgs)
+
+
+def random_walk(rng, n, step_bits, signed=True):
+    lo = -(1 << (step_bits - 1)) if signed else 0
+    d = rng.integers(lo, 1 << (step_bits - 1), n, dtype=np.int64)
+    return [int(x) for x in np.cumsum(d)]
