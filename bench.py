@@ -165,6 +165,7 @@ def main():
     dt = time.perf_counter() - t0
     st = b.stats()
     kern_ms, kern_n, kern_name = b.kernel_time()
+    ktimes = b.kernel_times()
     if dist is not None:
         import torch
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -178,7 +179,7 @@ def main():
     rows_per_s = rows_total / (ms_per_step / 1e3)
 
     # roofline of the dominant kernel: algorithmic bytes moved by that kernel per launch / its avg time
-    kb = kernel_bytes(b, kern_name, st)
+    kb = kernel_bytes(b, kern_name, st) or 0
     achieved = kb / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     line = {
         "metric": "decoded GB/s + rows/s per GPU and whole node (1/2/4/8); % HBM peak",
@@ -204,6 +205,10 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": kb},
+        "kernels": {k: {"ms": round(ms, 4), "launches_per_step": round(n / args.steps, 2),
+                        "GBps": round(kernel_bytes(b, k, st) / (ms / 1e3) / 1e9, 1)
+                        if kernel_bytes(b, k, st) is not None and ms > 0 else None}
+                    for k, (ms, n) in ktimes.items()},
     }
     if rank == 0 and not args.no_cpu_baseline:
         rps, gbs, thr, desc = cpu_baseline(data)
@@ -221,11 +226,13 @@ def kernel_bytes(b, name, st):
     """Algorithmic bytes of one launch of kernel `name` (SURVEY §8(d) accounting restricted to what
     that kernel reads and writes): k_values = value sections read + values written; k_levels =
     rep/def sections read + validity bitmap / levels written."""
-    if name == "k_values":
-        return int(st.values_kernel_bytes)
+    if name == "k_values[delta]":
+        return int(st.delta_kernel_bytes)
+    if name == "k_values[other]":
+        return int(st.values_kernel_bytes - st.delta_kernel_bytes)
     if name == "k_levels":
         return int(st.levels_kernel_bytes)
-    return int(st.input_bytes + st.output_bytes)
+    return None
 
 
 if __name__ == "__main__":

@@ -133,6 +133,7 @@ typedef struct {
   double host_decompress_ms; /* SNAPPY/GZIP on host threads */
   int64_t levels_kernel_bytes; /* algorithmic bytes of k_levels: level sections + validity/levels written */
   int64_t values_kernel_bytes; /* algorithmic bytes of k_values: value sections + values/offsets written */
+  int64_t delta_kernel_bytes;  /* the DELTA_BINARY_PACKED pages' share of values_kernel_bytes */
 } pqgpu_batch_stats;
 
 /* ---- version / device ---------------------------------------------- */
@@ -207,6 +208,10 @@ int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
  * events on the stream the kernel runs on; and its name. */
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
 int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
+/* The same for every timed launch slot (0 <= slot < PQGPU_TIMER_SLOTS); PQ_ERR_ARG past the end. */
+#define PQGPU_TIMER_SLOTS 9
+int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
+                            size_t name_len);
 
 #ifdef __cplusplus
 }

@@ -235,8 +235,8 @@ struct KernelTimer {
     pool.clear();
   }
 };
-static const char *kTimerNames[9] = {"k_levels", "k_values", "k_scan_runs", "k_bases", "k_dict_ba",
-                                     "k_ba_offsets", "k_ba_gather", "k_records", "k_values"};
+static const char *kTimerNames[9] = {"k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_dict_ba",
+                                     "k_ba_offsets", "k_ba_gather", "k_records", "k_values[other]"};
 
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
@@ -953,7 +953,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMemcpy(rec.data(), A + b->o_rec, np * 4, hipMemcpyDeviceToHost), err);
   }
   int first = PQ_OK;
-  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0;
+  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0;
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
     clear_err(&hc.dev_err);
@@ -982,8 +982,10 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.o_valid) out_bytes += (int64_t)(hc.num_slots + 7) / 8;
       if (hc.o_lists) out_bytes += (hc.records + 1) * 4;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
-        lvl_bytes += b->pages[p].rep_len + b->pages[p].def_len;
-        val_bytes += b->pages[p].val_len;
+        const PageDesc &pd = b->pages[p];
+        lvl_bytes += pd.rep_len + pd.def_len;
+        val_bytes += pd.val_len;
+        if (pd.vkind == VK_DELTA32 || pd.vkind == VK_DELTA64) dl_bytes += pd.val_len + (int64_t)nn[p] * w;
       }
       if (hc.o_def) lvl_bytes += (int64_t)hc.num_slots;
       if (hc.o_rep) lvl_bytes += (int64_t)hc.num_slots;
@@ -993,6 +995,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   b->stats.levels_kernel_bytes = lvl_bytes;
   b->stats.values_kernel_bytes = val_bytes;
+  b->stats.delta_kernel_bytes = dl_bytes;
   b->stats.output_bytes = out_bytes;
   b->stats.num_slots = slots;
   b->stats.num_values = values;
@@ -1326,6 +1329,18 @@ int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, c
   if (avg_ms) *avg_ms = t.total_ms[best] / (double)t.launches[best];
   if (launches) *launches = t.launches[best];
   if (name && name_len) snprintf(name, name_len, "%s", kTimerNames[best]);
+  return PQ_OK;
+}
+
+int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
+                            size_t name_len) {
+  if (!b || slot < 0 || slot >= PQGPU_TIMER_SLOTS) return PQ_ERR_ARG;
+  (void)hipDeviceSynchronize();
+  b->timer.resolve();
+  const KernelTimer &t = b->timer;
+  if (avg_ms) *avg_ms = t.launches[slot] ? t.total_ms[slot] / (double)t.launches[slot] : 0.0;
+  if (launches) *launches = t.launches[slot];
+  if (name && name_len) snprintf(name, name_len, "%s", kTimerNames[slot]);
   return PQ_OK;
 }
 

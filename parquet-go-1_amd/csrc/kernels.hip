@@ -335,6 +335,7 @@ struct LevelSink {
   uint32_t cmp;          // level value that counts (maxD for def, 0 for rep)
   uint32_t count;        // lane-local count of (level == cmp)
   uint32_t err_code, err_pos;
+  uint32_t stage_len;    // bytes held by the LDS stage passed to window()/piece()
 
   DEV static void or_bits(uint32_t *dst, uint64_t g, uint64_t m) {
     if (!m) return;
@@ -366,7 +367,7 @@ struct LevelSink {
     if (bp) {
       const uint64_t bo = (uint64_t)value * 8 + (uint64_t)k * bw;   // stream bit offset
       const uint64_t be = bo + (uint64_t)nb * bw;
-      const bool staged = stg && value >= sb && be + 64 <= (uint64_t)(sb + kStage) * 8;
+      const bool staged = stg && value >= sb && be + 64 <= (uint64_t)(sb + stage_len) * 8;
       if (bw == 1) {
         uint64_t raw;
         if (staged) raw = lds_bits64(stg, (uint32_t)(bo - (uint64_t)sb * 8), nb);
@@ -422,7 +423,7 @@ struct LevelLDS {
 // where rep == 0), then definition levels (validity bitmap built in LDS, flushed with
 // coalesced stores). One call site of the walker for both streams.
 // Reference: page_v1.go:42-48 / page_v2.go:40-46 readValues -> decodePackedArray.
-__global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(64) k_levels_serial(BatchDev b, const uint32_t *pages) {
   __shared__ LevelLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
@@ -449,6 +450,7 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
     sk.count = 0;
     sk.err_code = 0;
     sk.err_pos = 0;
+    sk.stage_len = kStage;
     __syncthreads();
     if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
       if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
@@ -494,6 +496,276 @@ __global__ void __launch_bounds__(64) k_levels(BatchDev b, const uint32_t *pages
     }
   }
   if (lane == 0) b.page_nn[pi] = nn;
+}
+
+// ---------------------------------------------------------------------------
+// Parallel level decoder: one 256-thread workgroup per page (replaces the serial
+// per-page chain walk of k_levels_serial for every page).
+//
+// The RLE/bit-packed hybrid stream (hybrid_decoder.go:77-131) is a chain of run
+// headers: the position of run k+1 is known only after run k's header is decoded.
+// The stream is processed in chunks of kLvChunk byte positions, each split into
+// 64-position windows:
+//  1. every position of the chunk is decoded as if a run header started there
+//     (decode_hdr; invalid candidates inside payloads are harmless) and, inside its
+//     window, the chain is followed by pointer doubling over the wave's lanes
+//     (6 shuffle rounds) to the exit position X (first chain position >= window end);
+//  2. one thread follows X from the chunk's entry: the true chain's entry position in
+//     each window it touches (one LDS read per window instead of one hop per run);
+//  3. per window, the chain lanes are marked from the entry (register chase) and the
+//     window's value total is summed;
+//  4. window totals are prefix-summed: every true run knows its first value index;
+//  5. the first run that stops the reference's loop (error, EOF-truncated bit-packed
+//     run, or the run that reaches num_values) is found with an LDS atomicMin on
+//     (value index, position);
+//  6. runs before the stop (and the stop's partial run) expand in parallel into the
+//     validity bitmap / level arrays (LevelSink).
+// Results equal the serial walk's exactly, including error class and position.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLvChunk = 4096;             // candidate header positions per chunk
+constexpr uint32_t kLvWin = kLvChunk / 64;      // windows per chunk (one per lane of a wave)
+constexpr uint32_t kLvStage = kLvChunk + 2048;  // staged bytes: the chunk + payloads of its last runs
+constexpr uint32_t kNone = 0xffffffffu;
+
+struct LevelParLDS {
+  uint32_t stage[kLvStage / 4 + 8];
+  uint32_t X[kLvChunk];      // exit position of each candidate header
+  uint32_t entry[kLvWin];    // true chain's first position in each window (kNone: skipped)
+  uint64_t mask[kLvWin];     // true chain's lanes per window
+  uint64_t tot[kLvWin];      // values in each window's true runs
+  uint64_t wpre[kLvWin];     // value index of each window's first true run
+  unsigned long long stop_key;
+  uint64_t chunk_tot, cnt[4];
+  uint32_t next_pos, stop_err, stop_pos;
+  uint32_t bits[kSegSlots / 32];
+};
+
+DEV void stage_load_blk(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n, uint32_t words) {
+  const uint8_t *src = s + sb;
+  const uint32_t lim = n > sb ? n - sb : 0;
+  for (uint32_t k = threadIdx.x; k < words; k += blockDim.x) {
+    const uint32_t o = 4 * k;
+    stg[k] = o + 4 <= lim ? ld32(src + o) : (o < lim ? ld32(src + o) & ((1u << (8 * (lim - o))) - 1u) : 0u);
+  }
+}
+
+DEV uint64_t wave_excl_scan64(uint64_t v) { return wave_incl_scan64(v) - v; }
+
+// Decode `need` values of one hybrid stream into the sink; every thread of the
+// workgroup calls this (all control flow is workgroup-uniform).
+DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
+  const uint8_t *s = sk.s;
+  const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6, nwv = blockDim.x >> 6;
+  uint32_t pos0 = 0;
+  uint64_t done = 0;
+  for (;;) {
+    if (done >= need) break;
+    if (pos0 >= n) { sk.error((uint32_t)done, PQ_ERR_EOF); break; }  // next header read at EOF
+    const uint32_t cs = pos0, sb = cs & ~3u;
+    const uint32_t clen = min(kLvChunk, n - cs);
+    const uint32_t nw = (clen + 63) >> 6;
+    __syncthreads();
+    stage_load_blk(L.stage, s, sb, n, kLvStage / 4 + 8);
+    for (uint32_t w = tid; w < kLvWin; w += blockDim.x) L.entry[w] = kNone;
+    if (tid == 0) L.stop_key = ~0ull;
+    __syncthreads();
+    st.lap(0);
+    // 1. exits by pointer doubling inside each window
+    for (uint32_t w = wv; w < nw; w += nwv) {
+      const uint32_t ws = cs + 64 * w, we = ws + 64, c = ws + lane;
+      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+      uint32_t J = c + h.adv;
+#pragma unroll
+      for (int r = 0; r < 6; r++) {
+        const bool in = J < we;
+        const uint32_t Jt = (uint32_t)__shfl((int)J, (int)(in ? J - ws : lane), 64);
+        J = in ? Jt : J;
+      }
+      L.X[64 * w + lane] = J;
+    }
+    __syncthreads();
+    st.lap(1);
+    // 2. the true chain's entry in each window it touches
+    if (tid == 0) {
+      const uint32_t ce = cs + clen;
+      uint32_t p = cs;
+      while (p < ce) {
+        L.entry[(p - cs) >> 6] = p;
+        p = L.X[p - cs];
+      }
+      L.next_pos = p;
+    }
+    __syncthreads();
+    st.lap(2);
+    // 3. chain lanes and value totals per window
+    for (uint32_t w = wv; w < nw; w += nwv) {
+      const uint32_t e = L.entry[w];
+      uint64_t mask = 0, tot = 0;
+      if (e != kNone) {
+        const uint32_t ws = cs + 64 * w, c = ws + lane;
+        const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+        const uint32_t adv = min(h.adv, 64u);
+        uint32_t p = sgpr(e - ws);
+        while (p < 64) {
+          mask |= 1ull << p;
+          p = sgpr(p + rdlane(adv, p));
+        }
+        tot = wave_sum64(((mask >> lane) & 1ull) ? h.nvals : 0u);
+      }
+      if (lane == 0) { L.mask[w] = mask; L.tot[w] = tot; }
+    }
+    __syncthreads();
+    st.lap(3);
+    // 4. value index of each window's first run
+    if (wv == 0) {
+      const uint64_t t = lane < nw ? L.tot[lane] : 0;
+      const uint64_t incl = wave_incl_scan64(t);
+      if (lane < nw) L.wpre[lane] = done + incl - t;
+      if (lane == 63) L.chunk_tot = incl;
+    }
+    __syncthreads();
+    // 5. the run that ends the reference's loop
+    for (uint32_t w = wv; w < nw; w += nwv) {
+      const uint64_t mask = L.mask[w];
+      if (!mask) continue;
+      const uint32_t ws = cs + 64 * w, c = ws + lane;
+      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+      const bool mine = (mask >> lane) & 1ull;
+      const uint64_t C = L.wpre[w] + wave_excl_scan64(mine ? h.nvals : 0u);
+      if (mine && C < need) {
+        const uint64_t rem = need - C;
+        if (h.err || (h.okvals < h.nvals && h.okvals < rem) || h.nvals >= rem)
+          atomicMin(&L.stop_key, (unsigned long long)((C << 32) | c));
+      }
+    }
+    __syncthreads();
+    st.lap(4);
+    const unsigned long long key = L.stop_key;
+    const uint32_t cstop = key == ~0ull ? kNone : (uint32_t)key;
+    // 6. expansion of the runs before the stop (and the stop's own values)
+    for (uint32_t w = wv; w < nw; w += nwv) {
+      const uint64_t mask = L.mask[w];
+      if (!mask) continue;
+      const uint32_t ws = cs + 64 * w, c = ws + lane;
+      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+      const bool mine = (mask >> lane) & 1ull;
+      const uint64_t C = L.wpre[w] + wave_excl_scan64(mine ? h.nvals : 0u);
+      uint32_t cnt = 0;
+      if (mine && C < need && c <= cstop) {
+        const uint64_t rem = need - C;
+        if (c < cstop) {
+          cnt = h.nvals;
+        } else {  // the stopping run
+          uint32_t e = h.err, epos = (uint32_t)C;
+          if (e == kErrLongVarint) e = resolve_long_varint(s, c, n);
+          if (e) {
+            cnt = 0;
+          } else if (h.okvals < h.nvals && h.okvals < rem) {
+            cnt = h.okvals;
+            e = PQ_ERR_EOF;
+            epos = (uint32_t)(C + h.okvals);
+          } else {
+            cnt = (uint32_t)rem;
+          }
+          L.stop_err = e;
+          L.stop_pos = epos;
+        }
+      }
+      sk.window(mine && cnt > 0, (uint32_t)C, cnt, h.bp != 0, h.value, c, L.stage, sb);
+    }
+    st.lap(5);
+    __syncthreads();
+    if (cstop != kNone) {
+      if (L.stop_err) sk.error(L.stop_pos, L.stop_err);
+      break;
+    }
+    done += L.chunk_tot;
+    pos0 = L.next_pos;
+    st.acc[6]++;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *pages) {
+  __shared__ LevelParLDS lds;
+  const uint32_t pi = pages[blockIdx.x];
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint8_t *base = (const uint8_t *)pd.data;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t ns = pd.num_slots;
+  uint32_t *vbits = (uint32_t *)cd.validity;
+  for (uint32_t k = tid; k < kSegSlots / 32; k += blockDim.x) lds.bits[k] = 0;
+  uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
+  Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+  st.begin();
+  for (uint32_t which = 0; which < 2; which++) {
+    const bool rep = which == 0;
+    if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
+    LevelSink sk;
+    sk.s = base + (rep ? pd.rep_off : pd.def_off);
+    sk.n = rep ? pd.rep_len : pd.def_len;
+    sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+    sk.out = rep ? (uint8_t *)cd.rep_levels + pd.slot_base
+                 : (cd.def_levels ? (uint8_t *)cd.def_levels + pd.slot_base : nullptr);
+    sk.bits_lds = rep ? nullptr : lds.bits;
+    sk.bits_glob = rep ? nullptr : vbits;
+    sk.slot_base = pd.slot_base;
+    sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
+    sk.count = 0;
+    sk.err_code = 0;
+    sk.err_pos = 0;
+    sk.stage_len = kLvStage;
+    __syncthreads();
+    if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+      if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+    } else {
+      lv_walk(lds, sk, ns, st);
+    }
+    const uint64_t wc = wave_sum64(sk.count);
+    if (lane == 0) lds.cnt[wv] = wc;
+    __syncthreads();
+    uint64_t cntv = 0;
+    for (uint32_t k = 0; k < (blockDim.x >> 6); k++) cntv += lds.cnt[k];
+    if (sk.err_code) {  // workgroup-uniform
+      if (tid == 0) {
+        report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
+        b.page_nn[pi] = 0;
+        if (rep) b.page_rec[pi] = (uint32_t)cntv;
+      }
+      st.flush(0);
+      return;  // the reference fails the page at the first level error
+    }
+    if (rep) {
+      if (tid == 0) b.page_rec[pi] = (uint32_t)cntv;
+    } else {
+      nn = (uint32_t)cntv;
+    }
+    __syncthreads();
+  }
+  if (cd.max_def > 0) {
+    __syncthreads();
+    // flush the LDS bitmap segment to the chunk bitmap
+    const uint32_t seg = min(ns, kSegSlots);
+    const uint32_t nw = (seg + 31) / 32;
+    const uint32_t sh = (uint32_t)(pd.slot_base & 31);
+    const uint64_t w0 = pd.slot_base >> 5;
+    for (uint32_t k = tid; k < nw; k += blockDim.x) {
+      uint32_t v = lds.bits[k];
+      if (k == nw - 1 && (seg & 31)) v &= (1u << (seg & 31)) - 1u;
+      if (sh == 0) {
+        if (k == 0 || k == nw - 1) atomicOr(&vbits[w0 + k], v);
+        else vbits[w0 + k] = v;
+      } else if (v) {
+        atomicOr(&vbits[w0 + k], v << sh);
+        uint32_t hi = v >> (32 - sh);
+        if (hi) atomicOr(&vbits[w0 + k + 1], hi);
+      }
+    }
+  }
+  st.lap(7);
+  st.flush(0);
+  if (tid == 0) b.page_nn[pi] = nn;
 }
 
 // ---------------------------------------------------------------------------
@@ -1435,7 +1707,7 @@ hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_level_pages) return hipSuccess;
-  hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
+  hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(256), 0, s, b, l.level_pages);
   return hipGetLastError();
 }
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

@@ -71,7 +71,7 @@ class BatchStats(ctypes.Structure):
                 ("num_values", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
                 ("staged_bytes", ctypes.c_int64), ("host_plan_ms", ctypes.c_double),
                 ("host_decompress_ms", ctypes.c_double), ("levels_kernel_bytes", ctypes.c_int64),
-                ("values_kernel_bytes", ctypes.c_int64)]
+                ("values_kernel_bytes", ctypes.c_int64), ("delta_kernel_bytes", ctypes.c_int64)]
 
 
 _LIB = None
@@ -82,7 +82,7 @@ _EXPORTS = [
     "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
     "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
-    "pqgpu_batch_debug_counters",
+    "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot",
 ]
 
 
@@ -125,6 +125,8 @@ def lib():
         "pqgpu_batch_kernel_timing": ([P, ctypes.c_int], ctypes.c_int),
         "pqgpu_batch_debug_counters": ([P, P, ctypes.c_int], ctypes.c_int),
         "pqgpu_batch_kernel_time": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        "pqgpu_batch_kernel_slot": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                      ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -326,6 +328,17 @@ class Batch:
         name = ctypes.create_string_buffer(64)
         lib().pqgpu_batch_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n), name, 64)
         return ms.value, n.value, name.value.decode()
+
+    def kernel_times(self):
+        """{kernel name: (average ms per launch, launches)} for every timed launch slot."""
+        out = {}
+        for k in range(9):
+            ms, n = ctypes.c_double(), ctypes.c_int64()
+            name = ctypes.create_string_buffer(64)
+            lib().pqgpu_batch_kernel_slot(self._h, k, ctypes.byref(ms), ctypes.byref(n), name, 64)
+            if n.value:
+                out[name.value.decode()] = (ms.value, n.value)
+        return out
 
     def result(self, cid, copy=True):
         """ColumnData for chunk `cid` (raises DecodeError if that chunk failed)."""
