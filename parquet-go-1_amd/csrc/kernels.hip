@@ -118,6 +118,18 @@ DEV uint64_t wave_incl_scan64(uint64_t v) {
   }
   return v;
 }
+// wave64 inclusive prefix sum with DPP row shifts and row broadcasts (GFX9 DPP)
+template <int CTRL, int ROWS = 0xf>
+DEV uint32_t dpp0(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false); }
+DEV uint32_t wave_incl_scan32(uint32_t x) {
+  x += dpp0<0x111>(x);       // row_shr:1
+  x += dpp0<0x112>(x);       // row_shr:2
+  x += dpp0<0x114>(x);       // row_shr:4
+  x += dpp0<0x118>(x);       // row_shr:8
+  x += dpp0<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp0<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
 DEV uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -190,53 +202,58 @@ DEV uint32_t resolve_long_varint(const uint8_t *s, uint32_t c, uint32_t n) {
 }
 
 struct Hdr {
-  uint32_t err, nvals, okvals, value, adv, bp;
+  uint32_t err, nvals, okvals, value, adv, bp, cnt;
 };
 
-// Decode the run header that would start at stream position c (stage holds [sb, ...)).
+// Decode the run header that would start at stream position c (stage holds [sb, ...)):
+// the readUVariant32 header (hybrid_decoder.go:77-99) and the run it announces.
+// Branch-light: one round of four aligned LDS reads gives the 12 bytes from c; the
+// varint terminator comes from a byte mask and the 7-bit groups are compacted with
+// shifts (no per-byte loop). Go ReadUvarint semantics: a 10th byte > 1 or any 11th
+// byte overflows; a value above 2^31-1 is out of range; no terminator within 12
+// bytes is resolved lazily by the caller (kErrLongVarint).
 DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t c, uint32_t n, uint32_t bw,
                    uint32_t rs) {
-  Hdr r{0, 0, 0, 0, 1, 0};
+  Hdr r{0, 0, 0, 0, 1, 0, 0};
   if (c >= n) { r.err = PQ_ERR_EOF; return r; }
-  uint32_t off = c - sb;
-  uint32_t w0 = lds_ld32(stg, off), w1 = lds_ld32(stg, off + 4), w2 = lds_ld32(stg, off + 8);
-  uint64_t h = 0;
-  unsigned sh = 0;
-  bool term = false;
-  uint32_t k = 0;
-  for (; k < 12; k++) {
-    if (c + k >= n) { r.err = PQ_ERR_EOF; break; }
-    uint32_t wv = k < 4 ? w0 : (k < 8 ? w1 : w2);
-    uint32_t by = (wv >> (8 * (k & 3))) & 0xffu;
-    if (by < 0x80u) {
-      if (k > 9 || (k == 9 && by > 1)) r.err = PQ_ERR_RANGE;
-      else if (sh < 64) h |= (uint64_t)by << sh;
-      term = true;
-      break;
-    }
-    if (sh < 64) h |= (uint64_t)(by & 0x7f) << sh;
-    sh += 7;
+  const uint32_t off = c - sb, a = off >> 2, sh = off & 3;
+  const uint32_t w0 = stg[a], w1 = stg[a + 1], w2 = stg[a + 2], w3 = stg[a + 3];
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32);
+  const uint64_t t_lo = ~lo & 0x8080808080808080ull;
+  const uint32_t t_hi = ~u2 & 0x80808080u;
+  // varint length L (bytes including the terminator); 13 = none within 12 bytes
+  const uint32_t L = t_lo ? (uint32_t)(__builtin_ctzll(t_lo) >> 3) + 1
+                          : (t_hi ? (uint32_t)(__builtin_ctz(t_hi) >> 3) + 9 : 13u);
+  if (c + L > n) {  // the stream ends inside the varint (ReadByte at EOF)
+    r.err = PQ_ERR_EOF;
+    return r;
   }
-  // > 12-byte varint: Go keeps reading until a terminator (overflow) or EOF. Only a header
-  // the walker actually reaches needs the answer (resolve_long_varint); speculative
-  // candidates inside bit-packed payloads (0xFF bytes) must not scan memory.
-  if (!r.err && !term) r.err = kErrLongVarint;
-  const uint32_t hl = k + 1;
-  if (!r.err && h > 0x7fffffffull) r.err = PQ_ERR_RANGE;
-  if (r.err) return r;
+  if (L == 13) { r.err = kErrLongVarint; return r; }
+  if (L >= 11 || (L == 10 && ((u2 >> 8) & 0xffu) > 1)) { r.err = PQ_ERR_RANGE; return r; }
+  uint64_t y = (L >= 8 ? lo : lo & ((1ull << (8 * L)) - 1ull)) & 0x7f7f7f7f7f7f7f7full;
+  y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
+  y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
+  uint64_t h = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
+  if (L >= 9) h |= (uint64_t)(u2 & 0x7fu) << 56;
+  if (L == 10) h |= (uint64_t)((u2 >> 8) & 1u) << 63;
+  if (h > 0x7fffffffull) { r.err = PQ_ERR_RANGE; return r; }
   const uint32_t cnt = (uint32_t)(h >> 1);
   r.bp = (uint32_t)(h & 1);
+  r.cnt = cnt;
   if (cnt == 0) { r.err = PQ_ERR_INVALID; return r; }
+  const uint32_t hl = L;
   const uint32_t pay = c + hl;
   if (r.bp) {
-    uint64_t nv = (uint64_t)cnt * 8;
+    const uint64_t nv = (uint64_t)cnt * 8;
     r.nvals = nv > 0x7fffffffull ? 0x7fffffffu : (uint32_t)nv;
-    uint64_t pb = (uint64_t)cnt * bw;
-    uint64_t a = hl + pb;
-    r.adv = a > 0x3fffffffull ? 0x3fffffffu : (uint32_t)a;
+    const uint64_t pb = (uint64_t)cnt * bw;
+    const uint64_t adv = hl + pb;
+    r.adv = adv > 0x3fffffffull ? 0x3fffffffu : (uint32_t)adv;
     if ((uint64_t)pay + pb > n) {
-      uint64_t g = pay >= n ? 0 : ((uint64_t)(n - pay) + bw - 1) / bw;  // groups that start before EOF
-      uint64_t ok = g * 8;
+      const uint64_t g = pay >= n ? 0 : ((uint64_t)(n - pay) + bw - 1) / bw;  // groups that start before EOF
+      const uint64_t ok = g * 8;
       r.okvals = ok > r.nvals ? r.nvals : (uint32_t)ok;
     } else {
       r.okvals = r.nvals;
@@ -249,7 +266,14 @@ DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t 
     if (pay >= n) r.err = PQ_ERR_EOF;
     else if (pay + rs > n) r.err = PQ_ERR_UNEXPECTED_EOF;
     else {
-      uint32_t v = lds_ld32(stg, pay - sb);
+      // value bytes at offset L of the 12 register bytes (canonical headers: L <= 5)
+      uint32_t v;
+      if (L <= 8) {
+        const uint64_t mid = ((uint64_t)u1 >> 0) | ((uint64_t)u2 << 32);  // bytes 4..11
+        v = L < 4 ? __builtin_amdgcn_alignbyte(u1, u0, L) : (uint32_t)(mid >> (8 * (L - 4)));
+      } else {
+        v = lds_ld32(stg, pay - sb);
+      }
       r.value = rs >= 4 ? v : (v & ((1u << (8 * rs)) - 1u));
       if (bw < 32 && (r.value >> bw) != 0) r.err = PQ_ERR_INVALID;
     }
@@ -522,14 +546,18 @@ __global__ void __launch_bounds__(64) k_levels_serial(BatchDev b, const uint32_t
 //     validity bitmap / level arrays (LevelSink).
 // Results equal the serial walk's exactly, including error class and position.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLvChunk = 4096;             // candidate header positions per chunk
-constexpr uint32_t kLvWin = kLvChunk / 64;      // windows per chunk (one per lane of a wave)
+constexpr uint32_t kLvChunk = 2048;             // candidate header positions per chunk
+constexpr uint32_t kLvWin = kLvChunk / 64;      // windows per chunk
 constexpr uint32_t kLvStage = kLvChunk + 2048;  // staged bytes: the chunk + payloads of its last runs
 constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kRecErr = 1u << 31, kRecBp = 1u << 30;
 
 struct LevelParLDS {
   uint32_t stage[kLvStage / 4 + 8];
   uint32_t X[kLvChunk];      // exit position of each candidate header
+  uint32_t recA[kLvChunk];   // candidate run: count (30 bits) | kRecBp | kRecErr
+  uint32_t recB[kLvChunk];   // RLE value, bit-packed payload position, or the error class
+  uint8_t adv[kLvChunk];     // header + payload bytes, clamped to 64 (chain steps inside a window)
   uint32_t entry[kLvWin];    // true chain's first position in each window (kNone: skipped)
   uint64_t mask[kLvWin];     // true chain's lanes per window
   uint64_t tot[kLvWin];      // values in each window's true runs
@@ -550,6 +578,27 @@ DEV void stage_load_blk(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n
 }
 
 DEV uint64_t wave_excl_scan64(uint64_t v) { return wave_incl_scan64(v) - v; }
+// Run value counts are clamped to `need` (exact for every run up to the stopping one);
+// with need <= 2^25 a window's 64 counts sum within 32 bits and the DPP scan applies.
+DEV uint64_t lv_excl(uint32_t v, bool small) {
+  return small ? (uint64_t)(wave_incl_scan32(v) - v) : wave_excl_scan64(v);
+}
+DEV uint64_t lv_sum(uint32_t v, bool small) { return small ? rdlane(wave_incl_scan32(v), 63) : wave_sum64(v); }
+
+// Values of a cached candidate run and how many of them the reference returns before
+// EOF (a bit-packed run whose payload is cut by the end of the stream, decode_hdr).
+DEV uint32_t rec_nvals(uint32_t A) {
+  const uint32_t cnt = A & (kRecBp - 1);
+  return (A & kRecBp) ? (cnt >= (1u << 28) ? 0x7fffffffu : cnt * 8) : cnt;
+}
+DEV uint32_t rec_okvals(uint32_t A, uint32_t B, uint32_t nv, uint32_t n, uint32_t bw) {
+  if (!(A & kRecBp)) return nv;
+  const uint64_t pb = (uint64_t)(A & (kRecBp - 1)) * bw;
+  if ((uint64_t)B + pb <= n) return nv;
+  const uint64_t g = B >= n ? 0 : ((uint64_t)(n - B) + bw - 1) / bw;
+  const uint64_t ok = g * 8;
+  return ok > nv ? nv : (uint32_t)ok;
+}
 
 // Decode `need` values of one hybrid stream into the sink; every thread of the
 // workgroup calls this (all control flow is workgroup-uniform).
@@ -557,6 +606,7 @@ DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
   const uint8_t *s = sk.s;
   const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6, nwv = blockDim.x >> 6;
+  const bool small = need <= (1u << 25);
   uint32_t pos0 = 0;
   uint64_t done = 0;
   for (;;) {
@@ -571,10 +621,13 @@ DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     if (tid == 0) L.stop_key = ~0ull;
     __syncthreads();
     st.lap(0);
-    // 1. exits by pointer doubling inside each window
+    // 1. decode every candidate once (cached), exits by pointer doubling inside each window
     for (uint32_t w = wv; w < nw; w += nwv) {
-      const uint32_t ws = cs + 64 * w, we = ws + 64, c = ws + lane;
+      const uint32_t ws = cs + 64 * w, we = ws + 64, c = ws + lane, i = 64 * w + lane;
       const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+      L.recA[i] = h.err ? kRecErr : (h.bp ? kRecBp | h.cnt : h.cnt);  // cnt < 2^30
+      L.recB[i] = h.err ? h.err : h.value;
+      L.adv[i] = (uint8_t)min(h.adv, 64u);
       uint32_t J = c + h.adv;
 #pragma unroll
       for (int r = 0; r < 6; r++) {
@@ -582,7 +635,7 @@ DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         const uint32_t Jt = (uint32_t)__shfl((int)J, (int)(in ? J - ws : lane), 64);
         J = in ? Jt : J;
       }
-      L.X[64 * w + lane] = J;
+      L.X[i] = J;
     }
     __syncthreads();
     st.lap(1);
@@ -603,15 +656,14 @@ DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       const uint32_t e = L.entry[w];
       uint64_t mask = 0, tot = 0;
       if (e != kNone) {
-        const uint32_t ws = cs + 64 * w, c = ws + lane;
-        const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
-        const uint32_t adv = min(h.adv, 64u);
+        const uint32_t ws = cs + 64 * w, i = 64 * w + lane;
+        const uint32_t adv = L.adv[i], A = L.recA[i];
         uint32_t p = sgpr(e - ws);
         while (p < 64) {
           mask |= 1ull << p;
           p = sgpr(p + rdlane(adv, p));
         }
-        tot = wave_sum64(((mask >> lane) & 1ull) ? h.nvals : 0u);
+        tot = lv_sum(((mask >> lane) & 1ull) ? min(rec_nvals(A), need) : 0u, small);
       }
       if (lane == 0) { L.mask[w] = mask; L.tot[w] = tot; }
     }
@@ -625,58 +677,51 @@ DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       if (lane == 63) L.chunk_tot = incl;
     }
     __syncthreads();
-    // 5. the run that ends the reference's loop
+    st.lap(4);
+    // 5. expansion of every true run below need; the first run that ends the reference's
+    //    loop (error, EOF-cut bit-packed run, or the run reaching need) is found with an
+    //    atomicMin on (value index, position). Runs past an error stop may expand too:
+    //    the page then fails and its output is not used.
     for (uint32_t w = wv; w < nw; w += nwv) {
       const uint64_t mask = L.mask[w];
       if (!mask) continue;
-      const uint32_t ws = cs + 64 * w, c = ws + lane;
-      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
+      const uint32_t ws = cs + 64 * w, c = ws + lane, i = 64 * w + lane;
+      const uint32_t A = L.recA[i], B = L.recB[i];
+      const uint32_t nv = (A & kRecErr) ? 0u : rec_nvals(A);
       const bool mine = (mask >> lane) & 1ull;
-      const uint64_t C = L.wpre[w] + wave_excl_scan64(mine ? h.nvals : 0u);
+      const uint64_t C = L.wpre[w] + lv_excl(mine ? min(nv, need) : 0u, small);
+      uint32_t cnt = 0;
       if (mine && C < need) {
         const uint64_t rem = need - C;
-        if (h.err || (h.okvals < h.nvals && h.okvals < rem) || h.nvals >= rem)
-          atomicMin(&L.stop_key, (unsigned long long)((C << 32) | c));
+        const uint32_t ok = (A & kRecErr) ? 0u : rec_okvals(A, B, nv, n, bw);
+        bool stop = true;
+        if (A & kRecErr) cnt = 0;
+        else if (ok < nv && ok < rem) cnt = ok;
+        else if (nv >= rem) cnt = (uint32_t)rem;
+        else { cnt = nv; stop = false; }
+        if (stop) atomicMin(&L.stop_key, (unsigned long long)((C << 32) | c));
       }
+      sk.window(mine && cnt > 0, (uint32_t)C, cnt, (A & kRecBp) != 0, B, c, L.stage, sb);
     }
     __syncthreads();
-    st.lap(4);
-    const unsigned long long key = L.stop_key;
-    const uint32_t cstop = key == ~0ull ? kNone : (uint32_t)key;
-    // 6. expansion of the runs before the stop (and the stop's own values)
-    for (uint32_t w = wv; w < nw; w += nwv) {
-      const uint64_t mask = L.mask[w];
-      if (!mask) continue;
-      const uint32_t ws = cs + 64 * w, c = ws + lane;
-      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
-      const bool mine = (mask >> lane) & 1ull;
-      const uint64_t C = L.wpre[w] + wave_excl_scan64(mine ? h.nvals : 0u);
-      uint32_t cnt = 0;
-      if (mine && C < need && c <= cstop) {
-        const uint64_t rem = need - C;
-        if (c < cstop) {
-          cnt = h.nvals;
-        } else {  // the stopping run
-          uint32_t e = h.err, epos = (uint32_t)C;
-          if (e == kErrLongVarint) e = resolve_long_varint(s, c, n);
-          if (e) {
-            cnt = 0;
-          } else if (h.okvals < h.nvals && h.okvals < rem) {
-            cnt = h.okvals;
-            e = PQ_ERR_EOF;
-            epos = (uint32_t)(C + h.okvals);
-          } else {
-            cnt = (uint32_t)rem;
-          }
-          L.stop_err = e;
-          L.stop_pos = epos;
-        }
-      }
-      sk.window(mine && cnt > 0, (uint32_t)C, cnt, h.bp != 0, h.value, c, L.stage, sb);
-    }
     st.lap(5);
-    __syncthreads();
-    if (cstop != kNone) {
+    const unsigned long long key = L.stop_key;
+    if (key != ~0ull) {
+      if (tid == 0) {  // the stopping run's outcome
+        const uint32_t c = (uint32_t)key, i = c - cs;
+        const uint64_t C = key >> 32;
+        const uint32_t A = L.recA[i], B = L.recB[i];
+        uint32_t e = 0, epos = (uint32_t)C;
+        if (A & kRecErr) {
+          e = B == kErrLongVarint ? resolve_long_varint(s, c, n) : B;
+        } else {
+          const uint32_t nv = rec_nvals(A), ok = rec_okvals(A, B, nv, n, bw);
+          if (ok < nv && ok < need - C) { e = PQ_ERR_EOF; epos = (uint32_t)(C + ok); }
+        }
+        L.stop_err = e;
+        L.stop_pos = epos;
+      }
+      __syncthreads();
       if (L.stop_err) sk.error(L.stop_pos, L.stop_err);
       break;
     }

@@ -26,7 +26,7 @@ dt = time.perf_counter() - t0
 d = b.debug_counters()
 pages = f.num_row_groups * 64 * 2
 print(f"decode {dt*1e3:.3f} ms for {rows} rows; {pages} level pages, {pages//2} DELTA pages")
-names = ["stage", "p1_exits", "p2_entries", "p3_masks", "p45_stop", "p6_expand", "chunks#", "flush"]
+names = ["stage", "p1_exits", "p2_entries", "p3_masks", "p4_prefix", "p5_expand", "chunks#", "flush"]
 for k, n in enumerate(names):
     v = int(d[k])
     print(f"levels {n:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
