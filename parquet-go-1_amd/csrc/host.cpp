@@ -57,6 +57,7 @@ static void clear_err(pqgpu_error *e) {
 struct pqgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
 };
 
 struct pqgpu_file {
@@ -205,6 +206,12 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
+static bool spec_disabled() {
+  const char *on = getenv("PQ_SPEC"), *off = getenv("PQ_NO_SPEC");
+  if (off && atoi(off) != 0) return true;
+  return !(on && atoi(on) != 0);
+}
+
 struct KernelTimer {
   bool enabled = false;
   struct Rec { int slot; hipEvent_t a, b; };
@@ -244,10 +251,18 @@ struct pqgpu_batch {
   std::vector<PageDesc> pages;
   std::vector<uint8_t> stage;
   std::vector<WorkItem> items;
+  std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
   std::vector<uint32_t> level_pages, scan_pages, base_chunks, dict_ba_chunks, ba_chunks, rec_pages;
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
   std::vector<uint32_t> page_nn_init;
+  std::vector<uint32_t> page_nn_spec;   // header non-null counts (speculative mode)
+  std::vector<uint64_t> page_vbase_spec; // their per-chunk exclusive prefix
+  bool spec = false;                     // this upload runs values concurrently with k_levels
+  // Speculative concurrent schedule (values beside k_levels) is opt-in: PQ_SPEC=1. Measured on
+  // cfg2 it loses to the serial order (both kernels contend for LDS); see DESIGN.md.
+  bool force_serial = spec_disabled();
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<uint64_t> ba_tile_off;
   uint64_t ba_tiles_total = 0;
   uint32_t ba_max_tiles = 0;
@@ -260,9 +275,11 @@ struct pqgpu_batch {
   size_t d_arena_cap = 0;
   uint64_t arena_size = 0;
   // arena offsets of batch-level arrays
+  uint64_t o_nnv = 0, o_spec_flag = 0;
   uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
+  uint64_t l_level_bw1 = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   uint32_t n_delta_items = 0;
@@ -536,6 +553,12 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
       pd.num_slots = (uint32_t)ph.dph2.num_values;
       pd.flags |= PF_V2;
+      if (ph.dph2.num_nulls >= 0 && ph.dph2.num_nulls <= ph.dph2.num_values) {
+        // a hint only: the reference counts non-nulls from the definition levels
+        // (page_v2.go:47-50); k_bases checks the hint against that count
+        pd.flags |= PF_BASE_KNOWN;
+        pd.expect_nn = (uint32_t)(ph.dph2.num_values - ph.dph2.num_nulls);
+      }
       if (ph.dph2.rep_len > 0 && max_rep > 0) { pd.rep_off = 0; pd.rep_len = (uint32_t)ph.dph2.rep_len; pd.flags |= PF_REP; }
       if (ph.dph2.def_len > 0 && max_def > 0) {
         pd.def_off = (uint32_t)ph.dph2.rep_len;
@@ -567,6 +590,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
   b->items.clear();
   b->level_pages.clear();
+  b->level_pages_bw1.clear();
   b->scan_pages.clear();
   b->base_chunks.clear();
   b->dict_ba_chunks.clear();
@@ -594,6 +618,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
+  b->o_spec_flag = take(4);
   b->z_end = a;
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -623,7 +648,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
       PageDesc &pd = b->pages[p];
       in_bytes += pd.rep_len + pd.def_len + pd.val_len;
-      if (hc.col.max_def > 0 || hc.col.max_rep > 0) b->level_pages.push_back(p);
+      if (hc.col.max_def == 1 && hc.col.max_rep == 0) b->level_pages_bw1.push_back(p);
+      else if (hc.col.max_def > 0 || hc.col.max_rep > 0) b->level_pages.push_back(p);
       else b->page_nn_init[p] = pd.num_slots;
       if (hc.col.max_rep > 0) b->rec_pages.push_back(p);
       const uint32_t ns_p = pd.num_slots;
@@ -654,6 +680,26 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
     }
   }
+  // Speculative mode: every page's non-null count is known from its header (or it has no
+  // definition levels), so the values kernels need not wait for k_levels.
+  b->spec = !b->force_serial && (!b->level_pages.empty() || !b->level_pages_bw1.empty());
+  b->page_nn_spec.assign(np, 0);
+  b->page_vbase_spec.assign(np, 0);
+  for (uint32_t c = 0; c < nc && b->spec; c++) {
+    HostChunk &hc = b->chunks[c];
+    if (hc.err.code) continue;
+    uint64_t base = 0;
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+      const PageDesc &pd = b->pages[p];
+      uint32_t nn;
+      if (hc.col.max_def == 0 && hc.col.max_rep == 0) nn = pd.num_slots;
+      else if (pd.flags & PF_BASE_KNOWN) nn = pd.expect_nn;
+      else { b->spec = false; break; }
+      b->page_nn_spec[p] = nn;
+      b->page_vbase_spec[p] = base;
+      base += nn;
+    }
+  }
   // Region set to 0xff before every decode: chunk error keys, dictionary tile table.
   b->o_err = take((uint64_t)nc * 8);
   b->f_begin = b->o_err;
@@ -669,6 +715,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
   b->o_chunks = take((uint64_t)nc * sizeof(ChunkDesc));
   b->o_nn = take((uint64_t)np * 4);
+  b->o_nnv = take((uint64_t)np * 4);
   b->o_vbase = take((uint64_t)np * 8);
   b->o_rbase = take((uint64_t)np * 8);
   b->o_runs = take(b->run_total * sizeof(HybRun));
@@ -680,6 +727,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_totals = take(b->ba_chunks.size() * 8);
   b->o_dbg = take(64 * 8);
   b->l_level = take(b->level_pages.size() * 4);
+  b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
   b->l_base = take(b->base_chunks.size() * 4);
   b->l_dict_ba = take(b->dict_ba_chunks.size() * 4);
@@ -759,11 +807,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
   HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
   HIPCHECK(up(b->o_nn, b->page_nn_init.data(), np * 4), err);
+  if (b->spec) {
+    HIPCHECK(up(b->o_nnv, b->page_nn_spec.data(), np * 4), err);
+    HIPCHECK(up(b->o_vbase, b->page_vbase_spec.data(), np * 8), err);
+  }
   HIPCHECK(hipMemsetAsync(A + b->o_dbg, 0, 64 * 8, s), err);
   HIPCHECK(up(b->o_tile_base, b->tile_base.data(), np * 8), err);
   HIPCHECK(up(b->o_items, b->items.data(), b->items.size() * sizeof(WorkItem)), err);
   HIPCHECK(up(b->o_ba_tile_off, b->ba_tile_off.data(), b->ba_tile_off.size() * 8), err);
   HIPCHECK(up(b->l_level, b->level_pages.data(), b->level_pages.size() * 4), err);
+  HIPCHECK(up(b->l_level_bw1, b->level_pages_bw1.data(), b->level_pages_bw1.size() * 4), err);
   HIPCHECK(up(b->l_scan, b->scan_pages.data(), b->scan_pages.size() * 4), err);
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_dict_ba, b->dict_ba_chunks.data(), b->dict_ba_chunks.size() * 4), err);
@@ -786,6 +839,9 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.chunks = (const ChunkDesc *)(A + b->o_chunks);
   d.chunk_err = (unsigned long long *)(A + b->o_err);
   d.page_nn = (uint32_t *)(A + b->o_nn);
+  d.page_nn_v = (uint32_t *)(A + b->o_nnv);
+  d.spec_mismatch = (uint32_t *)(A + b->o_spec_flag);
+  d.spec = b->spec ? 1u : 0u;
   d.page_rec = (uint32_t *)(A + b->o_rec);
   d.page_vbase = (uint64_t *)(A + b->o_vbase);
   d.page_rbase = (uint64_t *)(A + b->o_rbase);
@@ -806,6 +862,8 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   LaunchLists l;
   l.level_pages = (const uint32_t *)(A + b->l_level);
   l.n_level_pages = (uint32_t)b->level_pages.size();
+  l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
+  l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
   l.scan_pages = (const uint32_t *)(A + b->l_scan);
   l.n_scan_pages = (uint32_t)b->scan_pages.size();
   l.base_chunks = (const uint32_t *)(A + b->l_base);
@@ -851,15 +909,33 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(hipMemsetAsync(A + b->f_begin, 0xff, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
-  HIPCHECK(timed(b, 4, s, [&] { return launch_dict_ba(d, l, s); }), err);
-  HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
-  HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
-  HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
-  {  // DELTA work items and the other value work items as two launches (separately profiled)
-    LaunchLists l1 = l, l2 = l;
-    l1.n_items = b->n_delta_items;
-    l2.items = l.items + b->n_delta_items;
-    l2.n_items = l.n_items - b->n_delta_items;
+  // DELTA work items and the other value work items go out as two launches (separately profiled).
+  LaunchLists l1 = l, l2 = l;
+  l1.n_items = b->n_delta_items;
+  l2.items = l.items + b->n_delta_items;
+  l2.n_items = l.n_items - b->n_delta_items;
+  if (b->spec) {
+    // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
+    // side stream concurrently with the level decode; k_bases then checks the header counts
+    // the values path used against the decoded ones (sync_impl re-runs serially on a miss).
+    hipStream_t v = b->ctx->side;
+    if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
+    if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
+    HIPCHECK(hipEventRecord(b->ev_fork, s), err);
+    HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
+    HIPCHECK(timed(b, 4, v, [&] { return launch_dict_ba(d, l, v); }), err);
+    HIPCHECK(timed(b, 2, v, [&] { return launch_scan_runs(d, l, v); }), err);
+    HIPCHECK(timed(b, 1, v, [&] { return launch_values(d, l1, v); }), err);
+    HIPCHECK(timed(b, 8, v, [&] { return launch_values(d, l2, v); }), err);
+    HIPCHECK(hipEventRecord(b->ev_join, v), err);
+    HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+  } else {
+    HIPCHECK(timed(b, 4, s, [&] { return launch_dict_ba(d, l, s); }), err);
+    HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
     HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l1, s); }), err);
     HIPCHECK(timed(b, 8, s, [&] { return launch_values(d, l2, s); }), err);
   }
@@ -941,6 +1017,17 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   clear_err(err);
   HIPCHECK(hipStreamSynchronize(s), err);
   if (!b->decoded) return PQ_OK;
+  if (b->spec) {
+    uint32_t miss = 0;
+    HIPCHECK(hipMemcpy(&miss, b->d_arena + b->o_spec_flag, 4, hipMemcpyDeviceToHost), err);
+    if (miss) {  // a page header's non-null count was wrong: decode again in serial order
+      b->force_serial = true;
+      b->uploaded = false;
+      int e = decode_impl(b, s, err);
+      if (e) return e;
+      HIPCHECK(hipStreamSynchronize(s), err);
+    }
+  }
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
   std::vector<uint64_t> keys(nc), vbase(np), rbase(np);
   std::vector<uint32_t> nn(np), rec(np);
@@ -1042,7 +1129,9 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   pqgpu_ctx *c = new pqgpu_ctx();
   c->device = device;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     set_err(err, PQ_ERR_HIP, -1, -1, hipGetErrorString(e));
     return PQ_ERR_HIP;
@@ -1055,6 +1144,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
 
@@ -1142,7 +1232,10 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (!b->ctx) { delete b; return; }
   (void)hipSetDevice(b->ctx->device);
   (void)hipStreamSynchronize(b->ctx->stream);
+  (void)hipStreamSynchronize(b->ctx->side);
   free_payloads(b);
+  if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+  if (b->ev_join) (void)hipEventDestroy(b->ev_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_stage) (void)hipFree(b->d_stage);
   if (b->h_pinned) (void)hipHostFree(b->h_pinned);
@@ -1159,6 +1252,7 @@ int pqgpu_batch_reset(pqgpu_batch *b) {
   b->pages.clear();
   b->stage.clear();
   b->uploaded = b->decoded = false;
+  b->force_serial = spec_disabled();
   b->stats = pqgpu_batch_stats{};
   return PQ_OK;
 }

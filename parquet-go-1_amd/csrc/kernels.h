@@ -12,7 +12,11 @@ struct BatchDev {
   const PageDesc *pages;
   const ChunkDesc *chunks;
   unsigned long long *chunk_err;  // [nchunks] first-error key (atomicMin), init ~0
-  uint32_t *page_nn;              // [npages] decoded non-null count
+  uint32_t *page_nn;              // [npages] decoded non-null count (written by k_levels)
+  uint32_t *page_nn_v;            // [npages] non-null count the values kernels use: a copy of
+                                  // page_nn (serial mode, k_bases) or the page header's count
+                                  // (speculative mode, uploaded; k_bases verifies it)
+  uint32_t *spec_mismatch;        // speculative mode: set when a header count differs from page_nn
   uint32_t *page_rec;             // [npages] records (rep == 0) per page
   uint64_t *page_vbase;           // [npages] value base within chunk
   uint64_t *page_rbase;           // [npages] record base within chunk
@@ -24,6 +28,7 @@ struct BatchDev {
   uint32_t *ba_tile_sum;          // BYTE_ARRAY: per 4096-value tile payload sum
   unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
+  uint32_t spec;                  // 1: value bases came from the page headers (see k_bases)
 };
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
@@ -31,7 +36,8 @@ constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kBaTile = 4096;     // values per BYTE_ARRAY scan tile
 
 struct LaunchLists {
-  const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams
+  const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams (generic)
+  const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
   const WorkItem *items; uint32_t n_items;               // values work items

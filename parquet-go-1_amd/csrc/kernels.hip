@@ -83,7 +83,10 @@ DEV uint64_t bits64c(const uint8_t *p, uint32_t n, uint64_t bo, uint32_t nb) {  
 
 DEV uint32_t lane_id() { return __lane_id(); }
 
-// Diagnostic phase stamps (PQ_DEBUG_STAMPS=1 only): per-wave cycle sums added to b.dbg.
+// Diagnostic phase stamps: per-wave cycle sums added to b.dbg. Compiled in only for the
+// diagnostic library (make diag -> lib/libpqgpu_diag.so, -DPQ_DIAG_STAMPS) and active there
+// when PQ_DEBUG_STAMPS=1; the production kernels carry no stamp code or registers.
+#ifdef PQ_DIAG_STAMPS
 DEV uint64_t stamp() { return __builtin_amdgcn_s_memtime(); }
 struct Stamps {
   unsigned long long *dbg;
@@ -96,7 +99,18 @@ struct Stamps {
     if (dbg && __lane_id() == 0)
       for (int k = 0; k < 8; k++) if (acc[k]) atomicAdd(&dbg[base + k], (unsigned long long)acc[k]);
   }
+  DEV void count(int k) { if (dbg) acc[k]++; }
 };
+#define PQ_STAMPS(name, dbgp) Stamps name{dbgp, 0, {0, 0, 0, 0, 0, 0, 0, 0}}
+#else
+struct Stamps {
+  DEV void begin() {}
+  DEV void lap(int) {}
+  DEV void flush(int) {}
+  DEV void count(int) {}
+};
+#define PQ_STAMPS(name, dbgp) Stamps name
+#endif
 DEV uint32_t rdlane(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
 DEV uint32_t wave_excl_scan(uint32_t v) {
@@ -301,12 +315,12 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
       __syncthreads();
       stage_load(L.stage, s, sb, n);
       __syncthreads();
-      if (st) { st->lap(0); st->acc[5]++; }
+      if (st) { st->lap(0); st->count(5); }
     }
     // ---- speculative header decode at c = pos + lane
     const uint32_t c = pos + lane;
     const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
-    if (st) { (void)__builtin_amdgcn_readfirstlane(h.err + h.adv + h.nvals); st->lap(1); st->acc[6]++; }
+    if (st) { (void)__builtin_amdgcn_readfirstlane(h.err + h.adv + h.nvals); st->lap(1); st->count(6); }
     // ---- follow the true chain lane to lane (scalar registers)
     uint64_t mask = 0;
     uint32_t cum = 0, p = 0, next_pos = pos;
@@ -438,135 +452,101 @@ struct LevelSink {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Level decoder: one workgroup per page with level streams.
+//
+// A hybrid stream (hybrid_decoder.go:81-165) is a chain of run headers: the position
+// of run k+1 is known only once run k's header is decoded. The stream is processed in
+// chunks of kLvChunk candidate header positions (the chunk plus the bytes past its end
+// are staged in LDS):
+//  P1  every position is decoded as if a run header started there. A header varint of
+//      at most 4 bytes whose run is well formed and complete inside the stream is a
+//      link p -> p + adv carrying the run's value count; anything else (errors, runs cut
+//      by EOF, longer varints) is a stop: a self-link with no values.
+//  P1b kLvRounds pointer-doubling rounds in LDS turn the links into 16-run jumps that
+//      carry the sum of the runs' value counts (saturating).
+//  P2  one lane follows the true chain from the chunk's entry by jumps, recording a
+//      checkpoint (position, value index) per jump; stops are decoded exactly
+//      (decode_hdr) and recorded as one-run checkpoints. The walk also finds where the
+//      reference's loop ends: the run that reaches num_values, an error run, or a
+//      bit-packed run cut by EOF.
+//  P3  one lane per checkpoint re-walks its <= 16 runs and expands them. Bit width 1
+//      with validity output only (flat OPTIONAL columns) ORs whole 32-bit words of
+//      payload into the LDS bitmap; other widths go through LevelSink::piece.
+// Results equal the reference's decodePackedArray loop exactly, including the error
+// class and the value position of the first error.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLvThreads = 64;             // one wave per page: no cross-wave barriers
+constexpr uint32_t kLvChunk = 1024;             // candidate header positions per chunk
+constexpr uint32_t kLvRounds = 4;               // doubling rounds: a jump spans 16 runs
+constexpr uint32_t kLvStageB = kLvChunk + 256;  // staged bytes: the chunk + headers / payload past its end
+constexpr uint32_t kLvMaxCk = kLvThreads;       // checkpoints per chunk (one fill lane each)
+constexpr uint32_t kLvMaxSlow = 32;             // exactly decoded runs per chunk
+constexpr uint32_t kLvLongRun = 512;            // runs longer than this expand cooperatively
+constexpr uint32_t kLvMaxLong = 64;
+constexpr uint32_t kNone = 0xffffffffu;
+enum : uint32_t { LV_RUN = 0, LV_STOP_NEED = 1, LV_STOP_ERR = 2, LV_STOP_TRUNC = 3 };
+
 struct LevelLDS {
-  WalkLDS walk;
+  uint32_t stage[kLvStageB / 4 + 4];
+  uint2 JV[kLvChunk];        // x: link / jump target of each position (>= chunk end: leaves the chunk)
+                             // y: values of the runs the jump passes (saturating at 2^31 - 1)
+  uint32_t ck_pos[kLvMaxCk + 1], ck_cum[kLvMaxCk], ck_slow[kLvMaxCk];
+  uint32_t slow_adv[kLvMaxSlow], slow_nv[kLvMaxSlow], slow_ok[kLvMaxSlow], slow_val[kLvMaxSlow],
+      slow_bp[kLvMaxSlow];
+  uint32_t long_f[kLvMaxLong], long_cnt[kLvMaxLong], long_bp[kLvMaxLong], long_val[kLvMaxLong];
+  uint32_t nck, nlong, stop_kind, stop_code, stop_vpos, next_e, done_out;
+  uint64_t cnt[16];
   uint32_t bits[kSegSlots / 32];
 };
 
-// One wave per page with level streams: repetition levels (counted: records start
-// where rep == 0), then definition levels (validity bitmap built in LDS, flushed with
-// coalesced stores). One call site of the walker for both streams.
-// Reference: page_v1.go:42-48 / page_v2.go:40-46 readValues -> decodePackedArray.
-__global__ void __launch_bounds__(64) k_levels_serial(BatchDev b, const uint32_t *pages) {
-  __shared__ LevelLDS lds;
-  const uint32_t pi = pages[blockIdx.x];
-  const PageDesc pd = b.pages[pi];
-  const ChunkDesc &cd = b.chunks[pd.chunk];
-  const uint8_t *base = (const uint8_t *)pd.data;
-  const uint32_t lane = lane_id();
-  const uint32_t ns = pd.num_slots;
-  uint32_t *vbits = (uint32_t *)cd.validity;
-  for (uint32_t k = lane; k < kSegSlots / 32; k += 64) lds.bits[k] = 0;
-  uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
-  for (uint32_t which = 0; which < 2; which++) {
-    const bool rep = which == 0;
-    if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
-    LevelSink sk;
-    sk.s = base + (rep ? pd.rep_off : pd.def_off);
-    sk.n = rep ? pd.rep_len : pd.def_len;
-    sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
-    sk.out = rep ? (uint8_t *)cd.rep_levels + pd.slot_base
-                 : (cd.def_levels ? (uint8_t *)cd.def_levels + pd.slot_base : nullptr);
-    sk.bits_lds = rep ? nullptr : lds.bits;
-    sk.bits_glob = rep ? nullptr : vbits;
-    sk.slot_base = pd.slot_base;
-    sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
-    sk.count = 0;
-    sk.err_code = 0;
-    sk.err_pos = 0;
-    sk.stage_len = kStage;
-    __syncthreads();
-    if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
-      if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
-    } else {
-      Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
-      st.begin();
-      hyb_walk(lds.walk, sk.s, sk.n, sk.bw, ns, sk, b.dbg ? &st : nullptr);
-      st.flush(0);
-    }
-    const uint64_t cntv = wave_sum64(sk.count);
-    if (sk.err_code) {
-      if (lane == 0) {
-        report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
-        b.page_nn[pi] = 0;
-        if (rep) b.page_rec[pi] = (uint32_t)cntv;
-      }
-      return;  // the reference fails the page at the first level error
-    }
-    if (rep) {
-      if (lane == 0) b.page_rec[pi] = (uint32_t)cntv;
-    } else {
-      nn = (uint32_t)cntv;
-    }
+// Fast candidate at stream position c: a header varint of at most 4 bytes whose run is
+// well formed and complete inside the stream (RLE value < 2^bw, bit-packed payload before
+// EOF). Returns the next position's offset (adv; 0 marks a stop that decode_hdr resolves),
+// the run's value count, its kind and its RLE value / payload position.
+struct FastHdr { uint32_t adv, nvals, bp, value; };
+DEV FastHdr fast_hdr(const uint32_t *stg, uint32_t sb, uint32_t c, uint32_t n, uint32_t bw, uint32_t rs) {
+  FastHdr f{0, 0, 0, 0};
+  if (c >= n) return f;
+  const uint32_t o = c - sb, a = o >> 2, sh = o & 3;
+  const uint32_t w0 = stg[a], w1 = stg[a + 1], w2 = stg[a + 2];
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  const uint32_t t = ~u0 & 0x80808080u;  // varint terminators among bytes 0..3
+  if (!t) return f;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t) >> 3) + 1;
+  uint32_t y = L >= 4 ? u0 : (u0 & ((1u << (8 * L)) - 1u));
+  y &= 0x7f7f7f7fu;
+  const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+  const uint32_t cnt = h >> 1;
+  if (cnt == 0) return f;
+  if (h & 1) {
+    const uint64_t adv = L + (uint64_t)cnt * bw;
+    if (c + adv > n) return f;
+    f.adv = (uint32_t)adv; f.nvals = cnt * 8; f.bp = 1; f.value = c + L;
+  } else {
+    const uint32_t adv = L + rs;
+    if (c + adv > n) return f;
+    const uint64_t x = ((uint64_t)u1 << 32) | u0;
+    const uint32_t v = (uint32_t)(x >> (8 * L));
+    const uint32_t val = rs >= 4 ? v : (v & ((1u << (8 * rs)) - 1u));
+    if (bw < 32 && (val >> bw) != 0) return f;
+    f.adv = adv; f.nvals = cnt; f.value = val;
   }
-  if (cd.max_def > 0) {
-    __syncthreads();
-    // flush the LDS bitmap segment to the chunk bitmap
-    const uint32_t seg = min(ns, kSegSlots);
-    const uint32_t nw = (seg + 31) / 32;
-    const uint32_t sh = (uint32_t)(pd.slot_base & 31);
-    const uint64_t w0 = pd.slot_base >> 5;
-    for (uint32_t k = lane; k < nw; k += 64) {
-      uint32_t v = lds.bits[k];
-      if (k == nw - 1 && (seg & 31)) v &= (1u << (seg & 31)) - 1u;
-      if (sh == 0) {
-        if (k == 0 || k == nw - 1) atomicOr(&vbits[w0 + k], v);
-        else vbits[w0 + k] = v;
-      } else if (v) {
-        atomicOr(&vbits[w0 + k], v << sh);
-        uint32_t hi = v >> (32 - sh);
-        if (hi) atomicOr(&vbits[w0 + k + 1], hi);
-      }
-    }
-  }
-  if (lane == 0) b.page_nn[pi] = nn;
+  return f;
 }
 
-// ---------------------------------------------------------------------------
-// Parallel level decoder: one 256-thread workgroup per page (replaces the serial
-// per-page chain walk of k_levels_serial for every page).
-//
-// The RLE/bit-packed hybrid stream (hybrid_decoder.go:77-131) is a chain of run
-// headers: the position of run k+1 is known only after run k's header is decoded.
-// The stream is processed in chunks of kLvChunk byte positions, each split into
-// 64-position windows:
-//  1. every position of the chunk is decoded as if a run header started there
-//     (decode_hdr; invalid candidates inside payloads are harmless) and, inside its
-//     window, the chain is followed by pointer doubling over the wave's lanes
-//     (6 shuffle rounds) to the exit position X (first chain position >= window end);
-//  2. one thread follows X from the chunk's entry: the true chain's entry position in
-//     each window it touches (one LDS read per window instead of one hop per run);
-//  3. per window, the chain lanes are marked from the entry (register chase) and the
-//     window's value total is summed;
-//  4. window totals are prefix-summed: every true run knows its first value index;
-//  5. the first run that stops the reference's loop (error, EOF-truncated bit-packed
-//     run, or the run that reaches num_values) is found with an LDS atomicMin on
-//     (value index, position);
-//  6. runs before the stop (and the stop's partial run) expand in parallel into the
-//     validity bitmap / level arrays (LevelSink).
-// Results equal the serial walk's exactly, including error class and position.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kLvChunk = 2048;             // candidate header positions per chunk
-constexpr uint32_t kLvWin = kLvChunk / 64;      // windows per chunk
-constexpr uint32_t kLvStage = kLvChunk + 2048;  // staged bytes: the chunk + payloads of its last runs
-constexpr uint32_t kNone = 0xffffffffu;
-constexpr uint32_t kRecErr = 1u << 31, kRecBp = 1u << 30;
-
-struct LevelParLDS {
-  uint32_t stage[kLvStage / 4 + 8];
-  uint32_t X[kLvChunk];      // exit position of each candidate header
-  uint32_t recA[kLvChunk];   // candidate run: count (30 bits) | kRecBp | kRecErr
-  uint32_t recB[kLvChunk];   // RLE value, bit-packed payload position, or the error class
-  uint8_t adv[kLvChunk];     // header + payload bytes, clamped to 64 (chain steps inside a window)
-  uint32_t entry[kLvWin];    // true chain's first position in each window (kNone: skipped)
-  uint64_t mask[kLvWin];     // true chain's lanes per window
-  uint64_t tot[kLvWin];      // values in each window's true runs
-  uint64_t wpre[kLvWin];     // value index of each window's first true run
-  unsigned long long stop_key;
-  uint64_t chunk_tot, cnt[4];
-  uint32_t next_pos, stop_err, stop_pos;
-  uint32_t bits[kSegSlots / 32];
-};
+// Bits [slot, slot + 32) (page-relative) of the validity bitmap, masked by m: the LDS
+// segment for the first kSegSlots slots of the page, the chunk's global bitmap beyond.
+DEV void lv_or_bits(LevelSink &sk, uint32_t slot, uint32_t m) {
+  if (!m) return;
+  if (slot + 32 <= kSegSlots) {
+    const uint32_t w = slot >> 5, sh = slot & 31;
+    atomicOr(&sk.bits_lds[w], m << sh);
+    if (sh && (m >> (32 - sh))) atomicOr(&sk.bits_lds[w + 1], m >> (32 - sh));
+  } else {
+    sk.set_bits(slot, m, 32);
+  }
+}
 
 DEV void stage_load_blk(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n, uint32_t words) {
   const uint8_t *src = s + sb;
@@ -577,162 +557,182 @@ DEV void stage_load_blk(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n
   }
 }
 
-DEV uint64_t wave_excl_scan64(uint64_t v) { return wave_incl_scan64(v) - v; }
-// Run value counts are clamped to `need` (exact for every run up to the stopping one);
-// with need <= 2^25 a window's 64 counts sum within 32 bits and the DPP scan applies.
-DEV uint64_t lv_excl(uint32_t v, bool small) {
-  return small ? (uint64_t)(wave_incl_scan32(v) - v) : wave_excl_scan64(v);
-}
-DEV uint64_t lv_sum(uint32_t v, bool small) { return small ? rdlane(wave_incl_scan32(v), 63) : wave_sum64(v); }
-
-// Values of a cached candidate run and how many of them the reference returns before
-// EOF (a bit-packed run whose payload is cut by the end of the stream, decode_hdr).
-DEV uint32_t rec_nvals(uint32_t A) {
-  const uint32_t cnt = A & (kRecBp - 1);
-  return (A & kRecBp) ? (cnt >= (1u << 28) ? 0x7fffffffu : cnt * 8) : cnt;
-}
-DEV uint32_t rec_okvals(uint32_t A, uint32_t B, uint32_t nv, uint32_t n, uint32_t bw) {
-  if (!(A & kRecBp)) return nv;
-  const uint64_t pb = (uint64_t)(A & (kRecBp - 1)) * bw;
-  if ((uint64_t)B + pb <= n) return nv;
-  const uint64_t g = B >= n ? 0 : ((uint64_t)(n - B) + bw - 1) / bw;
-  const uint64_t ok = g * 8;
-  return ok > nv ? nv : (uint32_t)ok;
-}
-
-// Decode `need` values of one hybrid stream into the sink; every thread of the
-// workgroup calls this (all control flow is workgroup-uniform).
-DEV void lv_walk(LevelParLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
-  const uint8_t *s = sk.s;
-  const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6, nwv = blockDim.x >> 6;
-  const bool small = need <= (1u << 25);
-  uint32_t pos0 = 0;
-  uint64_t done = 0;
-  for (;;) {
-    if (done >= need) break;
-    if (pos0 >= n) { sk.error((uint32_t)done, PQ_ERR_EOF); break; }  // next header read at EOF
-    const uint32_t cs = pos0, sb = cs & ~3u;
-    const uint32_t clen = min(kLvChunk, n - cs);
-    const uint32_t nw = (clen + 63) >> 6;
-    __syncthreads();
-    stage_load_blk(L.stage, s, sb, n, kLvStage / 4 + 8);
-    for (uint32_t w = tid; w < kLvWin; w += blockDim.x) L.entry[w] = kNone;
-    if (tid == 0) L.stop_key = ~0ull;
-    __syncthreads();
-    st.lap(0);
-    // 1. decode every candidate once (cached), exits by pointer doubling inside each window
-    for (uint32_t w = wv; w < nw; w += nwv) {
-      const uint32_t ws = cs + 64 * w, we = ws + 64, c = ws + lane, i = 64 * w + lane;
-      const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
-      L.recA[i] = h.err ? kRecErr : (h.bp ? kRecBp | h.cnt : h.cnt);  // cnt < 2^30
-      L.recB[i] = h.err ? h.err : h.value;
-      L.adv[i] = (uint8_t)min(h.adv, 64u);
-      uint32_t J = c + h.adv;
-#pragma unroll
-      for (int r = 0; r < 6; r++) {
-        const bool in = J < we;
-        const uint32_t Jt = (uint32_t)__shfl((int)J, (int)(in ? J - ws : lane), 64);
-        J = in ? Jt : J;
-      }
-      L.X[i] = J;
+// Expand one run (first value index f, cnt values) into the sink, from one lane.
+template <bool BW1>
+DEV void lv_emit_run(LevelSink &sk, const uint32_t *stg, uint32_t sb, uint32_t send, uint32_t f, uint32_t cnt,
+                     uint32_t bp, uint32_t value) {
+  if (cnt == 0) return;
+  if constexpr (BW1) {
+    if (!bp) {  // RLE: a constant run of ones (value == maxD) or zeros
+      if (value != sk.cmp) return;
+      sk.count += cnt;
+      for (uint32_t q = 0; q < cnt; q += 32) lv_or_bits(sk, f + q, cnt - q >= 32 ? ~0u : ((1u << (cnt - q)) - 1u));
+      return;
     }
-    __syncthreads();
-    st.lap(1);
-    // 2. the true chain's entry in each window it touches
-    if (tid == 0) {
-      const uint32_t ce = cs + clen;
-      uint32_t p = cs;
-      while (p < ce) {
-        L.entry[(p - cs) >> 6] = p;
-        p = L.X[p - cs];
-      }
-      L.next_pos = p;
+    // bit-packed, width 1: value k of the run is bit k of the payload (LSB first)
+    for (uint32_t q = 0; q < cnt; q += 32) {
+      const uint32_t by = value + (q >> 3);  // q is a multiple of 32: byte aligned
+      uint32_t w;
+      if (by >= sb && by + 4 <= send) w = lds_ld32(stg, by - sb);
+      else w = bits32c(sk.s, sk.n, (uint64_t)by * 8, 32);
+      if (cnt - q < 32) w &= (1u << (cnt - q)) - 1u;
+      sk.count += __popc(w);
+      lv_or_bits(sk, f + q, w);
     }
-    __syncthreads();
-    st.lap(2);
-    // 3. chain lanes and value totals per window
-    for (uint32_t w = wv; w < nw; w += nwv) {
-      const uint32_t e = L.entry[w];
-      uint64_t mask = 0, tot = 0;
-      if (e != kNone) {
-        const uint32_t ws = cs + 64 * w, i = 64 * w + lane;
-        const uint32_t adv = L.adv[i], A = L.recA[i];
-        uint32_t p = sgpr(e - ws);
-        while (p < 64) {
-          mask |= 1ull << p;
-          p = sgpr(p + rdlane(adv, p));
-        }
-        tot = lv_sum(((mask >> lane) & 1ull) ? min(rec_nvals(A), need) : 0u, small);
-      }
-      if (lane == 0) { L.mask[w] = mask; L.tot[w] = tot; }
-    }
-    __syncthreads();
-    st.lap(3);
-    // 4. value index of each window's first run
-    if (wv == 0) {
-      const uint64_t t = lane < nw ? L.tot[lane] : 0;
-      const uint64_t incl = wave_incl_scan64(t);
-      if (lane < nw) L.wpre[lane] = done + incl - t;
-      if (lane == 63) L.chunk_tot = incl;
-    }
-    __syncthreads();
-    st.lap(4);
-    // 5. expansion of every true run below need; the first run that ends the reference's
-    //    loop (error, EOF-cut bit-packed run, or the run reaching need) is found with an
-    //    atomicMin on (value index, position). Runs past an error stop may expand too:
-    //    the page then fails and its output is not used.
-    for (uint32_t w = wv; w < nw; w += nwv) {
-      const uint64_t mask = L.mask[w];
-      if (!mask) continue;
-      const uint32_t ws = cs + 64 * w, c = ws + lane, i = 64 * w + lane;
-      const uint32_t A = L.recA[i], B = L.recB[i];
-      const uint32_t nv = (A & kRecErr) ? 0u : rec_nvals(A);
-      const bool mine = (mask >> lane) & 1ull;
-      const uint64_t C = L.wpre[w] + lv_excl(mine ? min(nv, need) : 0u, small);
-      uint32_t cnt = 0;
-      if (mine && C < need) {
-        const uint64_t rem = need - C;
-        const uint32_t ok = (A & kRecErr) ? 0u : rec_okvals(A, B, nv, n, bw);
-        bool stop = true;
-        if (A & kRecErr) cnt = 0;
-        else if (ok < nv && ok < rem) cnt = ok;
-        else if (nv >= rem) cnt = (uint32_t)rem;
-        else { cnt = nv; stop = false; }
-        if (stop) atomicMin(&L.stop_key, (unsigned long long)((C << 32) | c));
-      }
-      sk.window(mine && cnt > 0, (uint32_t)C, cnt, (A & kRecBp) != 0, B, c, L.stage, sb);
-    }
-    __syncthreads();
-    st.lap(5);
-    const unsigned long long key = L.stop_key;
-    if (key != ~0ull) {
-      if (tid == 0) {  // the stopping run's outcome
-        const uint32_t c = (uint32_t)key, i = c - cs;
-        const uint64_t C = key >> 32;
-        const uint32_t A = L.recA[i], B = L.recB[i];
-        uint32_t e = 0, epos = (uint32_t)C;
-        if (A & kRecErr) {
-          e = B == kErrLongVarint ? resolve_long_varint(s, c, n) : B;
-        } else {
-          const uint32_t nv = rec_nvals(A), ok = rec_okvals(A, B, nv, n, bw);
-          if (ok < nv && ok < need - C) { e = PQ_ERR_EOF; epos = (uint32_t)(C + ok); }
-        }
-        L.stop_err = e;
-        L.stop_pos = epos;
-      }
-      __syncthreads();
-      if (L.stop_err) sk.error(L.stop_pos, L.stop_err);
-      break;
-    }
-    done += L.chunk_tot;
-    pos0 = L.next_pos;
-    st.acc[6]++;
+  } else {
+    for (uint32_t q = 0; q < cnt; q += 64)
+      sk.piece(bp != 0, value, f + q, q, min(64u, cnt - q), stg, sb);
   }
 }
 
-__global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *pages) {
-  __shared__ LevelParLDS lds;
+// A run found by a fill lane: short runs expand right away, long ones are queued for the
+// workgroup (the fill lanes would otherwise wait on the one lane holding a long run).
+template <bool BW1>
+DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uint32_t f, uint32_t cnt, uint32_t bp,
+                     uint32_t value) {
+  if (cnt > kLvLongRun && !(BW1 && !bp && value != sk.cmp)) {
+    const uint32_t slot = atomicAdd(&L.nlong, 1u);
+    if (slot < kLvMaxLong) {
+      L.long_f[slot] = f; L.long_cnt[slot] = cnt; L.long_bp[slot] = bp; L.long_val[slot] = value;
+      return;
+    }
+    atomicSub(&L.nlong, 1u);
+  }
+  lv_emit_run<BW1>(sk, L.stage, sb, send, f, cnt, bp, value);
+}
+
+// Decode `need` level values of one stream into the sink; every thread of the workgroup
+// calls this (control flow outside per-lane work is workgroup-uniform).
+template <bool BW1>
+DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
+  const uint8_t *s = sk.s;
+  const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  uint32_t pos0 = 0, done = 0;
+  for (;;) {
+    if (done >= need) break;
+    if (pos0 >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
+    const uint32_t cs = pos0, sb = cs & ~3u;
+    const uint32_t clen = min(kLvChunk, n - cs), cend = cs + clen, send = sb + kLvStageB;
+    __syncthreads();
+    st.lap(7);
+    stage_load_blk(L.stage, s, sb, n, kLvStageB / 4 + 4);
+    __syncthreads();
+    st.lap(0);
+    // ---- P1: links
+    for (uint32_t i = tid; i < clen; i += nt) {
+      const FastHdr f = fast_hdr(L.stage, sb, cs + i, n, bw, rs);
+      L.JV[i] = make_uint2(cs + i + f.adv, f.nvals);
+    }
+    __syncthreads();
+    st.lap(1);
+    // ---- P1b: pointer doubling, in place. A (target, values) pair is read and written as
+    // one 8-byte LDS access, so a pair another lane already advanced this round is still a
+    // consistent (longer) jump: after the rounds every jump spans at least 2^kLvRounds runs
+    // (or ends on a stop / past the chunk), which is all P2 and P3 rely on.
+    for (uint32_t r = 0; r < kLvRounds; r++) {
+      for (uint32_t i = tid; i < clen; i += nt) {
+        const uint2 a = L.JV[i];
+        if (a.x < cend) {
+          const uint2 c2 = L.JV[a.x - cs];
+          L.JV[i] = make_uint2(c2.x, min(a.y + c2.y, 0x7fffffffu));
+        }
+      }
+    }
+    __syncthreads();
+    st.lap(2);
+    // ---- P2: the true chain by jumps (one lane)
+    if (tid == 0) {
+      __builtin_amdgcn_s_setprio(3);  // the serial walk is the page's critical path
+      uint32_t p = cs, cum = done, kind = LV_RUN, code = 0, vpos = 0, nck = 0, ns = 0;
+      for (;;) {
+        if (p >= cend) break;
+        if (nck == kLvMaxCk) break;  // checkpoint table full: the next chunk starts at p
+        const uint2 jv = L.JV[p - cs];
+        const uint32_t j = jv.x, v = jv.y;
+        L.ck_pos[nck] = p;
+        L.ck_cum[nck] = cum;
+        if (j != p) {  // a jump over fast runs (it may end on a stop)
+          L.ck_slow[nck++] = kNone;
+          if ((uint64_t)cum + v >= need) { kind = LV_STOP_NEED; break; }
+          cum += v;
+          p = j;
+          continue;
+        }
+        // p is a stop: the exact decoder (hybrid_decoder.go:142-165)
+        if (ns == kLvMaxSlow) break;  // slow table full: the next chunk starts at p
+        const Hdr h = decode_hdr(L.stage, sb, s, p, n, bw, rs);
+        L.slow_adv[ns] = h.adv; L.slow_nv[ns] = h.err ? 0 : h.nvals; L.slow_ok[ns] = h.err ? 0 : h.okvals;
+        L.slow_val[ns] = h.value; L.slow_bp[ns] = h.bp;
+        L.ck_slow[nck++] = ns++;
+        if (h.err) {
+          kind = LV_STOP_ERR; vpos = cum;
+          code = h.err == kErrLongVarint ? resolve_long_varint(s, p, n) : h.err;
+          break;
+        }
+        if (h.okvals < h.nvals && h.okvals < need - cum) {
+          kind = LV_STOP_TRUNC; vpos = cum + h.okvals; code = PQ_ERR_EOF;
+          break;
+        }
+        if (h.nvals >= need - cum) { kind = LV_STOP_NEED; break; }
+        cum += h.nvals;
+        p += h.adv;
+      }
+      L.ck_pos[nck] = kind == LV_RUN ? p : kNone;  // walk bound of the last checkpoint
+      L.nck = nck; L.stop_kind = kind; L.stop_code = code; L.stop_vpos = vpos;
+      L.next_e = p; L.done_out = cum; L.nlong = 0;
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+    st.lap(3);
+    // ---- P3: one lane per checkpoint re-walks its runs and expands them
+    const uint32_t nck = L.nck;
+    for (uint32_t k = tid; k < nck; k += nt) {
+      uint32_t p = L.ck_pos[k], C = L.ck_cum[k];
+      const uint32_t sl = L.ck_slow[k];
+      if (sl != kNone) {
+        const uint32_t nvv = L.slow_nv[sl], ok = L.slow_ok[sl];
+        if (C < need) lv_fill_run<BW1>(L, sk, sb, send, C, min(min(nvv, ok), need - C), L.slow_bp[sl], L.slow_val[sl]);
+        continue;
+      }
+      const uint32_t bound = min(L.ck_pos[k + 1], cend);
+      while (p < bound && C < need) {
+        const FastHdr f = fast_hdr(L.stage, sb, p, n, bw, rs);
+        if (!f.adv) break;  // a stop: the next checkpoint
+        lv_fill_run<BW1>(L, sk, sb, send, C, min(f.nvals, need - C), f.bp, f.value);
+        C += f.nvals;
+        p += f.adv;
+      }
+    }
+    st.lap(4);
+    __syncthreads();
+    // long runs: every thread expands 32-value pieces (64 for the generic sink)
+    const uint32_t nlong = L.nlong;
+    for (uint32_t r = 0; r < nlong; r++) {
+      const uint32_t f = L.long_f[r], cnt = L.long_cnt[r], bp = L.long_bp[r], val = L.long_val[r];
+      constexpr uint32_t P = BW1 ? 32 : 64;
+      for (uint32_t q = tid * P; q < cnt; q += nt * P) {
+        const uint32_t m = min(P, cnt - q);
+        if constexpr (BW1) lv_emit_run<true>(sk, L.stage, sb, send, f + q, m, bp, bp ? val + q / 8 : val);
+        else sk.piece(bp != 0, val, f + q, q, m, L.stage, sb);
+      }
+    }
+    if (nlong) __syncthreads();
+    st.lap(5);
+    if (L.stop_kind != LV_RUN) {
+      if (L.stop_kind != LV_STOP_NEED) sk.error(L.stop_vpos, L.stop_code);
+      break;
+    }
+    done = L.done_out;
+    pos0 = L.next_e;
+  }
+}
+
+// BW1: every level stream of the pages is a bit-width-1 definition stream with validity
+// output only (flat OPTIONAL columns: max_def == 1, max_rep == 0).
+template <bool BW1, int NT>
+__global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pages) {
+  __shared__ LevelLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
@@ -742,7 +742,7 @@ __global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *page
   uint32_t *vbits = (uint32_t *)cd.validity;
   for (uint32_t k = tid; k < kSegSlots / 32; k += blockDim.x) lds.bits[k] = 0;
   uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
-  Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+  PQ_STAMPS(st, b.dbg);
   st.begin();
   for (uint32_t which = 0; which < 2; which++) {
     const bool rep = which == 0;
@@ -760,12 +760,12 @@ __global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *page
     sk.count = 0;
     sk.err_code = 0;
     sk.err_pos = 0;
-    sk.stage_len = kLvStage;
+    sk.stage_len = kLvStageB;
     __syncthreads();
     if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
       if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
     } else {
-      lv_walk(lds, sk, ns, st);
+      lv_walk<BW1>(lds, sk, ns, st);
     }
     const uint64_t wc = wave_sum64(sk.count);
     if (lane == 0) lds.cnt[wv] = wc;
@@ -808,7 +808,7 @@ __global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *page
       }
     }
   }
-  st.lap(7);
+  st.lap(6);
   st.flush(0);
   if (tid == 0) b.page_nn[pi] = nn;
 }
@@ -816,6 +816,14 @@ __global__ void __launch_bounds__(256) k_levels(BatchDev b, const uint32_t *page
 // ---------------------------------------------------------------------------
 // Value bases: exclusive scan of per-page non-null counts (and record counts)
 // within each chunk. One workgroup per chunk (pages per chunk are few).
+//
+// Serial mode: the value bases and the counts the values kernels use come from
+// k_levels (page_nn). Speculative mode (every page carries a non-null count in
+// its header, e.g. DataPageHeaderV2.num_nulls): the host uploaded those counts
+// and their bases, the values kernels ran concurrently with k_levels, and this
+// kernel only checks that the header counts equal the decoded ones — the
+// reference derives notNull from the definition levels (page_v1.go:49-52), so
+// any difference sends the batch back through the serial path (host.cpp).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_bases(BatchDev b, const uint32_t *chunks) {
   const ChunkDesc &cd = b.chunks[chunks[blockIdx.x]];
@@ -828,6 +836,13 @@ __global__ void __launch_bounds__(256) k_bases(BatchDev b, const uint32_t *chunk
     uint32_t gp = cd.first_page + p;
     uint64_t nv = p < cd.num_pages ? b.page_nn[gp] : 0;
     uint64_t nr = p < cd.num_pages ? b.page_rec[gp] : 0;
+    if (p < cd.num_pages) {
+      if (b.spec) {
+        if (b.page_nn_v[gp] != (uint32_t)nv) atomicOr(b.spec_mismatch, 1u);
+      } else {
+        b.page_nn_v[gp] = (uint32_t)nv;
+      }
+    }
     part_v[threadIdx.x] = nv;
     part_r[threadIdx.x] = nr;
     __syncthreads();
@@ -840,7 +855,7 @@ __global__ void __launch_bounds__(256) k_bases(BatchDev b, const uint32_t *chunk
       __syncthreads();
     }
     if (p < cd.num_pages) {
-      b.page_vbase[gp] = carry_v + part_v[threadIdx.x] - nv;
+      if (!b.spec) b.page_vbase[gp] = carry_v + part_v[threadIdx.x] - nv;
       b.page_rbase[gp] = carry_r + part_r[threadIdx.x] - nr;
     }
     __syncthreads();
@@ -886,7 +901,7 @@ __global__ void __launch_bounds__(64) k_scan_runs(BatchDev b, const uint32_t *pa
   __shared__ WalkLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
-  const uint32_t nn = b.page_nn[pi];
+  const uint32_t nn = b.page_nn_v[pi];
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
   uint32_t done = 0;
   if (nn && pd.dict_bw > 0) {
@@ -1277,7 +1292,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   uint32_t blk = 0;                                 // index of the next block
   const uint32_t g8 = mbvc / 8;                     // bytes per bit of miniblock width
   if (tid == 0) { L.err_code = 0; L.stop_val = limit; }
-  Stamps st{b.dbg, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+  PQ_STAMPS(st, b.dbg);
   st.begin();
   while ((uint64_t)blk * bs < limit) {
     // ---- (re)stage the window so that it starts at the next header
@@ -1441,7 +1456,7 @@ DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     carry += total;
     blk += nb;
     st.lap(4);
-    st.acc[5]++;
+    st.count(5);
     __syncthreads();
     st.lap(6);
     if (L.err_code || stop < limit || nb == 0) {
@@ -1540,7 +1555,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *item
   const WorkItem wi = items[blockIdx.x];
   const PageDesc &pd = b.pages[wi.page];
   const ChunkDesc &cd = b.chunks[pd.chunk];
-  const uint32_t nn = b.page_nn[wi.page];
+  const uint32_t nn = b.page_nn_v[wi.page];
   switch (wi.kind) {
     case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
@@ -1594,7 +1609,7 @@ __global__ void __launch_bounds__(256) k_ba_tile_sums(BatchDev b, const uint32_t
   const ChunkDesc &cd = b.chunks[ci];
   const uint64_t nn = cd.nn_capacity;  // actual NN is page_vbase of last page + page_nn
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn[lp] : 0;
+  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
   (void)nn;
   const uint64_t t = blockIdx.x;
   if (t * kBaTile >= total && !(t == 0)) return;
@@ -1616,7 +1631,7 @@ __global__ void __launch_bounds__(256) k_ba_tile_scan(BatchDev b, const uint32_t
   const uint32_t ci = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn[lp] : 0;
+  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
   const uint64_t ntiles = (total + kBaTile - 1) / kBaTile;
   uint32_t *ts = b.ba_tile_sum + tile_off[blockIdx.x];
   __shared__ uint64_t part[256];
@@ -1646,7 +1661,7 @@ __global__ void __launch_bounds__(256) k_ba_apply(BatchDev b, const uint32_t *ch
   const uint32_t ci = chunks[blockIdx.y];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn[lp] : 0;
+  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
   const uint64_t t = blockIdx.x;
   int32_t *offs = (int32_t *)cd.offsets;
   if (t == 0 && threadIdx.x == 0) offs[0] = 0;
@@ -1683,7 +1698,7 @@ __global__ void __launch_bounds__(256) k_ba_gather(BatchDev b, const uint32_t *c
   const uint32_t ci = chunks[blockIdx.y];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn[lp] : 0;
+  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
   const int32_t *offs = (const int32_t *)cd.offsets;
   uint8_t *pay = (uint8_t *)cd.payload;
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (uint64_t)gridDim.x * 256) {
@@ -1751,8 +1766,12 @@ hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s
   return hipGetLastError();
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
-  if (!l.n_level_pages) return hipSuccess;
-  hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(256), 0, s, b, l.level_pages);
+  if (l.n_level_pages_bw1)
+    hipLaunchKernelGGL((k_levels_t<true, kLvThreads>), dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b,
+                       l.level_pages_bw1);
+  if (l.n_level_pages)
+    hipLaunchKernelGGL((k_levels_t<false, kLvThreads>), dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b,
+                       l.level_pages);
   return hipGetLastError();
 }
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

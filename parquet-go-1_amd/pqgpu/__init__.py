@@ -27,7 +27,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "lib", "libpqgpu.so")
+LIB_PATH = os.environ.get("PQGPU_LIB") or os.path.join(_PKG, "lib", "libpqgpu.so")  # PQGPU_LIB: diagnostic build
 
 # Error classes (include/pqgpu.h)
 PQ_OK, PQ_ERR_EOF, PQ_ERR_UNEXPECTED_EOF, PQ_ERR_INVALID, PQ_ERR_UNSUPPORTED, PQ_ERR_DICT_INDEX = 0, 1, 2, 3, 4, 5

@@ -78,3 +78,17 @@ def test_file_reader_mirror(gpu_ctx):
     assert list(cols) == ["a"]
     orc = O.File(data).read_chunk(1, 0)
     pqtest.assert_chunk_equal(cols["a"], orc, "reader")
+
+
+def test_speculative_and_serial_schedules_agree(gpu_ctx, monkeypatch):
+    """V2 pages carry num_nulls, so values run concurrently with the level decode on header
+    counts (host.cpp decode_impl); PQ_SPEC=0 (the default) keeps the reference's serial order. Both must
+    give the oracle's bytes, including on a file whose num_nulls header is wrong."""
+    for name in ("cfg2_v2_small", "bad_v2_num_nulls", "edge_nulls_v2", "cfg4_v2"):
+        data = pqtest.load(name)
+        orc = pqtest.oracle_decode(data)
+        for serial in ("0", "1"):
+            monkeypatch.setenv("PQ_SPEC", "1" if serial == "0" else "0")
+            gpu = _gpu_decode(gpu_ctx, data)
+            for rg, col, r in orc:
+                pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"{name} serial={serial} rg{rg} col{col}")

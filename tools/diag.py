@@ -3,6 +3,7 @@ import os
 import sys
 import time
 os.environ["PQ_DEBUG_STAMPS"] = "1"
+os.environ.setdefault("PQGPU_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "parquet-go-1_amd", "lib", "libpqgpu_diag.so"))
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
@@ -26,10 +27,13 @@ dt = time.perf_counter() - t0
 d = b.debug_counters()
 pages = f.num_row_groups * 64 * 2
 print(f"decode {dt*1e3:.3f} ms for {rows} rows; {pages} level pages, {pages//2} DELTA pages")
-names = ["stage", "p1_exits", "p2_entries", "p3_masks", "p4_prefix", "p5_expand", "chunks#", "flush"]
+names = ["stage", "P1_links", "P1b_doubling", "P2_walk", "P3_fill", "P3_bar", "end", "chunk_top"]
 for k, n in enumerate(names):
     v = int(d[k])
     print(f"levels {n:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
+for k, nm in enumerate(["p3_mask", "p3_desc_scan", "p3_rle", "p3_owner_shfl", "p3_emit", "p3_tail"]):
+    v = int(d[16 + k])
+    print(f"levels {nm:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
 dn = ["reload", "hdr_walk", "unpack", "scan", "write", "batches#", "end_barrier", "-"]
 for k, n in enumerate(dn):
     v = int(d[8 + k])

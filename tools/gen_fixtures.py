@@ -219,6 +219,16 @@ def edge_cases():
     return files
 
 
+def pqinspect_uvar_bytes(x):
+    out = bytearray()
+    while True:
+        if x < 0x80:
+            out.append(x)
+            return bytes(out)
+        out.append((x & 0x7F) | 0x80)
+        x >>= 7
+
+
 def corrupt(files):
     """Byte-patched variants with known reference error classes."""
     out = {}
@@ -262,6 +272,20 @@ def corrupt(files):
         q = q2 + ((h >> 1) * 1 if h & 1 else 1)
     b4[runs[2]] = 0
     out["bad_def_empty_run"] = bytes(b4)
+    # V2 page header whose num_nulls disagrees with its definition levels: the reference
+    # ignores the field (notNull is counted from the levels, page_v2.go:47-50), so the file
+    # decodes; the GPU decoder's speculative value bases miss and it re-runs serially.
+    b5 = bytearray(files["cfg2_v2_small"])
+    ph, j = [(ph, j) for ph, j in pqinspect.pages(bytes(b5)) if ph[1] == 3][1]
+    nv, nulls = ph[8][1], ph[8][2]
+    zz = lambda v: pqinspect_uvar_bytes((v << 1) ^ (v >> 31))
+    pat = b"\x15" + zz(nv) + b"\x15" + zz(nulls)
+    k = bytes(b5).rfind(pat, 0, j)
+    assert k > 0
+    new = zz(nulls + 1) if len(zz(nulls + 1)) == len(zz(nulls)) else zz(nulls - 1)
+    q = k + 2 + len(zz(nv))
+    b5[q:q + len(new)] = new
+    out["bad_v2_num_nulls"] = bytes(b5)
     # truncated file: cut the last data page of cfg2_v2_small in half (chunk-level read error)
     out["truncated"] = files["cfg1"][: len(files["cfg1"]) // 2] + files["cfg1"][-(8 + 400):]
     return out
