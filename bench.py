@@ -34,22 +34,33 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md
 
 
-def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2):
-    """cfg2 file bytes. Null masks are nudged so that no DELTA page has a
-    non-null count ≡ 1 (mod 256) or ≤ 1 (Appendix A Q1: the reference fails on those)."""
+def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2, first_rg=0):
+    """cfg2 file bytes: row groups [first_rg, first_rg + rows / rg_rows) of one
+    logical file whose row group g is drawn from default_rng([seed, g]) (column a) and
+    default_rng([seed + 1, g]) (column b), so rank shards are a row-group partition of one file.
+    Null masks are nudged so that no DELTA page has a non-null count ≡ 1 (mod 256) or ≤ 1
+    (Appendix A Q1: the reference fails on those)."""
     import pyarrow as pa
     import pyarrow.parquet as pq
-    rng = np.random.default_rng(seed)
-    a = np.cumsum(rng.integers(0, 2**16, rows)).astype(np.int64)
-    m = rng.random(rows) < 0.1
+    nrg = max(1, -(-rows // rg_rows))
+    parts = []
+    for g in range(first_rg, first_rg + nrg):
+        n = min(rg_rows, rows - (g - first_rg) * rg_rows)
+        rng = np.random.default_rng([seed, g])
+        rng3 = np.random.default_rng([seed + 1, g])
+        # column a: running sum of uniform [0, 2^16) increments, restarted per row group at
+        # g * 2^15 * rg_rows (its expected start), so row group g is the same in every shard
+        parts.append((np.cumsum(rng.integers(0, 2**16, n)) + g * 2**15 * rg_rows, rng.random(n) < 0.1,
+                      rng3.random(n), rng3.random(n) < 0.1))
+    a = np.concatenate([p[0] for p in parts]).astype(np.int64)
+    m = np.concatenate([p[1] for p in parts])
+    b = np.concatenate([p[2] for p in parts])
+    m2 = np.concatenate([p[3] for p in parts])
     pages = m[: rows // page_rows * page_rows].reshape(-1, page_rows)
     nn = page_rows - pages.sum(1)
     for p in np.flatnonzero((nn % 256 == 1) | (nn <= 1)):
         k = np.flatnonzero(pages[p])[0]
         pages[p, k] = False  # one more non-null value
-    rng3 = np.random.default_rng(seed + 1)
-    b = rng3.random(rows)
-    m2 = rng3.random(rows) < 0.1
     t = pa.table({"a": pa.array(a, mask=m), "b": pa.array(b, mask=m2)})
     bio = io.BytesIO()
     pq.write_table(t, bio, use_dictionary=False, data_page_version="2.0", compression="NONE",
@@ -121,8 +132,14 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
     import pqgpu
+    from pqgpu import shard
 
-    data, truth = gen_cfg2(args.rows, seed=2 + 2 * rank)
+    # weak scaling: the logical file has 16 row groups of cfg2 per GPU; rank r decodes its
+    # contiguous row-group range (no collective on the data path)
+    rg_rows = 4_194_304
+    per_rank_rg = max(1, -(-args.rows // rg_rows))
+    g0, g1 = shard.row_group_range(per_rank_rg * world, rank, world)
+    data, truth = gen_cfg2(min(args.rows, (g1 - g0) * rg_rows), rg_rows=rg_rows, first_rg=g0)
     ctx = pqgpu.Context(local_rank if world > 1 else 0)
     f = pqgpu.File(data)
     b = pqgpu.Batch(ctx)
@@ -166,11 +183,7 @@ def main():
     st = b.stats()
     kern_ms, kern_n, kern_name = b.kernel_time()
     ktimes = b.kernel_times()
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = shard.max_over_ranks(dt, dist, device="cuda")
     ms_per_step = dt / args.steps * 1e3
     rows_total = args.rows * world
     out_gb = st.output_bytes * world / 1e9
@@ -181,6 +194,7 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes moved by that kernel per launch / its avg time
     kb = kernel_bytes(b, kern_name, st) or 0
     achieved = kb / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(kern_name, args.rows)
     line = {
         "metric": "decoded GB/s + rows/s per GPU and whole node (1/2/4/8); % HBM peak",
         "value": round(value, 2),
@@ -193,7 +207,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int64+f64 (bit copies), u8 levels",
-        "data": "synthetic (numpy default_rng seeds 2,3; pyarrow 25 writer)",
+        "data": "synthetic (numpy default_rng([2|3, row group]); pyarrow 25 writer)",
         "config": {"workload": "cfg2: INT64 DELTA_BINARY_PACKED + DOUBLE PLAIN, OPTIONAL 10% nulls, V2, "
                                "UNCOMPRESSED", "rows_per_gpu": args.rows, "row_groups_per_gpu": f.num_row_groups,
                    "page_rows": 65536, "parallelism": f"row-group shards x{world}"},
@@ -203,8 +217,8 @@ def main():
         "bytes_per_step": {"input": st.input_bytes, "output": st.output_bytes},
         "roofline": {"bound": "hbm", "kernel": kern_name, "kernel_ms": round(kern_ms, 4),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_launch": kb},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src, "bytes_per_launch": kb},
         "kernels": {k: {"ms": round(ms, 4), "launches_per_step": round(n / args.steps, 2),
                         "GBps": round(kernel_bytes(b, k, st) / (ms / 1e3) / 1e9, 1)
                         if kernel_bytes(b, k, st) is not None and ms > 0 else None}
@@ -220,6 +234,19 @@ def main():
     b.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, rows, path=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")):
+    """HBM bytes per launch of `kernel` from the committed PMC run of this same workload
+    (tools/pmc_traffic.sh + tools/pmc_summary.py: FETCH_SIZE / WRITE_SIZE in separate passes,
+    FETCH_SIZE doubled per the gfx950 calibration). rocprofv3 cannot run inside the bench
+    process, so the counters come from that run; None when absent or for another workload."""
+    if rows != 67_108_864 or not os.path.exists(path):
+        return None, None
+    k = json.load(open(path))["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_corrected"], os.path.relpath(path, ROOT)
 
 
 def kernel_bytes(b, name, st):

@@ -1,0 +1,358 @@
+// Package gpudecode binds the MI355X Parquet column-chunk decoder (libpqgpu,
+// C ABI in include/pqgpu.h) for github.com/fraugster/parquet-go.
+//
+// It is the Go half of the drop-in boundary described in INTEGRATION.md: the
+// reference's readChunk/readPages + pageReader.readValues
+// (chunk_reader.go:182-362, page_v1.go:33-63, page_v2.go:31-60) hand a whole
+// column chunk to the GPU; goparquet's in-package shim (gpu_pagereader.go)
+// presents the decoded chunk back as pageReaders.
+//
+// cgo pointer rules: C never retains Go memory. File bytes are copied into C
+// memory (the library borrows them for the lifetime of a File); result copies
+// go into Go slices passed for the duration of one call only.
+package gpudecode
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../parquet-go-1_amd/lib -lpqgpu -Wl,-rpath,${SRCDIR}/../../parquet-go-1_amd/lib
+#include <stdlib.h>
+#include <string.h>
+#include "pqgpu.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"io"
+	"unsafe"
+)
+
+// Error classes of include/pqgpu.h, mirrored as Go errors. EOF classes wrap the
+// io sentinels so that callers' errors.Is(err, io.EOF) keeps working
+// (readwrite_test.go:1004, :1049, :1097 in the reference).
+var (
+	ErrInvalid     = errors.New("invalid data")
+	ErrUnsupported = errors.New("unsupported")
+	ErrDictIndex   = errors.New("dict: invalid index")
+	ErrCRC         = errors.New("CRC32 check failed")
+	ErrDecompress  = errors.New("decompression failed")
+	ErrThrift      = errors.New("thrift decode error")
+	ErrRange       = errors.New("int32 out of range")
+	ErrHIP         = errors.New("HIP runtime error")
+)
+
+// DecodeError carries the failing chunk and page (page -1: chunk level, the
+// error readChunk/readPages return; otherwise the page whose readValues fails).
+type DecodeError struct {
+	Chunk, Page int
+	Msg         string
+	err         error
+}
+
+func (e *DecodeError) Error() string { return e.Msg }
+func (e *DecodeError) Unwrap() error { return e.err }
+
+func classErr(code C.int) error {
+	switch code {
+	case C.PQ_ERR_EOF:
+		return io.EOF
+	case C.PQ_ERR_UNEXPECTED_EOF:
+		return io.ErrUnexpectedEOF
+	case C.PQ_ERR_UNSUPPORTED:
+		return ErrUnsupported
+	case C.PQ_ERR_DICT_INDEX:
+		return ErrDictIndex
+	case C.PQ_ERR_CRC:
+		return ErrCRC
+	case C.PQ_ERR_DECOMPRESS:
+		return ErrDecompress
+	case C.PQ_ERR_THRIFT:
+		return ErrThrift
+	case C.PQ_ERR_RANGE:
+		return ErrRange
+	case C.PQ_ERR_HIP, C.PQ_ERR_NOMEM, C.PQ_ERR_ARG:
+		return ErrHIP
+	}
+	return ErrInvalid
+}
+
+func toErr(rc C.int, e *C.pqgpu_error) error {
+	if rc == C.PQ_OK {
+		return nil
+	}
+	return &DecodeError{Chunk: int(e.chunk), Page: int(e.page), Msg: C.GoString(&e.msg[0]), err: classErr(rc)}
+}
+
+// Context is one GPU (pqgpu_ctx). Not safe for concurrent use: one goroutine
+// per GPU, like the reference's FileReader (file_reader.go:18).
+type Context struct{ c *C.pqgpu_ctx }
+
+// NewContext opens GPU `device`; it fails when no MI355X is visible (there is
+// no CPU fallback).
+func NewContext(device int) (*Context, error) {
+	var e C.pqgpu_error
+	var c *C.pqgpu_ctx
+	if err := toErr(C.pqgpu_ctx_create(C.int(device), &c, &e), &e); err != nil {
+		return nil, err
+	}
+	return &Context{c}, nil
+}
+
+func (x *Context) Close() { C.pqgpu_ctx_destroy(x.c); x.c = nil }
+
+// File is a parsed footer over a C copy of the file bytes
+// (ReadFileMetaData file_meta.go:24-74 + makeSchema schema.go:1048-1079).
+type File struct {
+	f   *C.pqgpu_file
+	buf unsafe.Pointer
+	n   C.size_t
+}
+
+func OpenFile(data []byte) (*File, error) {
+	buf := C.malloc(C.size_t(len(data)) + 1)
+	if len(data) > 0 {
+		C.memcpy(buf, unsafe.Pointer(&data[0]), C.size_t(len(data)))
+	}
+	var e C.pqgpu_error
+	var f *C.pqgpu_file
+	if err := toErr(C.pqgpu_file_open((*C.uint8_t)(buf), C.size_t(len(data)), &f, &e), &e); err != nil {
+		C.free(buf)
+		return nil, err
+	}
+	return &File{f: f, buf: buf, n: C.size_t(len(data))}, nil
+}
+
+func (f *File) Close()             { C.pqgpu_file_close(f.f); C.free(f.buf); f.f = nil }
+func (f *File) NumRowGroups() int  { return int(C.pqgpu_file_num_row_groups(f.f)) }
+func (f *File) NumColumns() int    { return int(C.pqgpu_file_num_columns(f.f)) }
+func (f *File) RowGroupRows(rg int) int64 {
+	return int64(C.pqgpu_file_row_group_num_rows(f.f, C.int(rg)))
+}
+
+// Batch decodes a set of column chunks with one launch per kernel.
+type Batch struct{ b *C.pqgpu_batch }
+
+func NewBatch(ctx *Context) (*Batch, error) {
+	var e C.pqgpu_error
+	var b *C.pqgpu_batch
+	if err := toErr(C.pqgpu_batch_create(ctx.c, &b, &e), &e); err != nil {
+		return nil, err
+	}
+	return &Batch{b}, nil
+}
+
+func (b *Batch) Close() { C.pqgpu_batch_destroy(b.b); b.b = nil }
+
+// AddFileChunk plans column `col` of row group `rg` (readChunk chunk_reader.go:299-362).
+// A chunk-level error is returned here; the chunk id stays valid for Status.
+func (b *Batch) AddFileChunk(f *File, rg, col int, validateCRC bool) (int32, error) {
+	var e C.pqgpu_error
+	var id C.int32_t
+	crc := C.int(0)
+	if validateCRC {
+		crc = 1
+	}
+	err := toErr(C.pqgpu_batch_add_file_chunk(b.b, f.f, C.int(rg), C.int(col), crc, &id, &e), &e)
+	return int32(id), err
+}
+
+// ColumnInfo is a leaf column's schema facts (readColumnSchema schema.go:893-924).
+type ColumnInfo struct {
+	PhysicalType, TypeLength, MaxDef, MaxRep, Repetition int
+	Path                                                 string
+}
+
+// ChunkMeta is the subset of parquet.ColumnMetaData readChunk consults
+// (chunk_reader.go:299-362). Offsets are absolute positions in the buffer
+// passed to AddChunk; DictionaryPageOffset < 0 when unset.
+type ChunkMeta struct {
+	PhysicalType, Codec                     int
+	NumValues, TotalCompressedSize          int64
+	DataPageOffset, DictionaryPageOffset    int64
+	HasFilePath                             bool
+}
+
+// AddChunk plans one column chunk whose pages are in buf (the library copies
+// the page bytes it needs before returning, so buf may be Go memory).
+func (b *Batch) AddChunk(buf []byte, col ColumnInfo, meta ChunkMeta, validateCRC bool) (int32, error) {
+	var ci C.pqgpu_column_info
+	ci.physical_type = C.int32_t(col.PhysicalType)
+	ci.type_length = C.int32_t(col.TypeLength)
+	ci.max_def = C.int32_t(col.MaxDef)
+	ci.max_rep = C.int32_t(col.MaxRep)
+	ci.repetition = C.int32_t(col.Repetition)
+	var cm C.pqgpu_chunk_meta
+	cm.physical_type = C.int32_t(meta.PhysicalType)
+	cm.codec = C.int32_t(meta.Codec)
+	cm.num_values = C.int64_t(meta.NumValues)
+	cm.total_compressed_size = C.int64_t(meta.TotalCompressedSize)
+	cm.data_page_offset = C.int64_t(meta.DataPageOffset)
+	cm.dictionary_page_offset = C.int64_t(meta.DictionaryPageOffset)
+	if meta.HasFilePath {
+		cm.has_file_path = 1
+	}
+	crc := C.int(0)
+	if validateCRC {
+		crc = 1
+	}
+	var p *C.uint8_t
+	if len(buf) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(&buf[0]))
+	}
+	var e C.pqgpu_error
+	var id C.int32_t
+	err := toErr(C.pqgpu_batch_add_chunk(b.b, p, C.size_t(len(buf)), &ci, &cm, crc, &id, &e), &e)
+	return int32(id), err
+}
+
+// Decode launches every page of every chunk (asynchronous); Sync waits and
+// returns the first error in (chunk, page, stage, value) order.
+func (b *Batch) Decode() error {
+	var e C.pqgpu_error
+	return toErr(C.pqgpu_batch_decode(b.b, nil, &e), &e)
+}
+
+func (b *Batch) Sync() error {
+	var e C.pqgpu_error
+	return toErr(C.pqgpu_batch_sync(b.b, nil, &e), &e)
+}
+
+// Status is the error of chunk id alone (nil when it decoded).
+func (b *Batch) Status(id int32) error {
+	var e C.pqgpu_error
+	return toErr(C.pqgpu_batch_chunk_status(b.b, C.int32_t(id), &e), &e)
+}
+
+// Page is the pageReader-sized slice of a decoded chunk.
+type Page struct {
+	SlotFirst, SlotCount, ValueFirst, ValueCount int64
+}
+
+// Chunk holds one decoded column chunk in host memory.
+type Chunk struct {
+	PhysicalType, ValueWidth, MaxDef, MaxRep int
+	NumSlots, NumValues, NumRecords          int64
+	Values                                   []byte   // fixed-width values, little endian (non-null only)
+	Offsets                                  []int32  // BYTE_ARRAY: NumValues+1 offsets into Payload
+	Payload                                  []byte   // BYTE_ARRAY bytes
+	DefLevels, RepLevels                     []uint8  // nil when the level is constant 0
+	Validity                                 []uint32 // bit i = slot i is non-null; nil when MaxDef == 0
+	ListOffsets                              []int32  // MaxRep > 0: record starts, NumRecords+1 entries
+	Pages                                    []Page
+}
+
+// Result copies chunk id's outputs to host memory.
+func (b *Batch) Result(id int32) (*Chunk, error) {
+	var e C.pqgpu_error
+	var r C.pqgpu_chunk_result
+	if err := toErr(C.pqgpu_batch_chunk_result(b.b, C.int32_t(id), &r, &e), &e); err != nil {
+		return nil, err
+	}
+	ch := &Chunk{
+		PhysicalType: int(r.physical_type), ValueWidth: int(r.value_width),
+		MaxDef: int(r.max_def), MaxRep: int(r.max_rep),
+		NumSlots: int64(r.num_slots), NumValues: int64(r.num_values), NumRecords: int64(r.num_records),
+	}
+	var vp, op, pp, dp, rp, valp, lp unsafe.Pointer
+	if r.values != nil {
+		ch.Values = make([]byte, ch.NumValues*int64(ch.ValueWidth)+1)
+		vp = unsafe.Pointer(&ch.Values[0])
+	}
+	if r.offsets != nil {
+		ch.Offsets = make([]int32, ch.NumValues+1)
+		op = unsafe.Pointer(&ch.Offsets[0])
+		ch.Payload = make([]byte, int64(r.payload_bytes)+1)
+		pp = unsafe.Pointer(&ch.Payload[0])
+	}
+	if r.def_levels != nil {
+		ch.DefLevels = make([]uint8, ch.NumSlots+1)
+		dp = unsafe.Pointer(&ch.DefLevels[0])
+	}
+	if r.rep_levels != nil {
+		ch.RepLevels = make([]uint8, ch.NumSlots+1)
+		rp = unsafe.Pointer(&ch.RepLevels[0])
+	}
+	if r.validity != nil {
+		ch.Validity = make([]uint32, (ch.NumSlots+31)/32+1)
+		valp = unsafe.Pointer(&ch.Validity[0])
+	}
+	if r.list_offsets != nil {
+		ch.ListOffsets = make([]int32, ch.NumRecords+1)
+		lp = unsafe.Pointer(&ch.ListOffsets[0])
+	}
+	if err := toErr(C.pqgpu_batch_copy_chunk(b.b, C.int32_t(id), vp, (*C.int32_t)(op), (*C.uint8_t)(pp),
+		(*C.uint8_t)(dp), (*C.uint8_t)(rp), (*C.uint32_t)(valp), (*C.int32_t)(lp), &e), &e); err != nil {
+		return nil, err
+	}
+	if ch.Values != nil {
+		ch.Values = ch.Values[:ch.NumValues*int64(ch.ValueWidth)]
+	}
+	if ch.Payload != nil {
+		ch.Payload = ch.Payload[:int64(r.payload_bytes)]
+	}
+	if ch.DefLevels != nil {
+		ch.DefLevels = ch.DefLevels[:ch.NumSlots]
+	}
+	if ch.RepLevels != nil {
+		ch.RepLevels = ch.RepLevels[:ch.NumSlots]
+	}
+	pages, err := b.pages(id)
+	if err != nil {
+		return nil, err
+	}
+	ch.Pages = pages
+	return ch, nil
+}
+
+func (b *Batch) pages(id int32) ([]Page, error) {
+	var e C.pqgpu_error
+	var n C.int32_t
+	if err := toErr(C.pqgpu_batch_chunk_pages(b.b, C.int32_t(id), &n, nil, nil, nil, nil, 0, &e), &e); err != nil {
+		return nil, err
+	}
+	if n == 0 {
+		return nil, nil
+	}
+	cols := make([][]int64, 4)
+	for k := range cols {
+		cols[k] = make([]int64, int(n))
+	}
+	if err := toErr(C.pqgpu_batch_chunk_pages(b.b, C.int32_t(id), &n,
+		(*C.int64_t)(unsafe.Pointer(&cols[0][0])), (*C.int64_t)(unsafe.Pointer(&cols[1][0])),
+		(*C.int64_t)(unsafe.Pointer(&cols[2][0])), (*C.int64_t)(unsafe.Pointer(&cols[3][0])), n, &e), &e); err != nil {
+		return nil, err
+	}
+	out := make([]Page, int(n))
+	for k := range out {
+		out[k] = Page{cols[0][k], cols[1][k], cols[2][k], cols[3][k]}
+	}
+	return out, nil
+}
+
+// DefLevel returns the definition level of slot i (derived from Validity when
+// MaxDef == 1 and the levels are not materialised).
+func (ch *Chunk) DefLevel(i int64) int32 {
+	if ch.DefLevels != nil {
+		return int32(ch.DefLevels[i])
+	}
+	if ch.Validity == nil {
+		return 0
+	}
+	if ch.Validity[i>>5]>>(uint(i)&31)&1 == 1 {
+		return int32(ch.MaxDef)
+	}
+	return 0
+}
+
+// RepLevel returns the repetition level of slot i.
+func (ch *Chunk) RepLevel(i int64) int32 {
+	if ch.RepLevels == nil {
+		return 0
+	}
+	return int32(ch.RepLevels[i])
+}
+
+func (ch *Chunk) String() string {
+	return fmt.Sprintf("chunk{type %d, %d slots, %d values, %d pages}", ch.PhysicalType, ch.NumSlots, ch.NumValues, len(ch.Pages))
+}

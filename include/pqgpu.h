@@ -193,6 +193,15 @@ int pqgpu_batch_num_chunks(const pqgpu_batch *b);
 /* Per-chunk status after sync (the error of that chunk alone). */
 int pqgpu_batch_chunk_status(const pqgpu_batch *b, int32_t chunk_id, pqgpu_error *err);
 int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t chunk_id, pqgpu_chunk_result *out, pqgpu_error *err);
+/* Per-page split of a decoded chunk, the reference's pageReader granularity
+ * (ColumnStore.readNextPage data_store.go:236-260 reads one page at a time):
+ * data page k of the chunk owns level slots [slot_first[k], +slot_count[k])
+ * and non-null values [value_first[k], +value_count[k]) of the chunk result.
+ * Call with cap = 0 to query *num_pages. Valid after pqgpu_batch_sync. A
+ * chunk error's pqgpu_error.page names the page whose readValues fails. */
+int pqgpu_batch_chunk_pages(const pqgpu_batch *b, int32_t chunk_id, int32_t *num_pages, int64_t *slot_first,
+                            int64_t *slot_count, int64_t *value_first, int64_t *value_count, int32_t cap,
+                            pqgpu_error *err);
 /* Copy one chunk's outputs to host buffers sized from pqgpu_batch_chunk_result
  * (any pointer may be NULL to skip that array). */
 int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values, int32_t *offsets, uint8_t *payload,

@@ -256,6 +256,8 @@ struct pqgpu_batch {
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
   std::vector<uint32_t> page_nn_init;
+  std::vector<uint64_t> page_vbase_out;  // after sync: per-page value bases / non-null counts
+  std::vector<uint32_t> page_nn_out;
   std::vector<uint32_t> page_nn_spec;   // header non-null counts (speculative mode)
   std::vector<uint64_t> page_vbase_spec; // their per-chunk exclusive prefix
   bool spec = false;                     // this upload runs values concurrently with k_levels
@@ -1039,6 +1041,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMemcpy(rbase.data(), A + b->o_rbase, np * 8, hipMemcpyDeviceToHost), err);
     HIPCHECK(hipMemcpy(rec.data(), A + b->o_rec, np * 4, hipMemcpyDeviceToHost), err);
   }
+  b->page_vbase_out = vbase;
+  b->page_nn_out = nn;
   int first = PQ_OK;
   int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0;
   for (uint32_t c = 0; c < nc; c++) {
@@ -1337,6 +1341,31 @@ int pqgpu_batch_chunk_status(const pqgpu_batch *b, int32_t id, pqgpu_error *err)
   const pqgpu_error &e = hc.err.code ? hc.err : hc.dev_err;
   if (err) *err = e;
   return e.code;
+}
+
+int pqgpu_batch_chunk_pages(const pqgpu_batch *b, int32_t id, int32_t *num_pages, int64_t *slot_first,
+                            int64_t *slot_count, int64_t *value_first, int64_t *value_count, int32_t cap,
+                            pqgpu_error *err) {
+  clear_err(err);
+  if (!b || id < 0 || id >= (int32_t)b->chunks.size() || !num_pages) {
+    set_err(err, PQ_ERR_ARG, id, -1, "bad chunk id");
+    return PQ_ERR_ARG;
+  }
+  if (!b->decoded || b->page_nn_out.size() != b->pages.size()) {
+    set_err(err, PQ_ERR_ARG, id, -1, "batch not decoded and synced");
+    return PQ_ERR_ARG;
+  }
+  const HostChunk &hc = b->chunks[id];
+  *num_pages = (int32_t)hc.num_pages;
+  if ((int64_t)hc.num_pages > cap) return PQ_OK;  // size query
+  for (uint32_t k = 0; k < hc.num_pages; k++) {
+    const uint32_t p = hc.first_page + k;
+    if (slot_first) slot_first[k] = (int64_t)b->pages[p].slot_base;
+    if (slot_count) slot_count[k] = (int64_t)b->pages[p].num_slots;
+    if (value_first) value_first[k] = (int64_t)b->page_vbase_out[p];
+    if (value_count) value_count[k] = (int64_t)b->page_nn_out[p];
+  }
+  return PQ_OK;
 }
 
 int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_result *out, pqgpu_error *err) {

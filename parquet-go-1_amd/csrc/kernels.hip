@@ -463,14 +463,14 @@ struct LevelSink {
 //      at most 4 bytes whose run is well formed and complete inside the stream is a
 //      link p -> p + adv carrying the run's value count; anything else (errors, runs cut
 //      by EOF, longer varints) is a stop: a self-link with no values.
-//  P1b kLvRounds pointer-doubling rounds in LDS turn the links into 16-run jumps that
+//  P1b kLvRounds pointer-doubling rounds in LDS turn the links into >= 8-run jumps that
 //      carry the sum of the runs' value counts (saturating).
 //  P2  one lane follows the true chain from the chunk's entry by jumps, recording a
 //      checkpoint (position, value index) per jump; stops are decoded exactly
 //      (decode_hdr) and recorded as one-run checkpoints. The walk also finds where the
 //      reference's loop ends: the run that reaches num_values, an error run, or a
 //      bit-packed run cut by EOF.
-//  P3  one lane per checkpoint re-walks its <= 16 runs and expands them. Bit width 1
+//  P3  one lane per checkpoint re-walks its runs and expands them. Bit width 1
 //      with validity output only (flat OPTIONAL columns) ORs whole 32-bit words of
 //      payload into the LDS bitmap; other widths go through LevelSink::piece.
 // Results equal the reference's decodePackedArray loop exactly, including the error
@@ -478,7 +478,7 @@ struct LevelSink {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLvThreads = 64;             // one wave per page: no cross-wave barriers
 constexpr uint32_t kLvChunk = 1024;             // candidate header positions per chunk
-constexpr uint32_t kLvRounds = 4;               // doubling rounds: a jump spans 16 runs
+constexpr uint32_t kLvRounds = 3;               // doubling rounds: a jump spans >= 8 runs
 constexpr uint32_t kLvStageB = kLvChunk + 256;  // staged bytes: the chunk + headers / payload past its end
 constexpr uint32_t kLvMaxCk = kLvThreads;       // checkpoints per chunk (one fill lane each)
 constexpr uint32_t kLvMaxSlow = 32;             // exactly decoded runs per chunk
@@ -696,12 +696,15 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         continue;
       }
       const uint32_t bound = min(L.ck_pos[k + 1], cend);
-      while (p < bound && C < need) {
-        const FastHdr f = fast_hdr(L.stage, sb, p, n, bw, rs);
-        if (!f.adv) break;  // a stop: the next checkpoint
+      // software-pipelined: the next run's header is read before this run expands
+      FastHdr f = p < bound ? fast_hdr(L.stage, sb, p, n, bw, rs) : FastHdr{0, 0, 0, 0};
+      while (f.adv && C < need) {  // !f.adv: a stop (the next checkpoint) or the bound
+        const uint32_t pn = p + f.adv;
+        const FastHdr fn = pn < bound ? fast_hdr(L.stage, sb, pn, n, bw, rs) : FastHdr{0, 0, 0, 0};
         lv_fill_run<BW1>(L, sk, sb, send, C, min(f.nvals, need - C), f.bp, f.value);
         C += f.nvals;
-        p += f.adv;
+        p = pn;
+        f = fn;
       }
     }
     st.lap(4);

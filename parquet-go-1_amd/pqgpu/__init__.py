@@ -82,7 +82,7 @@ _EXPORTS = [
     "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
     "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
-    "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot",
+    "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages",
 ]
 
 
@@ -128,6 +128,8 @@ def lib():
                                      ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         "pqgpu_batch_kernel_slot": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                      ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        "pqgpu_batch_chunk_pages": ([P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), P, P, P, P, ctypes.c_int32, E],
+                                    ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -339,6 +341,18 @@ class Batch:
             if n.value:
                 out[name.value.decode()] = (ms.value, n.value)
         return out
+
+    def pages(self, cid):
+        """Per-page split of chunk `cid` (pageReader granularity): array of
+        (slot_first, slot_count, value_first, value_count) rows."""
+        err = Error()
+        n = ctypes.c_int32()
+        _check(lib().pqgpu_batch_chunk_pages(self._h, cid, ctypes.byref(n), None, None, None, None, 0,
+                                             ctypes.byref(err)), err)
+        out = np.zeros((4, n.value), np.int64)
+        ptr = [out[k].ctypes.data_as(ctypes.c_void_p) for k in range(4)]
+        _check(lib().pqgpu_batch_chunk_pages(self._h, cid, ctypes.byref(n), *ptr, n.value, ctypes.byref(err)), err)
+        return out.T.copy()
 
     def result(self, cid, copy=True):
         """ColumnData for chunk `cid` (raises DecodeError if that chunk failed)."""

@@ -92,3 +92,26 @@ def test_speculative_and_serial_schedules_agree(gpu_ctx, monkeypatch):
             gpu = _gpu_decode(gpu_ctx, data)
             for rg, col, r in orc:
                 pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"{name} serial={serial} rg{rg} col{col}")
+
+
+def test_chunk_page_split(gpu_ctx):
+    """pqgpu_batch_chunk_pages: page k of a chunk owns its header's num_values level slots and
+    the non-null values its definition levels count, in order (data_store.go:236-260)."""
+    for name in ("cfg2_v2_small", "edge_nulls_v1", "cfg4_small", "edge_tiny_pages"):
+        data = pqtest.load(name)
+        f = pqgpu.File(data)
+        b = pqgpu.Batch(gpu_ctx)
+        ids = [(rg, c, b.add_file_chunk(f, rg, c)[0]) for rg in range(f.num_row_groups) for c in range(f.num_columns)]
+        b.decode()
+        assert b.sync() is None
+        for rg, c, cid in ids:
+            r = b.result(cid)
+            pg = b.pages(cid)
+            assert pg[:, 1].sum() == r.num_slots and pg[:, 3].sum() == r.num_values
+            assert (pg[:, 0] == np.concatenate([[0], np.cumsum(pg[:-1, 1])])).all()
+            assert (pg[:, 2] == np.concatenate([[0], np.cumsum(pg[:-1, 3])])).all()
+            dl = np.asarray(r.dLevels)
+            for s0, sn, v0, vn in pg:  # values counted per page from the def levels (helpers.go:141-143)
+                want = int((dl[s0:s0 + sn] == r.max_def).sum()) if r.max_def > 0 else sn
+                assert vn == want, (name, rg, c)
+        b.close()
