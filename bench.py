@@ -257,6 +257,8 @@ def kernel_bytes(b, name, st):
         return int(st.delta_kernel_bytes)
     if name == "k_values[other]":
         return int(st.values_kernel_bytes - st.delta_kernel_bytes)
+    if name == "k_values":  # DELTA and the other value work items in one launch
+        return int(st.values_kernel_bytes)
     if name == "k_levels":
         return int(st.levels_kernel_bytes)
     return None

@@ -217,8 +217,8 @@ struct KernelTimer {
   struct Rec { int slot; hipEvent_t a, b; };
   std::vector<Rec> recs;          // pending launch records
   std::vector<hipEvent_t> pool;   // free events
-  double total_ms[9] = {0};
-  int64_t launches[9] = {0};
+  double total_ms[PQGPU_TIMER_SLOTS] = {0};
+  int64_t launches[PQGPU_TIMER_SLOTS] = {0};
   hipEvent_t get() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e = nullptr;
@@ -242,8 +242,9 @@ struct KernelTimer {
     pool.clear();
   }
 };
-static const char *kTimerNames[9] = {"k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_dict_ba",
-                                     "k_ba_offsets", "k_ba_gather", "k_records", "k_values[other]"};
+static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
+    "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_dict_ba", "k_ba_offsets",
+    "k_ba_gather", "k_records", "k_values[other]", "k_values", "k_delta_prep"};
 
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
@@ -252,6 +253,10 @@ struct pqgpu_batch {
   std::vector<uint8_t> stage;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
+  std::vector<uint32_t> delta_pages;      // tiled DELTA pages
+  std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
+  uint64_t dblk_total = 0;
+  uint32_t n_delta_tiles = 0;
   std::vector<uint32_t> level_pages, scan_pages, base_chunks, dict_ba_chunks, ba_chunks, rec_pages;
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
@@ -264,6 +269,7 @@ struct pqgpu_batch {
   // Speculative concurrent schedule (values beside k_levels) is opt-in: PQ_SPEC=1. Measured on
   // cfg2 it loses to the serial order (both kernels contend for LDS); see DESIGN.md.
   bool force_serial = spec_disabled();
+  bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<uint64_t> ba_tile_off;
   uint64_t ba_tiles_total = 0;
@@ -277,7 +283,7 @@ struct pqgpu_batch {
   size_t d_arena_cap = 0;
   uint64_t arena_size = 0;
   // arena offsets of batch-level arrays
-  uint64_t o_nnv = 0, o_spec_flag = 0;
+  uint64_t o_nnv = 0, o_spec_flag = 0, o_dblk = 0, o_dblk_base = 0, o_dblk_n = 0, o_dblk_sum = 0, l_delta = 0;
   uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
@@ -414,7 +420,9 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     pd->delta_mbc = (uint16_t)std::min<int32_t>(mbc, 65535);
     pd->delta_mbvc = (uint32_t)mbvc;
     pd->delta_first_mb = (uint32_t)(vstart + mb_start);
-    if (mbvc % 8 != 0 || bs > 1024 || mbc > 64) pd->flags |= PF_DELTA_SLOW;
+    // tiled pipeline shapes (kernels.hip k_delta_*): whole groups per miniblock, blocks tiling
+    // kDeltaTileVals, widths packed in one 64-bit word; anything else: exact scalar path
+    if (mbvc % 8 != 0 || bs < 128 || (int32_t)kDeltaTileVals % bs != 0 || mbc > 8) pd->flags |= PF_DELTA_SLOW;
     if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
     return PQ_OK;
   }
@@ -593,6 +601,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->items.clear();
   b->level_pages.clear();
   b->level_pages_bw1.clear();
+  b->delta_pages.clear();
+  b->dblk_base.assign(np, 0);
+  b->dblk_total = 0;
   b->scan_pages.clear();
   b->base_chunks.clear();
   b->dict_ba_chunks.clear();
@@ -674,7 +685,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           break;
         }
         case VK_DELTA32: case VK_DELTA64:
-          if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_DELTA, {0, 0, 0}});
+          if (!ns_p) break;
+          if (pd.flags & PF_DELTA_SLOW) {
+            b->items.push_back(WorkItem{p, 0, ns_p, WI_DELTA, {0, 0, 0}});
+          } else {
+            const uint32_t bs = (uint32_t)pd.delta_mbc * pd.delta_mbvc;
+            b->delta_pages.push_back(p);
+            b->dblk_base[p] = b->dblk_total;
+            b->dblk_total += ((uint64_t)ns_p + bs - 1) / bs + 1;
+            tiles(WI_DELTA_TILE, kDeltaTileVals);
+          }
           break;
         case VK_PLAIN_BA:
           if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_PLAIN_BA, {0, 0, 0}});
@@ -707,12 +727,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_begin = b->o_err;
   b->o_tile_first = take(b->tile_total * 4);
   b->f_end = a;
-  // DELTA pages first (long-running, latency-bound work items), then the bandwidth-bound tiles
-  std::stable_sort(b->items.begin(), b->items.end(), [](const WorkItem &x, const WorkItem &y) {
-    return (x.kind == WI_DELTA) > (y.kind == WI_DELTA);
-  });
+  // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
+  // pages (long-running), then the bandwidth-bound tiles
+  auto rank = [](uint8_t k) { return k == WI_DELTA_TILE ? 0 : k == WI_DELTA ? 1 : 2; };
+  std::stable_sort(b->items.begin(), b->items.end(),
+                   [&](const WorkItem &x, const WorkItem &y) { return rank(x.kind) < rank(y.kind); });
   b->n_delta_items = 0;
-  for (auto &it : b->items) b->n_delta_items += it.kind == WI_DELTA;
+  b->n_delta_tiles = 0;
+  for (auto &it : b->items) {
+    b->n_delta_items += it.kind == WI_DELTA || it.kind == WI_DELTA_TILE;
+    b->n_delta_tiles += it.kind == WI_DELTA_TILE;
+  }
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
   b->o_chunks = take((uint64_t)nc * sizeof(ChunkDesc));
@@ -728,6 +753,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_tile_off = take(b->ba_tile_off.size() * 8);
   b->o_ba_totals = take(b->ba_chunks.size() * 8);
   b->o_dbg = take(64 * 8);
+  b->o_dblk = take(b->dblk_total * sizeof(DeltaBlk));
+  b->o_dblk_sum = take(b->dblk_total * 8);
+  b->o_dblk_base = take((uint64_t)np * 8);
+  b->o_dblk_n = take((uint64_t)np * 4);
+  b->l_delta = take(b->delta_pages.size() * 4);
   b->l_level = take(b->level_pages.size() * 4);
   b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
@@ -824,6 +854,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_dict_ba, b->dict_ba_chunks.data(), b->dict_ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
+  HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
+  HIPCHECK(up(b->l_delta, b->delta_pages.data(), b->delta_pages.size() * 4), err);
   // the host copies above read from std::vector memory: wait before those vectors change
   HIPCHECK(hipStreamSynchronize(s), err);
   b->stats.num_chunks = nc;
@@ -842,6 +874,10 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.chunk_err = (unsigned long long *)(A + b->o_err);
   d.page_nn = (uint32_t *)(A + b->o_nn);
   d.page_nn_v = (uint32_t *)(A + b->o_nnv);
+  d.dblk = (DeltaBlk *)(A + b->o_dblk);
+  d.dblk_base = (const uint64_t *)(A + b->o_dblk_base);
+  d.dblk_n = (uint32_t *)(A + b->o_dblk_n);
+  d.dblk_sum = (unsigned long long *)(A + b->o_dblk_sum);
   d.spec_mismatch = (uint32_t *)(A + b->o_spec_flag);
   d.spec = b->spec ? 1u : 0u;
   d.page_rec = (uint32_t *)(A + b->o_rec);
@@ -878,6 +914,9 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_ba_chunks = (uint32_t)b->ba_chunks.size();
   l.rec_pages = (const uint32_t *)(A + b->l_rec);
   l.n_rec_pages = (uint32_t)b->rec_pages.size();
+  l.delta_pages = (const uint32_t *)(A + b->l_delta);
+  l.n_delta_pages = (uint32_t)b->delta_pages.size();
+  l.n_delta_tiles = b->n_delta_tiles;
   return l;
 }
 
@@ -927,8 +966,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(timed(b, 4, v, [&] { return launch_dict_ba(d, l, v); }), err);
     HIPCHECK(timed(b, 2, v, [&] { return launch_scan_runs(d, l, v); }), err);
-    HIPCHECK(timed(b, 1, v, [&] { return launch_values(d, l1, v); }), err);
-    HIPCHECK(timed(b, 8, v, [&] { return launch_values(d, l2, v); }), err);
+    HIPCHECK(timed(b, 10, v, [&] { return launch_delta_prep(d, l, v); }), err);
+    HIPCHECK(timed(b, 9, v, [&] { return launch_values(d, l, v); }), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
     HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
@@ -938,8 +977,15 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
-    HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l1, s); }), err);
-    HIPCHECK(timed(b, 8, s, [&] { return launch_values(d, l2, s); }), err);
+    HIPCHECK(timed(b, 10, s, [&] { return launch_delta_prep(d, l, s); }), err);
+    if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items as two launches (profiling)
+      HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l1, s); }), err);
+      HIPCHECK(timed(b, 8, s, [&] { return launch_values(d, l2, s); }), err);
+    } else {
+      // one grid: the DELTA pages (latency-bound: serial header walks and per-batch barriers)
+      // are dispatched first and the bandwidth-bound tiles fill the CUs around them
+      HIPCHECK(timed(b, 9, s, [&] { return launch_values(d, l, s); }), err);
+    }
   }
   if (!b->ba_chunks.empty()) {
     HIPCHECK(timed(b, 5, s, [&] {
@@ -1432,7 +1478,7 @@ int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable) {
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
   b->timer.resolve();
   b->timer.enabled = enable != 0;
-  for (int k = 0; k < 9; k++) { b->timer.total_ms[k] = 0; b->timer.launches[k] = 0; }
+  for (int k = 0; k < PQGPU_TIMER_SLOTS; k++) { b->timer.total_ms[k] = 0; b->timer.launches[k] = 0; }
   return PQ_OK;
 }
 
@@ -1441,7 +1487,7 @@ int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, c
   b->timer.resolve();
   const KernelTimer &t = b->timer;
   int best = -1;
-  for (int k = 0; k < 9; k++)
+  for (int k = 0; k < PQGPU_TIMER_SLOTS; k++)
     if (t.launches[k] && (best < 0 || t.total_ms[k] > t.total_ms[best])) best = k;
   if (best < 0) {
     if (avg_ms) *avg_ms = 0;

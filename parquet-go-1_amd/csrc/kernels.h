@@ -26,6 +26,10 @@ struct BatchDev {
   uint32_t *tile_first;           // dict tiles: first run index per tile
   const uint64_t *tile_base;      // [npages] first tile-table entry per page
   uint32_t *ba_tile_sum;          // BYTE_ARRAY: per 4096-value tile payload sum
+  DeltaBlk *dblk;                 // DELTA block tables of all tiled DELTA pages
+  const uint64_t *dblk_base;      // [npages] first DeltaBlk of the page
+  uint32_t *dblk_n;               // [npages] blocks the header walk produced
+  unsigned long long *dblk_sum;   // [total blocks] sum of each block's deltas (wrapping)
   unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
   uint32_t spec;                  // 1: value bases came from the page headers (see k_bases)
@@ -44,6 +48,8 @@ struct LaunchLists {
   const uint32_t *dict_ba_chunks; uint32_t n_dict_ba;    // chunks with a BYTE_ARRAY dictionary page
   const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with BYTE_ARRAY output
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
+  const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)
+  uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE
 };
 
 hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s);
@@ -54,6 +60,7 @@ hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s)
 hipError_t launch_ba_offsets(const BatchDev &b, const LaunchLists &l, uint64_t *payload_totals_dev, hipStream_t s);
 hipError_t launch_ba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // walk + sums + prefix
 
 // Names of the kernels, for the timing hook.
 extern const char *kValuesKernelName;

@@ -927,17 +927,13 @@ __global__ void __launch_bounds__(64) k_scan_runs(BatchDev b, const uint32_t *pa
 struct DictLDS {
   HybRun runs[1024];
 };
-constexpr uint32_t kDeltaWin = 16384;  // bytes of a DELTA stream staged in LDS at a time
-constexpr uint32_t kDeltaBatch = 16;  // blocks per batch (256 groups of 8 deltas at 128 values/block)
-struct DeltaLDS {
-  uint32_t win[kDeltaWin / 4 + 8];  // stream bytes [win0, win0 + kDeltaWin), 16-B aligned in memory
-  uint32_t blk_hdr[kDeltaBatch];      // stream position of each block header of the batch
-  uint64_t wsum[4];                 // per-wave totals of the batch scan
-  uint32_t nblocks, err_code, err_pos, stop_val, next_hdr, reload;
+struct DeltaTileLDS {
+  uint64_t scan[260];        // per-group exclusive scan + per-wave totals
+  uint32_t stage[(kDeltaTileVals * 8 + 8 * 24 + 64) / 4];  // the tile's payload bytes
 };
 union ValuesLDS {
   DictLDS dict;
-  DeltaLDS delta;
+  DeltaTileLDS dtile;        // WI_DELTA_TILE
   uint8_t slow_widths[256];
 };
 
@@ -1178,39 +1174,62 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
 
 
 
-// One DELTA block header (minDelta zigzag varint + mbc miniblock widths, the reads of
-// deltabp_decoder.go:125-150) at stream position pos, read from the LDS window that holds
-// stream bytes [win0, ...). Returns the error class (0 = ok) and, on success, minDelta,
-// the width and payload offset (relative to pos) of miniblock m, and the block's total
-// length. The common case (varint <= 8 bytes, <= 4 miniblocks) is branch-free register
-// work on one round of LDS reads; longer headers walk the window byte by byte, and a
-// varint longer than 10 bytes is resolved from global memory (Go overflow vs EOF).
-DEV uint32_t delta_blk(const uint32_t *win, int32_t win0, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64,
-                       uint32_t mbc, uint32_t g8, uint32_t m, int64_t *min_delta, uint32_t *wm, uint32_t *moff,
-                       uint32_t *blen) {
-  const uint32_t off = (uint32_t)((int32_t)pos - win0);
-  const uint32_t a = off >> 2, sh = off & 3;
-  const uint32_t w0 = win[a], w1 = win[a + 1], w2 = win[a + 2], w3 = win[a + 3];
+// ---------------------------------------------------------------------------
+// DELTA_BINARY_PACKED, tiled pipeline (deltabp_decoder.go:113-174 / :272-333).
+//
+// The only serial part of the format is the chain of block headers (a block's
+// position follows from the previous block's miniblock widths). It runs alone:
+//  1. k_delta_walk: one workgroup per page streams the page through a 16 KiB LDS
+//     window (the next window is loaded into registers while lane 0 walks the
+//     current one, at issue priority 3) and writes one DeltaBlk per block: minDelta,
+//     miniblock widths, payload position. Header errors are reported at the block's
+//     first value position (next() reads the header there, :119-135).
+//  2. k_delta_sums: one thread per group of 8 deltas, every tile of every page in
+//     parallel: per-block sums of (delta + minDelta) (wrapping, LDS 64-bit atomics).
+//  3. k_delta_prefix: per page, exclusive scan of the block sums from the first value.
+//  4. WI_DELTA_TILE items of k_values (beside the PLAIN tiles): unpack, tile scan,
+//     block base, 8 values per thread; group read errors (io.ReadFull EOF /
+//     ErrUnexpectedEOF at the group's first position, :137-141) are reported here.
+// Semantics: value i = first + sum_{k<i} (delta_k + minDelta(block(k))); returning
+// value i reads the group (and at block starts the header) holding delta i (the Q1
+// look-ahead); positions >= valuesCount fail with io.EOF. The first error in value
+// order wins through the chunk's atomicMin error key.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDwWin = 16384;                     // walk window bytes
+constexpr uint32_t kDwWinLoad = kDwWin + 64;           // + overlap for a header straddling the end
+constexpr uint32_t kDwVec = (kDwWinLoad / 16 + 255) / 256;  // uint4 per thread per window
+
+struct DeltaWalkLDS {
+  uint32_t win[kDwWinLoad / 4 + 4];
+  uint32_t pos, j, done, reload;
+};
+
+// Block header at stream position pos (readMiniBlockHeader :88-111 / :247-270) from the
+// LDS window holding stream bytes [wa, wa + kDwWinLoad): zigzag minDelta varint, then
+// mbc (<= 8) width bytes. Returns the error class (0 = ok).
+DEV uint32_t delta_hdr_parse(const uint32_t *win, uint32_t wa, const uint8_t *gs, uint32_t n, uint32_t pos, bool is64,
+                             uint32_t mbc, int64_t *md, uint64_t *widths, uint32_t *hlen) {
+  const uint32_t off = pos - wa, a = off >> 2, sh = off & 3;
+  const uint32_t w0 = win[a], w1 = win[a + 1], w2 = win[a + 2], w3 = win[a + 3], w4 = win[a + 4];
   const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
-                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32);
+                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh), u3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32), hi = (uint64_t)u2 | ((uint64_t)u3 << 32);
   const uint64_t term = ~lo & 0x8080808080808080ull;
-  uint64_t x;
-  uint32_t L;
+  uint64_t x = 0;
+  uint32_t L = 0;
   if (term) {
-    L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;  // varint bytes (1..8)
-    if (pos + L > n) return PQ_ERR_EOF;              // stream ends inside the varint
+    L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;
+    if (pos + L > n) return PQ_ERR_EOF;  // the stream ends inside the varint (ReadByte at EOF)
     uint64_t y = lo & (L == 8 ? ~0ull : ((1ull << (8 * L)) - 1ull)) & 0x7f7f7f7f7f7f7f7full;
     y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
     y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
     x = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
-  } else {
-    x = 0;
+  } else {  // 9+ byte varint: Go's ReadUvarint byte by byte
     unsigned shv = 0;
     for (uint32_t k = 0;; k++) {
       if (pos + k >= n) return PQ_ERR_EOF;
       if (k == 10) return resolve_long_varint(gs, pos - 2, n) == PQ_ERR_RANGE ? PQ_ERR_RANGE : PQ_ERR_EOF;
-      const uint32_t by = lds_ld32(win, off + k) & 0xffu;
+      const uint32_t by = k < 8 ? (uint32_t)(lo >> (8 * k)) & 0xffu : (uint32_t)(hi >> (8 * (k - 8))) & 0xffu;
       if (by < 0x80) {
         if (k == 9 && by > 1) return PQ_ERR_RANGE;
         if (shv < 64) x |= (uint64_t)by << shv;
@@ -1224,252 +1243,466 @@ DEV uint32_t delta_blk(const uint32_t *win, int32_t win0, const uint8_t *gs, uin
   int64_t v = (int64_t)(x >> 1);
   if (x & 1) v = ~v;
   if (!is64 && (v > 2147483647ll || v < -2147483648ll)) return PQ_ERR_RANGE;
-  *min_delta = v;
   const uint32_t p = pos + L;
   if (p >= n && mbc > 0) return PQ_ERR_EOF;
   if (p + mbc > n) return PQ_ERR_UNEXPECTED_EOF;
-  const uint32_t lim = is64 ? 64u : 32u;
-  uint32_t sum = 0, before = 0, wsel = 0;
-  if (mbc <= 4 && L <= 8) {
-    uint32_t ww = L < 8 ? (uint32_t)((lo >> (8 * L)) | ((uint64_t)u2 << (64 - 8 * L))) : u2;
-    if (mbc < 4) ww &= (1u << (8 * mbc)) - 1u;
-    const uint32_t b0 = ww & 0xffu, b1 = (ww >> 8) & 0xffu, b2 = (ww >> 16) & 0xffu, b3 = ww >> 24;
-    if (max(max(b0, b1), max(b2, b3)) > lim) return PQ_ERR_INVALID;
-    sum = b0 + b1 + b2 + b3;
-    before = (m > 0 ? b0 : 0) + (m > 1 ? b1 : 0) + (m > 2 ? b2 : 0);
-    wsel = m == 0 ? b0 : m == 1 ? b1 : m == 2 ? b2 : b3;
+  // widths: bytes [L, L + mbc) of the 16 register bytes (L <= 10, mbc <= 8 -> within 18: use a
+  // second funnel when L + mbc > 16)
+  uint64_t wv;
+  if (L + mbc <= 16) {
+    wv = L == 8 ? hi : (L < 8 ? ((lo >> (8 * L)) | (hi << (64 - 8 * L))) : (hi >> (8 * (L - 8))));
   } else {
-    const uint32_t q = off + L;
-    for (uint32_t i = 0; i < mbc; i++) {
-      const uint32_t wi = lds_ld32(win, q + i) & 0xffu;
-      if (wi > lim) return PQ_ERR_INVALID;
-      if (i < m) before += wi;
-      if (i == m) wsel = wi;
-      sum += wi;
-    }
+    wv = 0;
+    for (uint32_t i = 0; i < mbc; i++) wv |= (uint64_t)(lds_ld32(win, off + L + i) & 0xffu) << (8 * i);
   }
-  *wm = wsel;
-  *moff = L + mbc + g8 * before;
-  *blen = L + mbc + g8 * sum;
+  if (mbc < 8) wv &= (1ull << (8 * mbc)) - 1ull;
+  const uint32_t lim = is64 ? 64u : 32u;
+  uint64_t t = wv;
+  for (uint32_t i = 0; i < mbc; i++, t >>= 8)
+    if ((t & 0xffu) > lim) return PQ_ERR_INVALID;
+  *md = v;
+  *widths = wv;
+  *hlen = L + mbc;
   return 0;
 }
 
-// Length of the DELTA block whose header starts at stream position pos, on the serial
-// critical path of the header walk: varint length from a byte mask, width sum with one
-// SAD. No validation (the unpack threads re-parse every header with delta_blk and report
-// its errors); returns 0 when the header needs delta_blk (varint > 8 bytes, mbc > 4).
-DEV uint32_t delta_blk_len(const uint32_t *win, int32_t win0, uint32_t pos, uint32_t mbc, uint32_t g8) {
-  const uint32_t off = (uint32_t)((int32_t)pos - win0);
-  const uint32_t a = off >> 2, sh = off & 3;
-  const uint32_t w0 = win[a], w1 = win[a + 1], w2 = win[a + 2], w3 = win[a + 3];
-  const uint32_t u0 = __builtin_amdgcn_alignbyte(w1, w0, sh), u1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
-                 u2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32);
-  const uint64_t term = ~lo & 0x8080808080808080ull;
-  if (!term || mbc > 4) return 0;
-  const uint32_t L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;
-  uint32_t ww = L < 8 ? (uint32_t)((lo >> (8 * L)) | ((uint64_t)u2 << (64 - 8 * L))) : u2;
-  ww &= mbc == 4 ? 0xffffffffu : ((1u << (8 * mbc)) - 1u);
-  return L + mbc + g8 * __builtin_amdgcn_sad_u8(ww, 0u, 0u);
+DEV uint32_t bytesum64(uint64_t w) {
+  return __builtin_amdgcn_sad_u8((uint32_t)w, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(w >> 32), 0u, 0u);
+}
+DEV uint32_t bytesum64_swar(uint64_t w) {  // scalar-friendly byte sum
+  w = (w & 0x00ff00ff00ff00ffull) + ((w >> 8) & 0x00ff00ff00ff00ffull);
+  w = (w & 0x0000ffff0000ffffull) + ((w >> 16) & 0x0000ffff0000ffffull);
+  return (uint32_t)w + (uint32_t)(w >> 32);
+}
+DEV uint64_t sgpr64(uint64_t v) {
+  return ((uint64_t)sgpr((uint32_t)(v >> 32)) << 32) | sgpr((uint32_t)v);
 }
 
-DEV void do_delta(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
-                  DeltaLDS &L) {
-  if (nn == 0) return;
+// Common-case block header hop (wave-uniform inputs and result): minDelta varint of at
+// most 8 bytes, mbc <= 8 widths within the 16 bytes read, every width valid, header and
+// widths inside the stream. Returns 0 when the exact parser (delta_hdr_parse) is needed.
+DEV uint32_t delta_hdr_fast(const uint32_t *win, uint32_t wa, uint32_t n, uint32_t pos, uint32_t mbc, uint32_t wlim,
+                            int64_t *md, uint64_t *widths) {
+  const uint32_t off = pos - wa, a = off >> 2, sh = off & 3;
+  const uint32_t w0 = sgpr(win[a]), w1 = sgpr(win[a + 1]), w2 = sgpr(win[a + 2]), w3 = sgpr(win[a + 3]),
+                 w4 = sgpr(win[a + 4]);
+  const uint32_t u0 = sgpr(__builtin_amdgcn_alignbyte(w1, w0, sh)), u1 = sgpr(__builtin_amdgcn_alignbyte(w2, w1, sh)),
+                 u2 = sgpr(__builtin_amdgcn_alignbyte(w3, w2, sh)), u3 = sgpr(__builtin_amdgcn_alignbyte(w4, w3, sh));
+  const uint64_t lo = (uint64_t)u0 | ((uint64_t)u1 << 32), hi = (uint64_t)u2 | ((uint64_t)u3 << 32);
+  const uint64_t term = ~lo & 0x8080808080808080ull;
+  if (!term) return 0;
+  const uint32_t L = (uint32_t)(__builtin_ctzll(term) >> 3) + 1;
+  if (L + mbc > 16 || pos + L + mbc > n) return 0;
+  uint64_t y = lo & (L == 8 ? ~0ull : ((1ull << (8 * L)) - 1ull)) & 0x7f7f7f7f7f7f7f7full;
+  y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
+  y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
+  const uint64_t x = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
+  int64_t v = (int64_t)(x >> 1);
+  if (x & 1) v = ~v;
+  if (wlim == 32 && (v > 2147483647ll || v < -2147483648ll)) return 0;
+  uint64_t wv = L == 8 ? hi : ((lo >> (8 * L)) | (hi << (64 - 8 * L)));
+  if (mbc < 8) wv &= (1ull << (8 * mbc)) - 1ull;
+  // any width byte > wlim: (byte + (127 - wlim)) reaches bit 7, or the byte has it already
+  const uint64_t add = (0x7full - wlim) * 0x0101010101010101ull;
+  if (((wv + add) | wv) & 0x8080808080808080ull) return 0;
+  *md = v;
+  *widths = wv;
+  return L + mbc;
+}
+
+DEV void delta_group_at(const DeltaBlk &B, uint32_t inb, uint32_t mbvc, uint32_t g8, uint32_t *goff, uint32_t *w);
+DEV void delta_unpack8_lds(const uint32_t *stg, int32_t base, uint32_t goff, uint32_t w, bool is64, int64_t md,
+                           uint64_t (&d)[8]);
+
+// One workgroup per page: block index (walk), block sums and their scan, fused. Windows
+// start at a block header and hold whole blocks (a block's payload is at most
+// kDeltaTileVals * 8 bytes), so the blocks walked in a window are summed from LDS before
+// the next window is loaded at the first block that did not fit.
+constexpr uint32_t kDiWin = kDeltaTileVals * 8 + 1024;  // window bytes (>= the largest block + header)
+constexpr uint32_t kDiMaxBlk = 256;                     // blocks per window
+struct DeltaIndexLDS {
+  uint32_t win[kDiWin / 4 + 8];
+  int64_t md[kDiMaxBlk];
+  uint64_t wd[kDiMaxBlk];
+  uint32_t pos[kDiMaxBlk];
+  unsigned long long acc[kDiMaxBlk];
+  uint64_t wsum[4];
+  uint32_t nblk, next, done;
+};
+
+__global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *pages) {
+  __shared__ DeltaIndexLDS L;
+  const uint32_t pi = pages[blockIdx.x];
+  const PageDesc &pd = b.pages[pi];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t nn = b.page_nn_v[pi];
   const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
   const uint32_t n = pd.val_len;
   const bool is64 = pd.vkind == VK_DELTA64;
-  const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const uint64_t vb = b.page_vbase[wi.page];
-  uint32_t limit = nn;  // next() returns EOF at positions >= the header's valuesCount
-  uint32_t final_err = 0, final_pos = 0;
-  if ((uint32_t)pd.delta_count < nn) { limit = (uint32_t)pd.delta_count; final_err = PQ_ERR_EOF; final_pos = limit; }
+  const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
+  DeltaBlk *tab = b.dblk + b.dblk_base[pi];
+  uint32_t limit = nn;
+  if ((uint32_t)pd.delta_count < nn) {
+    limit = (uint32_t)pd.delta_count;
+    if (tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, limit, PQ_ERR_EOF);  // next() past valuesCount
+  }
+  const uint32_t need = (uint32_t)(((uint64_t)limit + bs - 1) / bs);
+  uint32_t pos = pd.delta_first_mb - pd.val_off, j = 0;
   uint64_t carry = (uint64_t)pd.delta_first;
-  uint32_t hdr = pd.delta_first_mb - pd.val_off;  // next miniblock header (stream-relative)
-  const uint32_t gpb = bs / 8;                      // groups per block
-  const uint32_t bpb = max(1u, min(kDeltaBatch, 256u / gpb)); // blocks per batch
-  const uint32_t max_blk = 10 + mbc + bs * 8;       // upper bound of one block's bytes (widths <= 64)
-  int32_t win0 = 0;                                 // stream offset of LDS byte 0 (16-B aligned address)
-  bool staged = false;
-  uint32_t blk = 0;                                 // index of the next block
-  const uint32_t g8 = mbvc / 8;                     // bytes per bit of miniblock width
-  if (tid == 0) { L.err_code = 0; L.stop_val = limit; }
-  PQ_STAMPS(st, b.dbg);
-  st.begin();
-  while ((uint64_t)blk * bs < limit) {
-    // ---- (re)stage the window so that it starts at the next header
-    if (!staged || ((int64_t)hdr + max_blk > (int64_t)win0 + kDeltaWin && (int64_t)win0 + kDeltaWin < n)) {
-      __syncthreads();
-      // window starts at the 16-B aligned address at or below the next header (never below the
-      // 16-B aligned page start); loads stop 16 B past the stream end (page padding)
-      win0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
-      staged = true;
-      const uint4 *src = (const uint4 *)(s + win0);
+  const uint32_t wlim = is64 ? 64u : 32u;
+  const uint64_t wadd = (0x7full - wlim) * 0x0101010101010101ull;
+  const uint64_t wmask = mbc >= 8 ? ~0ull : ((1ull << (8 * mbc)) - 1ull);
+  bool stop = need == 0;
+  while (!stop) {
+    // ---- window at the next block header (16-B aligned address; wa may be a few bytes below 0)
+    const int32_t wa = (int32_t)pos - (int32_t)(((uintptr_t)(s + pos)) & 15u);
+    {
+      const uint4 *src = (const uint4 *)(s + wa);
+      const int64_t lim = (int64_t)n + 16 - wa;  // the page padding keeps 16 B past n readable
       uint4 *dst = (uint4 *)L.win;
-      const int64_t lim = (int64_t)n + 16 - win0;  // bytes worth loading
-      uint4 v[5];
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const uint32_t k = tid + j * 256;
-        v[j] = (k < kDeltaWin / 16 + 2 && (int64_t)k * 16 < lim) ? src[k] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const uint32_t k = tid + j * 256;
-        const int64_t o = (int64_t)win0 + 16 * (int64_t)k;  // stream offset of this uint4
-        if (o + 16 > (int64_t)n) {                             // zero the bytes past the stream end
-          uint32_t *e = &v[j].x;
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int64_t r = (int64_t)n - (o + 4 * q);
-            e[q] = r >= 4 ? e[q] : (r <= 0 ? 0u : e[q] & ((1u << (8 * r)) - 1u));
+      for (uint32_t q = tid; q < kDiWin / 16 + 1; q += 256) dst[q] = (int64_t)q * 16 < lim ? src[q] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const int64_t wend = (int64_t)wa + kDiWin;  // bytes [wa, wend) are staged
+    // ---- wave 0 walks the blocks that fit whole in the window
+    if (wv == 0) {
+      __builtin_amdgcn_s_setprio(3);
+      uint32_t k = 0, done = 0;
+      uint32_t p = pos, jj = j;
+      while (jj < need && k < kDiMaxBlk) {
+        int64_t md = 0;
+        uint64_t wd = 0;
+        uint32_t hl = 0;
+        if (p >= n) {  // next() reads block jj's header at EOF
+          if (lane == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, jj * bs, PQ_ERR_EOF);
+          done = 1;
+          break;
+        }
+        if ((int64_t)p + 32 > wend) break;  // header not staged: next window
+        {  // common case: minDelta varint of <= 4 bytes, widths within the 8 bytes read
+          const uint32_t off = (uint32_t)((int32_t)p - wa), a = off >> 2, sh = off & 3;
+          const uint64_t x01 = ((uint64_t)L.win[a + 1] << 32) | L.win[a];
+          const uint32_t x2 = L.win[a + 2];
+          const uint64_t u = (x01 >> (8 * sh)) | (sh ? ((uint64_t)x2 << (64 - 8 * sh)) : 0ull);
+          const uint32_t u0 = (uint32_t)u, t = ~u0 & 0x80808080u;
+          const uint32_t Lv = t ? (uint32_t)(__builtin_ctz(t) >> 3) + 1 : 8u;
+          if (Lv + mbc <= 8 && p + Lv + mbc <= n) {
+            const uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
+            const uint32_t x = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+            const uint64_t wvv = (u >> (8 * Lv)) & wmask;
+            if (!(((wvv + wadd) | wvv) & 0x8080808080808080ull)) {
+              md = (int64_t)(x >> 1) ^ -(int64_t)(x & 1);
+              wd = wvv;
+              hl = Lv + mbc;
+            }
           }
         }
-        if (k < kDeltaWin / 16 + 2) dst[k] = v[j];
-      }
-      __syncthreads();
-      st.lap(0);
-    }
-    // ---- header walk (thread 0): block positions only; every unpack thread re-parses its
-    // own block's header in parallel (and reports its errors) below
-    if (tid == 0) {
-      uint32_t nb = 0;
-      const int64_t wend = (int64_t)win0 + kDeltaWin;
-      for (; nb < bpb && (uint64_t)(blk + nb) * bs < limit; nb++) {
-        if ((int64_t)hdr + 16 + mbc > wend && wend < n) break;  // header not entirely staged: next window
-        uint32_t bl = delta_blk_len(L.win, win0, hdr, mbc, g8);
-        if (!bl) {
-          int64_t md;
-          uint32_t wm, mo;
-          if (delta_blk(L.win, win0, s, n, hdr, is64, mbc, g8, 0, &md, &wm, &mo, &bl)) {
-            L.blk_hdr[nb++] = hdr;  // the unpack threads report the error
+        if (!hl) {  // exact parse: longer varint, many miniblocks, or an error
+          const uint32_t e = delta_hdr_parse(L.win, (uint32_t)wa, s, n, p, is64, mbc, &md, &wd, &hl);
+          if (e) {  // the header of block jj is read by next() at position jj * bs
+            if (lane == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, jj * bs, e);
+            done = 1;
             break;
           }
         }
-        if (hdr + bl > n) {  // the stream ends inside this block (or its header is bad): reported below
-          L.blk_hdr[nb++] = hdr;
-          hdr += bl;
-          break;
-        }
-        if ((int64_t)hdr + bl > wend && wend < n && nb > 0) break;  // block body not staged (always take >= 1)
-        L.blk_hdr[nb] = hdr;
-        hdr += bl;
+        const uint32_t blen = hl + g8 * bytesum64(wd);
+        if ((int64_t)p + blen > wend && (int64_t)p + blen <= (int64_t)n + 0 && k > 0) break;  // next window
+        if (lane == 0) { L.md[k] = md; L.wd[k] = wd; L.pos[k] = p + hl; }
+        k++;
+        jj++;
+        p += blen;
       }
-      L.nblocks = nb;
-      L.next_hdr = hdr;
+      if (lane == 0) { L.nblk = k; L.next = p; L.done = done; }
+      __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
-    st.lap(1);
-    hdr = L.next_hdr;
-    const uint32_t nb = L.nblocks;
-    uint32_t stop = L.stop_val;
-    // ---- unpack: thread t -> group t of the batch (8 deltas)
-    const uint32_t g = tid;
-    const uint32_t bi = g / gpb;
-    const uint32_t d0 = (blk + bi) * bs + (g % gpb) * 8;  // first delta index of the group
-    uint64_t d[8];
-    uint64_t sum = 0;
-    uint32_t gerr = 0, gerr_pos = 0;
-    bool valid = bi < nb && d0 < stop;
-    uint32_t goff = 0, wbits = 0;
-    int64_t mdl = 0;
-    if (valid) {
-      const uint32_t inb = (g % gpb) * 8;
-      const uint32_t m = inb / mbvc, o = inb % mbvc;
-      const uint32_t bpos = L.blk_hdr[bi];
-      uint32_t mo, bl;
-      const uint32_t he = delta_blk(L.win, win0, s, n, bpos, is64, mbc, g8, m, &mdl, &wbits, &mo, &bl);
-      if (he) {  // header error: surfaces at the block's first position (read by next() there)
-        gerr = he;
-        gerr_pos = (blk + bi) * bs;
-      } else {
-        goff = bpos + mo + (o / 8) * wbits;  // group byte offset (stream-relative)
-        if (wbits > 0 && goff >= n) { gerr = PQ_ERR_EOF; gerr_pos = d0; }
-        else if ((uint64_t)goff + wbits > n) { gerr = PQ_ERR_UNEXPECTED_EOF; gerr_pos = d0; }
-      }
-    }
-    if (valid && !gerr) {
-      const uint64_t md = (uint64_t)mdl;
-      const uint32_t bo = (uint32_t)((int32_t)goff - win0) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        uint64_t u = lds_bits64(L.win, bo + j * wbits, wbits);
-        if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
-        d[j] = u + md;
-        sum += d[j];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; j++) d[j] = 0;
-    }
-    if (gerr) atomicMin(&L.stop_val, gerr_pos);
+    const uint32_t nb = L.nblk;
+    // ---- block sums of the window's blocks (groups past the stream end contribute 0;
+    // their read error is reported by the tile pass)
+    for (uint32_t q = tid; q < nb; q += 256) L.acc[q] = 0;
     __syncthreads();
-    st.lap(2);
-    const uint32_t stop2 = L.stop_val;
-    if (gerr && gerr_pos == stop2 && stop2 < stop) { L.err_code = gerr; L.err_pos = gerr_pos; }
-    stop = stop2;
-    const uint64_t contrib = (valid && d0 < stop) ? sum : 0;
-    // ---- block-wide exclusive scan of group sums: wave shuffle scan + 4-way combine
-    const uint64_t incl = wave_incl_scan64(contrib);
-    if (lane == 63) L.wsum[wv] = incl;
-    __syncthreads();
-    uint64_t before = 0, total = 0;
-    for (uint32_t k = 0; k < (blockDim.x >> 6); k++) {
-      uint64_t t = L.wsum[k];
-      if (k < wv) before += t;
-      total += t;
+    for (uint32_t gi = tid; gi < nb * gpb; gi += 256) {
+      const uint32_t k = gi / gpb, inb = (gi % gpb) * 8;
+      if ((uint64_t)(j + k) * bs + inb >= limit) continue;
+      DeltaBlk B;
+      B.widths = L.wd[k];
+      B.pos = L.pos[k];
+      uint32_t goff, w;
+      delta_group_at(B, inb, mbvc, g8, &goff, &w);
+      if ((uint64_t)goff + w > n || (int64_t)goff + 24 > wend) continue;
+      uint64_t d[8];
+      delta_unpack8_lds(L.win, wa, goff, w, is64, L.md[k], d);
+      uint64_t sum = 0;
+#pragma unroll
+      for (int e = 0; e < 8; e++) sum += d[e];
+      atomicAdd(&L.acc[k], (unsigned long long)sum);
     }
-    uint64_t run = carry + before + incl - contrib;
-    st.lap(3);
-    if (valid && d0 < stop) {
-      uint64_t out[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        out[j] = run;
-        run += d[j];
-      }
-      if (d0 + 8 <= stop) {
-        if (is64) {
-          uint64_t *o = (uint64_t *)cd.values + vb + d0;  // 8-B aligned; 16-B aligned when vb is even
-          if (((uintptr_t)o & 15) == 0) {
-            uint4 *o4 = (uint4 *)o;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              o4[j] = make_uint4((uint32_t)out[2 * j], (uint32_t)(out[2 * j] >> 32), (uint32_t)out[2 * j + 1],
-                                 (uint32_t)(out[2 * j + 1] >> 32));
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) o[j] = out[j];
-          }
-        } else {
-          uint32_t *o = (uint32_t *)cd.values + vb + d0;
-#pragma unroll
-          for (int j = 0; j < 8; j++) o[j] = (uint32_t)out[j];
-        }
-      } else {
-        for (int j = 0; j < 8; j++) {
-          if (d0 + j < stop) {
-            if (is64) ((uint64_t *)cd.values)[vb + d0 + j] = out[j];
-            else ((uint32_t *)cd.values)[vb + d0 + j] = (uint32_t)out[j];
-          }
-        }
-      }
-    }
-    carry += total;
-    blk += nb;
-    st.lap(4);
-    st.count(5);
     __syncthreads();
-    st.lap(6);
-    if (L.err_code || stop < limit || nb == 0) {
-      st.flush(8);
-      if (tid == 0 && L.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, L.err_pos, L.err_code);
-      return;
+    // ---- scan of the block sums -> block base values; complete block records
+    for (uint32_t k0 = 0; k0 < nb; k0 += 256) {
+      const uint32_t k = k0 + tid;
+      const uint64_t v = k < nb ? (uint64_t)L.acc[k] : 0;
+      const uint64_t incl = wave_incl_scan64(v);
+      if (lane == 63) L.wsum[wv] = incl;
+      __syncthreads();
+      uint64_t before = carry, total = 0;
+      for (uint32_t q = 0; q < 4; q++) {
+        if (q < wv) before += L.wsum[q];
+        total += L.wsum[q];
+      }
+      if (k < nb) {
+        DeltaBlk blk;
+        blk.min_delta = L.md[k];
+        blk.widths = L.wd[k];
+        blk.base = (int64_t)(before + incl - v);
+        blk.pos = L.pos[k];
+        blk.sum_lo = 0;
+        tab[j + k] = blk;
+      }
+      carry += total;
+      __syncthreads();
+    }
+    j += nb;
+    pos = L.next;
+    stop = L.done || j >= need || (nb == 0 && pos >= n);
+    __syncthreads();
+  }
+  if (tid == 0) b.dblk_n[pi] = j;
+}
+
+// Group g (8 deltas from position d0) of a page: payload offset and width.
+DEV void delta_group_at(const DeltaBlk &B, uint32_t inb, uint32_t mbvc, uint32_t g8, uint32_t *goff, uint32_t *w) {
+  const uint32_t m = inb / mbvc, o = inb % mbvc;
+  const uint64_t below = m >= 8 ? B.widths : (B.widths & ((1ull << (8 * m)) - 1ull));
+  *w = (uint32_t)(B.widths >> (8 * m)) & 0xffu;
+  *goff = B.pos + g8 * bytesum64(below) + (o / 8) * *w;
+}
+
+// The 8 deltas (unpacked + minDelta, wrapping) of a group of width w at byte goff.
+// A group is w bytes; widths <= 16 read 5 aligned dwords once, wider ones per value.
+DEV void delta_unpack8(const uint8_t *s, uint32_t goff, uint32_t w, bool is64, int64_t md, uint64_t (&d)[8]) {
+  if (w <= 16) {
+    const uint32_t *q = (const uint32_t *)((uintptr_t)(s + goff) & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)(s + goff) & 3);
+    const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
+    const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+    const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(x3, x2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x4, x3, sh) << 32);
+    const uint64_t mask = w >= 64 ? ~0ull : ((1ull << w) - 1ull);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t bo = k * w;
+      uint64_t u = bo >= 64 ? (hi >> (bo - 64)) : ((lo >> bo) | (bo ? (hi << (64 - bo)) : 0ull));
+      u &= mask;
+      if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
+      d[k] = u + (uint64_t)md;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint64_t u = bits64(s, (uint64_t)goff * 8 + (uint64_t)k * w, w);
+      if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
+      d[k] = u + (uint64_t)md;
     }
   }
-  st.flush(8);
-  if (final_err && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, final_pos, final_err);
+}
+
+// Common geometry of a DELTA tile work item for thread tid.
+struct DeltaGroup {
+  bool valid;        // group holds a needed delta of a walked block
+  uint32_t d0, j, goff, w, err;
+};
+DEV DeltaGroup delta_tile_group(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, uint32_t limit,
+                                uint32_t tid, DeltaBlk *B) {
+  DeltaGroup g{false, wi.v0 + 8 * tid, 0, 0, 0, 0};
+  const uint32_t mbvc = pd.delta_mbvc, bs = pd.delta_mbc * mbvc;
+  if (g.d0 >= limit) return g;
+  g.j = g.d0 / bs;
+  if (g.j >= b.dblk_n[wi.page]) return g;
+  *B = b.dblk[b.dblk_base[wi.page] + g.j];
+  g.valid = true;
+  delta_group_at(*B, g.d0 % bs, mbvc, mbvc / 8, &g.goff, &g.w);
+  const uint32_t n = pd.val_len;
+  if (g.w > 0 && g.goff >= n) g.err = PQ_ERR_EOF;  // io.ReadFull of the group (:137-141)
+  else if ((uint64_t)g.goff + g.w > n) g.err = PQ_ERR_UNEXPECTED_EOF;
+  return g;
+}
+
+// A DELTA tile's payload bytes (first to last walked block of the tile) staged in LDS with
+// coalesced 16-B loads; returns the stream offset of LDS byte 0 (16-B aligned address, may
+// be a few bytes below 0), or INT32_MIN when the tile has no walked block.
+constexpr uint32_t kDtStageB = kDeltaTileVals * 8 + 8 * 24 + 64;  // 64-bit widths + headers + slack
+DEV int32_t delta_stage_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, uint32_t *stg) {
+  const uint32_t bs = pd.delta_mbc * pd.delta_mbvc, g8 = pd.delta_mbvc / 8, n = pd.val_len;
+  const uint32_t j0 = wi.v0 / bs, nbt = kDeltaTileVals / bs, nb = b.dblk_n[wi.page];
+  if (j0 >= nb) return INT32_MIN;
+  const DeltaBlk *tab = b.dblk + b.dblk_base[wi.page];
+  const uint32_t j1 = min(j0 + nbt, nb) - 1;
+  const DeltaBlk last = tab[j1];
+  const uint32_t lo = tab[j0].pos;
+  const uint32_t hi = min((uint64_t)last.pos + (uint64_t)g8 * bytesum64(last.widths), (uint64_t)n);
+  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const int32_t base = (int32_t)lo - (int32_t)(((uintptr_t)(s + lo)) & 15u);
+  const int32_t end = (int32_t)max(hi, lo) + 16;  // the page padding keeps 16 B past n readable
+  const uint32_t nv = (uint32_t)(end - base + 15) / 16;
+  const uint4 *src = (const uint4 *)(s + base);
+  uint4 *dst = (uint4 *)stg;
+  for (uint32_t k = threadIdx.x; k < nv && k < kDtStageB / 16; k += blockDim.x) dst[k] = src[k];
+  return base;
+}
+
+// delta_unpack8 from the staged tile (group at stream offset goff, LDS byte 0 = offset base).
+DEV void delta_unpack8_lds(const uint32_t *stg, int32_t base, uint32_t goff, uint32_t w, bool is64, int64_t md,
+                           uint64_t (&d)[8]) {
+  const uint32_t o = (uint32_t)((int32_t)goff - base);
+  if (w <= 16) {
+    const uint32_t a = o >> 2, sh = o & 3;
+    const uint32_t x0 = stg[a], x1 = stg[a + 1], x2 = stg[a + 2], x3 = stg[a + 3], x4 = stg[a + 4];
+    const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+    const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(x3, x2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x4, x3, sh) << 32);
+    const uint64_t mask = (1ull << w) - 1ull;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t bo = k * w;
+      uint64_t u = bo >= 64 ? (hi >> (bo - 64)) : ((lo >> bo) | (bo ? (hi << (64 - bo)) : 0ull));
+      u &= mask;
+      if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
+      d[k] = u + (uint64_t)md;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint64_t u = lds_bits64(stg, o * 8 + (uint32_t)k * w, w);
+      if (!is64) u = (uint64_t)(int64_t)(int32_t)(uint32_t)u;
+      d[k] = u + (uint64_t)md;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_delta_sums(BatchDev b, const WorkItem *items) {
+  __shared__ uint32_t stg[kDtStageB / 4];
+  __shared__ unsigned long long acc[kDeltaTileVals / 128];
+  const WorkItem wi = items[blockIdx.x];
+  const PageDesc &pd = b.pages[wi.page];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t bs = pd.delta_mbc * pd.delta_mbvc;
+  const uint32_t nn = b.page_nn_v[wi.page];
+  const uint32_t limit = min(nn, (uint32_t)max(pd.delta_count, 0));
+  const uint32_t nbt = kDeltaTileVals / bs;  // blocks per tile (bs divides the tile)
+  if (tid < nbt) acc[tid] = 0;
+  if (wi.v0 >= limit) return;  // workgroup-uniform
+  const int32_t base = delta_stage_tile(b, wi, pd, stg);
+  __syncthreads();
+  DeltaBlk B;
+  const DeltaGroup g = delta_tile_group(b, wi, pd, limit, tid, &B);
+  if (g.valid && !g.err) {
+    uint64_t d[8];
+    delta_unpack8_lds(stg, base, g.goff, g.w, pd.vkind == VK_DELTA64, B.min_delta, d);
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) sum += d[k];
+    atomicAdd(&acc[(g.d0 - wi.v0) / bs], (unsigned long long)sum);
+  }
+  __syncthreads();
+  if (tid < nbt) {
+    const uint32_t j = wi.v0 / bs + tid;
+    if (j < b.dblk_n[wi.page]) b.dblk_sum[b.dblk_base[wi.page] + j] = acc[tid];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_delta_prefix(BatchDev b, const uint32_t *pages) {
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t carry;
+  const uint32_t pi = pages[blockIdx.x];
+  const PageDesc &pd = b.pages[pi];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t nb = b.dblk_n[pi];
+  DeltaBlk *tab = b.dblk + b.dblk_base[pi];
+  const unsigned long long *sums = b.dblk_sum + b.dblk_base[pi];
+  if (tid == 0) carry = (uint64_t)pd.delta_first;
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < nb; j0 += 256) {
+    const uint32_t j = j0 + tid;
+    const uint64_t v = j < nb ? sums[j] : 0;
+    const uint64_t incl = wave_incl_scan64(v);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint64_t before = carry, total = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (k < wv) before += wsum[k];
+      total += wsum[k];
+    }
+    if (j < nb) tab[j].base = (int64_t)(before + incl - v);
+    __syncthreads();
+    if (tid == 0) carry += total;
+    __syncthreads();
+  }
+}
+
+// WI_DELTA_TILE: 8 values per thread.
+DEV void do_delta_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
+                       uint64_t *scan, uint32_t *stg) {
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const bool is64 = pd.vkind == VK_DELTA64;
+  const uint32_t bs = pd.delta_mbc * pd.delta_mbvc;
+  const uint32_t limit = min(nn, (uint32_t)max(pd.delta_count, 0));
+  if (wi.v0 >= limit) return;  // workgroup-uniform
+  const int32_t base = delta_stage_tile(b, wi, pd, stg);
+  __syncthreads();
+  DeltaBlk B;
+  const DeltaGroup g = delta_tile_group(b, wi, pd, limit, tid, &B);
+  uint64_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t sum = 0;
+  if (g.valid && g.err) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, g.d0, g.err);
+  if (g.valid && !g.err) {
+    delta_unpack8_lds(stg, base, g.goff, g.w, is64, B.min_delta, d);
+#pragma unroll
+    for (int k = 0; k < 8; k++) sum += d[k];
+  }
+  // exclusive scan of group sums over the tile; a block's values restart from its base
+  const uint64_t incl = wave_incl_scan64(sum);
+  if (lane == 63) scan[256 + wv] = incl;
+  __syncthreads();
+  uint64_t before = 0;
+  for (uint32_t k = 0; k < wv; k++) before += scan[256 + k];
+  const uint64_t excl = before + incl - sum;
+  scan[tid] = excl;
+  __syncthreads();
+  // values of this group, staged in LDS (the payload stage is free after the scan barrier)
+  // and stored with coalesced 16-B writes: a thread's 8 values are 64 contiguous bytes, so
+  // storing them directly would make every store instruction write partial cache lines
+  uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g.valid && !g.err) {
+    const uint32_t gb = (g.j * bs - wi.v0) / 8;  // the block's first group in this tile
+    uint64_t run = (uint64_t)B.base + (excl - scan[gb]);
+#pragma unroll
+    for (int k = 0; k < 8; k++) { out[k] = run; run += d[k]; }
+  }
+  if (is64) {
+    uint4 *o = (uint4 *)stg + tid * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      o[k] = make_uint4((uint32_t)out[2 * k], (uint32_t)(out[2 * k] >> 32), (uint32_t)out[2 * k + 1],
+                        (uint32_t)(out[2 * k + 1] >> 32));
+  } else {
+    uint4 *o = (uint4 *)stg + tid * 2;
+    o[0] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
+    o[1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
+  }
+  __syncthreads();
+  const uint32_t w = is64 ? 8u : 4u;
+  const uint32_t cnt = min(kDeltaTileVals, limit - wi.v0);  // values of this tile before the limit
+  const uint64_t vb = b.page_vbase[wi.page];
+  uint8_t *dst = (uint8_t *)cd.values + (vb + wi.v0) * w;
+  const uint32_t bytes = cnt * w;
+  if (((uintptr_t)dst & 15) == 0) {
+    for (uint32_t q = tid; q < bytes / 16; q += blockDim.x) ((uint4 *)dst)[q] = ((const uint4 *)stg)[q];
+    for (uint32_t q = (bytes & ~15u) / 4 + tid; q < bytes / 4; q += blockDim.x) ((uint32_t *)dst)[q] = stg[q];
+  } else if (((uintptr_t)dst & 7) == 0) {
+    for (uint32_t q = tid; q < bytes / 8; q += blockDim.x) ((uint2 *)dst)[q] = ((const uint2 *)stg)[q];
+    for (uint32_t q = (bytes & ~7u) / 4 + tid; q < bytes / 4; q += blockDim.x) ((uint32_t *)dst)[q] = stg[q];
+  } else {
+    for (uint32_t q = tid; q < bytes / 4; q += blockDim.x) ((uint32_t *)dst)[q] = stg[q];
+  }
 }
 
 // Exact scalar restatement of deltaBitPackDecoder.next for pages whose miniblock
@@ -1492,7 +1725,7 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     return;
   }
   rpos += hl;
-  uint32_t cur_mb = 0, cur_w = 0;
+  uint32_t cur_mb = 0, cur_w = 0, mb_pos = 0;  // mb_pos: miniBlockPosition (bytes read in the miniblock)
   int64_t mbv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t prev = (uint64_t)pd.delta_first;
   const int32_t vcount = pd.delta_count;
@@ -1509,6 +1742,7 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
           cur_mb = 0;
         }
         cur_w = widths[cur_mb];
+        mb_pos = 0;
         cur_mb++;
       }
       if (cur_w > 0 && rpos >= n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_EOF); return; }
@@ -1517,7 +1751,14 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
         mbv[j] = is64 ? (int64_t)bits64(s + rpos, (uint64_t)j * cur_w, cur_w)
                       : (int64_t)(int32_t)bits32(s + rpos, (uint64_t)j * cur_w, cur_w);
       rpos += cur_w;
-      // the padding skip after the last group only moves the reader; nothing follows an INT page
+      mb_pos += cur_w;
+      // the padding skip after the last group (:149-164): it only moves the reader (nothing
+      // follows an INT page), but a negative remainder — miniblocks of fewer than 8 values —
+      // is "invalid stream"
+      if ((int64_t)pos + 8 >= (int64_t)vcount && (int64_t)(mbvc / 8) * cur_w < (int64_t)mb_pos) {
+        report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_INVALID);
+        return;
+      }
     }
     uint64_t ret = prev;
     prev = prev + (uint64_t)mbv[pos % 8] + (uint64_t)md;
@@ -1563,10 +1804,8 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *item
     case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
-    case WI_DELTA:
-      if (pd.flags & PF_DELTA_SLOW) do_delta_slow(b, wi, pd, cd, nn, lds.slow_widths);
-      else do_delta(b, wi, pd, cd, nn, lds.delta);
-      break;
+    case WI_DELTA: do_delta_slow(b, wi, pd, cd, nn, lds.slow_widths); break;
+    case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
   }
 }
@@ -1790,6 +2029,11 @@ hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_items) return hipSuccess;
   hipLaunchKernelGGL(k_values, dim3(l.n_items), dim3(256), 0, s, b, l.items);
+  return hipGetLastError();
+}
+hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_delta_pages) return hipSuccess;
+  hipLaunchKernelGGL(k_delta_walk, dim3(l.n_delta_pages), dim3(256), 0, s, b, l.delta_pages);
   return hipGetLastError();
 }
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

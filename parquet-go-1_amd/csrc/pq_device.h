@@ -41,7 +41,8 @@ enum : uint16_t {
   PF_DEF = 2,        // def stream present
   PF_V2 = 4,
   PF_BASE_KNOWN = 8, // value_base computed on host (required column or V2 num_nulls)
-  PF_DELTA_SLOW = 16,// DELTA page whose miniblock size is not a multiple of 8: exact scalar path
+  PF_DELTA_SLOW = 16,// DELTA page outside the tiled pipeline's shapes (miniblock not a multiple of 8
+                     // values, block size not dividing kDeltaTileVals, > 8 miniblocks): exact scalar path
 };
 
 // Error staging key (64 bit, smaller = reported first):
@@ -112,7 +113,19 @@ struct ChunkDesc {       // 192 B
 enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8 };
 
 // Work items of the values kernel.
-enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5 };
+enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,
+                 WI_DELTA_TILE = 6 };
+
+// DELTA_BINARY_PACKED block table entry (one per block of a page), written by the header
+// walk (k_delta_walk), completed by the per-page scan of block sums (k_delta_prefix).
+constexpr uint32_t kDeltaTileVals = 2048;  // values per DELTA tile (256 groups of 8)
+struct DeltaBlk {        // 32 B
+  int64_t min_delta;     // the block's minDelta (zigzag varint, deltabp_decoder.go:125-128)
+  uint64_t widths;       // miniblock bit widths, 8 bits each (<= 8 miniblocks)
+  int64_t base;          // value before the block's first delta (first + all earlier deltas)
+  uint32_t pos;          // stream offset of the block's first miniblock payload byte
+  uint32_t sum_lo;       // scratch: low half of the block's delta sum (k_delta_sums); unused
+};
 struct WorkItem {        // 16 B
   uint32_t page;         // global page index
   uint32_t v0;           // first value (within page) of this tile

@@ -334,7 +334,7 @@ class Batch:
     def kernel_times(self):
         """{kernel name: (average ms per launch, launches)} for every timed launch slot."""
         out = {}
-        for k in range(9):
+        for k in range(11):
             ms, n = ctypes.c_double(), ctypes.c_int64()
             name = ctypes.create_string_buffer(64)
             lib().pqgpu_batch_kernel_slot(self._h, k, ctypes.byref(ms), ctypes.byref(n), name, 64)

@@ -13,8 +13,13 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+SPLIT = os.environ.get("PQ_SPLIT_VALUES") == "1"
+
+
 def kname(name, order):
     if "k_values" in name:
+        if not SPLIT:
+            return "k_values"
         return "k_values[delta]" if order % 2 == 0 else "k_values[other]"
     if "k_levels" in name:
         return "k_levels"
