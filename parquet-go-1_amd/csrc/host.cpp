@@ -206,6 +206,13 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
+// PQ_DELTA_TILED=1: DELTA pages through the tiled pipeline (block walk kernel + 2048-value
+// tiles) instead of the single-pass page decoder.
+static bool delta_tiled() {
+  const char *t = getenv("PQ_DELTA_TILED");
+  return t && atoi(t) != 0;
+}
+
 static bool spec_disabled() {
   const char *on = getenv("PQ_SPEC"), *off = getenv("PQ_NO_SPEC");
   if (off && atoi(off) != 0) return true;
@@ -420,9 +427,14 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     pd->delta_mbc = (uint16_t)std::min<int32_t>(mbc, 65535);
     pd->delta_mbvc = (uint32_t)mbvc;
     pd->delta_first_mb = (uint32_t)(vstart + mb_start);
-    // tiled pipeline shapes (kernels.hip k_delta_*): whole groups per miniblock, blocks tiling
-    // kDeltaTileVals, widths packed in one 64-bit word; anything else: exact scalar path
-    if (mbvc % 8 != 0 || bs < 128 || (int32_t)kDeltaTileVals % bs != 0 || mbc > 8) pd->flags |= PF_DELTA_SLOW;
+    // shapes of the parallel paths (kernels.hip): whole groups per miniblock, widths packed in
+    // one 64-bit word; the page decoder needs a whole block (widest case) inside its LDS
+    // window, the tiled pipeline blocks that tile kDeltaTileVals; anything else: exact scalar path
+    const uint64_t max_blk = 10 + (uint64_t)mbc + (uint64_t)bs * (is64 ? 8 : 4);
+    const bool shape_ok = mbvc % 8 == 0 && mbc <= 8 &&
+                          (delta_tiled() ? (bs >= 128 && (int32_t)kDeltaTileVals % bs == 0)
+                                         : max_blk + 48 <= kDeltaWinLoad);
+    if (!shape_ok) pd->flags |= PF_DELTA_SLOW;
     if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
     return PQ_OK;
   }
@@ -688,6 +700,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           if (!ns_p) break;
           if (pd.flags & PF_DELTA_SLOW) {
             b->items.push_back(WorkItem{p, 0, ns_p, WI_DELTA, {0, 0, 0}});
+          } else if (!delta_tiled()) {
+            b->items.push_back(WorkItem{p, 0, ns_p, WI_DELTA_PAGE, {0, 0, 0}});
           } else {
             const uint32_t bs = (uint32_t)pd.delta_mbc * pd.delta_mbvc;
             b->delta_pages.push_back(p);
@@ -729,13 +743,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_end = a;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the bandwidth-bound tiles
-  auto rank = [](uint8_t k) { return k == WI_DELTA_TILE ? 0 : k == WI_DELTA ? 1 : 2; };
+  auto rank = [](uint8_t k) { return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : 2; };
   std::stable_sort(b->items.begin(), b->items.end(),
                    [&](const WorkItem &x, const WorkItem &y) { return rank(x.kind) < rank(y.kind); });
   b->n_delta_items = 0;
   b->n_delta_tiles = 0;
   for (auto &it : b->items) {
-    b->n_delta_items += it.kind == WI_DELTA || it.kind == WI_DELTA_TILE;
+    b->n_delta_items += it.kind == WI_DELTA || it.kind == WI_DELTA_TILE || it.kind == WI_DELTA_PAGE;
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
   }
   // batch-level arrays
@@ -880,6 +894,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.dblk_sum = (unsigned long long *)(A + b->o_dblk_sum);
   d.spec_mismatch = (uint32_t *)(A + b->o_spec_flag);
   d.spec = b->spec ? 1u : 0u;
+  d.ablate = getenv("PQ_ABLATE") ? (uint32_t)atoi(getenv("PQ_ABLATE")) : 0u;
   d.page_rec = (uint32_t *)(A + b->o_rec);
   d.page_vbase = (uint64_t *)(A + b->o_vbase);
   d.page_rbase = (uint64_t *)(A + b->o_rbase);

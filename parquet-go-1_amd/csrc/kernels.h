@@ -33,6 +33,7 @@ struct BatchDev {
   unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
   uint32_t spec;                  // 1: value bases came from the page headers (see k_bases)
+  uint32_t ablate;                // diagnostic build only (PQ_ABLATE): skip phases to time them
 };
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)

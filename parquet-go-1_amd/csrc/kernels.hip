@@ -31,13 +31,13 @@ const char *kValuesKernelName = "k_values";
 // ---------------------------------------------------------------------------
 DEV uint32_t ld32(const uint8_t *p) {
   uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t *q = (const uint32_t *)(p - (a & 3));  // pointer arithmetic keeps the address space
   uint32_t lo = q[0], hi = q[1];
   return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
 }
 DEV uint64_t ld64(const uint8_t *p) {
   uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t *q = (const uint32_t *)(p - (a & 3));
   uint32_t s = (uint32_t)(a & 3);
   uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
   uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, s);
@@ -83,6 +83,39 @@ DEV uint64_t bits64c(const uint8_t *p, uint32_t n, uint64_t bo, uint32_t nb) {  
 
 DEV uint32_t lane_id() { return __lane_id(); }
 
+// Global-memory pointers. Device addresses travel in descriptors as integers and in BatchDev
+// as generic pointers, which compile to FLAT instructions; a FLAT access counts in both vmcnt
+// and lgkmcnt, so every LDS wait (lgkmcnt) would also wait for all outstanding loads and
+// stores. Casting each pointer's origin to address space 1 lets the compiler emit global_*
+// instructions along every use.
+#define PQ_GLOBAL __attribute__((address_space(1)))
+template <class T>
+DEV T *gp(T *p) { return (T *)(PQ_GLOBAL T *)p; }
+template <class T>
+DEV T *gp_u64(uint64_t a) { return (T *)(PQ_GLOBAL T *)(uintptr_t)a; }
+DEV BatchDev global_view(BatchDev b) {
+  b.pages = gp(b.pages); b.chunks = gp(b.chunks); b.chunk_err = gp(b.chunk_err);
+  b.page_nn = gp(b.page_nn); b.page_nn_v = gp(b.page_nn_v); b.spec_mismatch = gp(b.spec_mismatch);
+  b.page_rec = gp(b.page_rec); b.page_vbase = gp(b.page_vbase); b.page_rbase = gp(b.page_rbase);
+  b.runs = gp(b.runs); b.run_base = gp(b.run_base); b.run_count = gp(b.run_count);
+  b.tile_first = gp(b.tile_first); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
+  b.dblk = gp(b.dblk); b.dblk_base = gp(b.dblk_base); b.dblk_n = gp(b.dblk_n); b.dblk_sum = gp(b.dblk_sum);
+  if (b.dbg) b.dbg = gp(b.dbg);
+  return b;
+}
+
+// Workgroup barrier for LDS hand-offs. __syncthreads() is a workgroup-scope release/acquire
+// over every address space, so it waits for all of the wave's outstanding global loads and
+// stores (vmcnt(0)) before s_barrier: prefetched windows and the previous batch's stores
+// would be drained at every barrier. Every barrier in this file orders LDS accesses only
+// (global results are never read back by another thread of the same workgroup), so the
+// fences are restricted to LDS and only lgkmcnt is waited for.
+DEV void wg_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Diagnostic phase stamps: per-wave cycle sums added to b.dbg. Compiled in only for the
 // diagnostic library (make diag -> lib/libpqgpu_diag.so, -DPQ_DIAG_STAMPS) and active there
 // when PQ_DEBUG_STAMPS=1; the production kernels carry no stamp code or registers.
@@ -100,14 +133,18 @@ struct Stamps {
       for (int k = 0; k < 8; k++) if (acc[k]) atomicAdd(&dbg[base + k], (unsigned long long)acc[k]);
   }
   DEV void count(int k) { if (dbg) acc[k]++; }
+  DEV void add(int k, uint64_t v) { if (dbg) acc[k] += v; }
 };
 #define PQ_STAMPS(name, dbgp) Stamps name{dbgp, 0, {0, 0, 0, 0, 0, 0, 0, 0}}
+#define PQ_ABLATE(b, bit) (((b).ablate >> (bit)) & 1u)
 #else
+#define PQ_ABLATE(b, bit) 0u
 struct Stamps {
   DEV void begin() {}
   DEV void lap(int) {}
   DEV void flush(int) {}
   DEV void count(int) {}
+  DEV void add(int, uint64_t) {}
 };
 #define PQ_STAMPS(name, dbgp) Stamps name
 #endif
@@ -306,15 +343,15 @@ DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
   const uint32_t rs = (bw + 7) >> 3;
   uint32_t pos = 0, done = 0, sb = 0;
   stage_load(L.stage, s, 0, n);
-  __syncthreads();
+  wg_barrier();
   while (done < need) {
     // keep the candidate headers (pos .. pos+76) and short-run payloads staged
     if (st) st->lap(7);
     if (pos + 208 > sb + kStage) {
       sb = sgpr(pos & ~3u);
-      __syncthreads();
+      wg_barrier();
       stage_load(L.stage, s, sb, n);
-      __syncthreads();
+      wg_barrier();
       if (st) { st->lap(0); st->count(5); }
     }
     // ---- speculative header decode at c = pos + lane
@@ -389,14 +426,14 @@ struct LevelSink {
   DEV void set_bits(uint32_t slot, uint64_t m, uint32_t nb) {
     if (!m) return;
     if (!bits_lds) {
-      if (bits_glob) or_bits(bits_glob, slot_base + slot, m);
+      if (bits_glob) or_bits(gp(bits_glob), slot_base + slot, m);
       return;
     }
     if (slot + nb <= kSegSlots) { or_bits(bits_lds, slot, m); return; }
-    if (slot >= kSegSlots) { or_bits(bits_glob, slot_base + slot, m); return; }
+    if (slot >= kSegSlots) { or_bits(gp(bits_glob), slot_base + slot, m); return; }
     const uint32_t lo = kSegSlots - slot;  // split at the LDS segment end
     or_bits(bits_lds, slot, m & ((1ull << lo) - 1ull));
-    or_bits(bits_glob, slot_base + kSegSlots, m >> lo);
+    or_bits(gp(bits_glob), slot_base + kSegSlots, m >> lo);
   }
 
   // Up to 64 values of one run, starting at value k of the run. `stg`/`sb`: the LDS stage.
@@ -614,17 +651,17 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     if (pos0 >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
     const uint32_t cs = pos0, sb = cs & ~3u;
     const uint32_t clen = min(kLvChunk, n - cs), cend = cs + clen, send = sb + kLvStageB;
-    __syncthreads();
+    wg_barrier();
     st.lap(7);
     stage_load_blk(L.stage, s, sb, n, kLvStageB / 4 + 4);
-    __syncthreads();
+    wg_barrier();
     st.lap(0);
     // ---- P1: links
     for (uint32_t i = tid; i < clen; i += nt) {
       const FastHdr f = fast_hdr(L.stage, sb, cs + i, n, bw, rs);
       L.JV[i] = make_uint2(cs + i + f.adv, f.nvals);
     }
-    __syncthreads();
+    wg_barrier();
     st.lap(1);
     // ---- P1b: pointer doubling, in place. A (target, values) pair is read and written as
     // one 8-byte LDS access, so a pair another lane already advanced this round is still a
@@ -639,7 +676,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         }
       }
     }
-    __syncthreads();
+    wg_barrier();
     st.lap(2);
     // ---- P2: the true chain by jumps (one lane)
     if (tid == 0) {
@@ -683,7 +720,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       L.next_e = p; L.done_out = cum; L.nlong = 0;
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();
+    wg_barrier();
     st.lap(3);
     // ---- P3: one lane per checkpoint re-walks its runs and expands them
     const uint32_t nck = L.nck;
@@ -708,7 +745,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       }
     }
     st.lap(4);
-    __syncthreads();
+    wg_barrier();
     // long runs: every thread expands 32-value pieces (64 for the generic sink)
     const uint32_t nlong = L.nlong;
     for (uint32_t r = 0; r < nlong; r++) {
@@ -720,7 +757,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         else sk.piece(bp != 0, val, f + q, q, m, L.stage, sb);
       }
     }
-    if (nlong) __syncthreads();
+    if (nlong) wg_barrier();
     st.lap(5);
     if (L.stop_kind != LV_RUN) {
       if (L.stop_kind != LV_STOP_NEED) sk.error(L.stop_vpos, L.stop_code);
@@ -734,15 +771,16 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
 // BW1: every level stream of the pages is a bit-width-1 definition stream with validity
 // output only (flat OPTIONAL columns: max_def == 1, max_rep == 0).
 template <bool BW1, int NT>
-__global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(NT) k_levels_t(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
   __shared__ LevelLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
-  const uint8_t *base = (const uint8_t *)pd.data;
+  const uint8_t *base = gp_u64<const uint8_t>(pd.data);
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t ns = pd.num_slots;
-  uint32_t *vbits = (uint32_t *)cd.validity;
+  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
   for (uint32_t k = tid; k < kSegSlots / 32; k += blockDim.x) lds.bits[k] = 0;
   uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
   PQ_STAMPS(st, b.dbg);
@@ -754,8 +792,8 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pag
     sk.s = base + (rep ? pd.rep_off : pd.def_off);
     sk.n = rep ? pd.rep_len : pd.def_len;
     sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
-    sk.out = rep ? (uint8_t *)cd.rep_levels + pd.slot_base
-                 : (cd.def_levels ? (uint8_t *)cd.def_levels + pd.slot_base : nullptr);
+    sk.out = rep ? gp_u64<uint8_t>(cd.rep_levels) + pd.slot_base
+                 : (cd.def_levels ? gp_u64<uint8_t>(cd.def_levels) + pd.slot_base : nullptr);
     sk.bits_lds = rep ? nullptr : lds.bits;
     sk.bits_glob = rep ? nullptr : vbits;
     sk.slot_base = pd.slot_base;
@@ -764,7 +802,7 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pag
     sk.err_code = 0;
     sk.err_pos = 0;
     sk.stage_len = kLvStageB;
-    __syncthreads();
+    wg_barrier();
     if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
       if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
     } else {
@@ -772,7 +810,7 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pag
     }
     const uint64_t wc = wave_sum64(sk.count);
     if (lane == 0) lds.cnt[wv] = wc;
-    __syncthreads();
+    wg_barrier();
     uint64_t cntv = 0;
     for (uint32_t k = 0; k < (blockDim.x >> 6); k++) cntv += lds.cnt[k];
     if (sk.err_code) {  // workgroup-uniform
@@ -789,10 +827,10 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pag
     } else {
       nn = (uint32_t)cntv;
     }
-    __syncthreads();
+    wg_barrier();
   }
   if (cd.max_def > 0) {
-    __syncthreads();
+    wg_barrier();
     // flush the LDS bitmap segment to the chunk bitmap
     const uint32_t seg = min(ns, kSegSlots);
     const uint32_t nw = (seg + 31) / 32;
@@ -828,12 +866,13 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b, const uint32_t *pag
 // reference derives notNull from the definition levels (page_v1.go:49-52), so
 // any difference sends the batch back through the serial path (host.cpp).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_bases(BatchDev b, const uint32_t *chunks) {
+__global__ void __launch_bounds__(256) k_bases(BatchDev b_in, const uint32_t *chunks) {
+  const BatchDev b = global_view(b_in);
   const ChunkDesc &cd = b.chunks[chunks[blockIdx.x]];
   __shared__ uint64_t carry_v, carry_r;
   __shared__ uint64_t part_v[256], part_r[256];
   if (threadIdx.x == 0) { carry_v = 0; carry_r = 0; }
-  __syncthreads();
+  wg_barrier();
   for (uint32_t p0 = 0; p0 < cd.num_pages; p0 += 256) {
     uint32_t p = p0 + threadIdx.x;
     uint32_t gp = cd.first_page + p;
@@ -848,22 +887,22 @@ __global__ void __launch_bounds__(256) k_bases(BatchDev b, const uint32_t *chunk
     }
     part_v[threadIdx.x] = nv;
     part_r[threadIdx.x] = nr;
-    __syncthreads();
+    wg_barrier();
     for (uint32_t d = 1; d < 256; d <<= 1) {
       uint64_t av = threadIdx.x >= d ? part_v[threadIdx.x - d] : 0;
       uint64_t ar = threadIdx.x >= d ? part_r[threadIdx.x - d] : 0;
-      __syncthreads();
+      wg_barrier();
       part_v[threadIdx.x] += av;
       part_r[threadIdx.x] += ar;
-      __syncthreads();
+      wg_barrier();
     }
     if (p < cd.num_pages) {
       if (!b.spec) b.page_vbase[gp] = carry_v + part_v[threadIdx.x] - nv;
       b.page_rbase[gp] = carry_r + part_r[threadIdx.x] - nr;
     }
-    __syncthreads();
+    wg_barrier();
     if (threadIdx.x == 255) { carry_v += part_v[255]; carry_r += part_r[255]; }
-    __syncthreads();
+    wg_barrier();
   }
 }
 
@@ -900,7 +939,8 @@ struct RunSink {
   }
 };
 
-__global__ void __launch_bounds__(64) k_scan_runs(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(64) k_scan_runs(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
   __shared__ WalkLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
@@ -908,7 +948,7 @@ __global__ void __launch_bounds__(64) k_scan_runs(BatchDev b, const uint32_t *pa
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
   uint32_t done = 0;
   if (nn && pd.dict_bw > 0) {
-    done = hyb_walk(lds, (const uint8_t *)pd.data + pd.val_off, pd.val_len, pd.dict_bw, nn, rs);
+    done = hyb_walk(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs);
   }
   if (lane_id() == 0) {
     b.run_count[pi] = rs.nruns;
@@ -930,11 +970,6 @@ struct DictLDS {
 struct DeltaTileLDS {
   uint64_t scan[260];        // per-group exclusive scan + per-wave totals
   uint32_t stage[(kDeltaTileVals * 8 + 8 * 24 + 64) / 4];  // the tile's payload bytes
-};
-union ValuesLDS {
-  DictLDS dict;
-  DeltaTileLDS dtile;        // WI_DELTA_TILE
-  uint8_t slow_widths[256];
 };
 
 // Reference fixed-width PLAIN error: binary.Read/io.ReadFull of w bytes per value
@@ -974,7 +1009,7 @@ DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, 
   uint4 *d = (uint4 *)(dst + head);
   const uint8_t *sp = src + head;
   const uint32_t sa = (uint32_t)((uintptr_t)sp & 15);
-  const uint4 *sb = (const uint4 *)((uintptr_t)sp & ~(uintptr_t)15);
+  const uint4 *sb = (const uint4 *)(sp - sa);
   const uint64_t pieces = body >> 4;
   uint64_t i = tid;
   if (sa == 0) {
@@ -1008,8 +1043,8 @@ DEV void do_plain(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   uint32_t e1 = (uint32_t)min((uint64_t)v1, fit);
   if (e1 < v1 && threadIdx.x == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)fit, plain_err(have, w));
   if (e1 <= wi.v0) return;
-  const uint8_t *src = (const uint8_t *)pd.data + pd.val_off + (uint64_t)wi.v0 * w;
-  uint8_t *dst = (uint8_t *)cd.values + (b.page_vbase[wi.page] + wi.v0) * w;
+  const uint8_t *src = gp_u64<const uint8_t>(pd.data) + pd.val_off + (uint64_t)wi.v0 * w;
+  uint8_t *dst = gp_u64<uint8_t>(cd.values) + (b.page_vbase[wi.page] + wi.v0) * w;
   copy_bytes(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
 }
 
@@ -1020,8 +1055,8 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   if (v1 > fit && threadIdx.x == 0 && wi.v0 <= fit)
     report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)fit, PQ_ERR_EOF);
   uint32_t e1 = (uint32_t)min((uint64_t)v1, fit);
-  const uint8_t *src = (const uint8_t *)pd.data + pd.val_off;
-  uint8_t *dst = (uint8_t *)cd.values + b.page_vbase[wi.page];
+  const uint8_t *src = gp_u64<const uint8_t>(pd.data) + pd.val_off;
+  uint8_t *dst = gp_u64<uint8_t>(cd.values) + b.page_vbase[wi.page];
   for (uint32_t v = wi.v0 + threadIdx.x; v < e1; v += blockDim.x) dst[v] = (src[v >> 3] >> (v & 7)) & 1;
 }
 
@@ -1031,7 +1066,7 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
                  DictLDS &lds) {
   uint32_t v1 = min(wi.v1, nn);
   if (wi.v0 >= v1) return;
-  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   const uint32_t bw = pd.dict_bw;
   const uint32_t tile = wi.v0 / kDictTile;
   const uint32_t nruns = b.run_count[wi.page];
@@ -1056,10 +1091,10 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   uint32_t first_err = 0xffffffffu, first_err_code = 0;
   for (uint32_t rb = r0; rb <= r1; rb += 1024) {
     uint32_t nr = min(1024u, r1 + 1 - rb);
-    __syncthreads();
+    wg_barrier();
     if (bw > 0)
       for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) lds.runs[k] = runs[rb + k];
-    __syncthreads();
+    wg_barrier();
     // value range covered by this batch of runs
     uint32_t lo = bw > 0 ? max(wi.v0, lds.runs[0].value_start) : wi.v0;
     uint32_t hi = v1;
@@ -1088,7 +1123,7 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
           else idx = r.info;
         }
         if (is_bool) {
-          ((uint8_t *)cd.values)[vb + v] = idx == 1;
+          (gp_u64<uint8_t>(cd.values))[vb + v] = idx == 1;
           continue;
         }
         if ((int32_t)idx < 0 || idx >= dcount) {
@@ -1096,17 +1131,17 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
           continue;
         }
         if (is_ba) {
-          const int32_t *doff = (const int32_t *)cd.dict_offsets;
+          const int32_t *doff = gp_u64<const int32_t>(cd.dict_offsets);
           int32_t o0 = doff[2 * idx], o1 = doff[2 * idx + 1];
-          ((uint64_t *)cd.ba_index)[vb + v] = cd.dict_values + (uint64_t)o0;
-          ((int32_t *)cd.offsets)[vb + v + 1] = o1 - o0;  // length, scanned later
+          (gp_u64<uint64_t>(cd.ba_index))[vb + v] = cd.dict_values + (uint64_t)o0;
+          (gp_u64<int32_t>(cd.offsets))[vb + v + 1] = o1 - o0;  // length, scanned later
         } else if (w == 4) {
-          ((uint32_t *)cd.values)[vb + v] = ((const uint32_t *)cd.dict_values)[idx];
+          (gp_u64<uint32_t>(cd.values))[vb + v] = (gp_u64<const uint32_t>(cd.dict_values))[idx];
         } else if (w == 8) {
-          ((uint64_t *)cd.values)[vb + v] = ((const uint64_t *)cd.dict_values)[idx];
+          (gp_u64<uint64_t>(cd.values))[vb + v] = (gp_u64<const uint64_t>(cd.dict_values))[idx];
         } else {
-          const uint8_t *src = (const uint8_t *)cd.dict_values + (uint64_t)idx * w;
-          uint8_t *dst = (uint8_t *)cd.values + (vb + v) * w;
+          const uint8_t *src = gp_u64<const uint8_t>(cd.dict_values) + (uint64_t)idx * w;
+          uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v) * w;
           for (uint32_t k = 0; k < w; k++) dst[k] = src[k];
         }
       }
@@ -1330,13 +1365,14 @@ struct DeltaIndexLDS {
   uint32_t nblk, next, done;
 };
 
-__global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(256) k_delta_walk(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
   __shared__ DeltaIndexLDS L;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc &pd = b.pages[pi];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t nn = b.page_nn_v[pi];
-  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   const uint32_t n = pd.val_len;
   const bool is64 = pd.vkind == VK_DELTA64;
   const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
@@ -1362,7 +1398,7 @@ __global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *
       uint4 *dst = (uint4 *)L.win;
       for (uint32_t q = tid; q < kDiWin / 16 + 1; q += 256) dst[q] = (int64_t)q * 16 < lim ? src[q] : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+    wg_barrier();
     const int64_t wend = (int64_t)wa + kDiWin;  // bytes [wa, wend) are staged
     // ---- wave 0 walks the blocks that fit whole in the window
     if (wv == 0) {
@@ -1415,12 +1451,12 @@ __global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *
       if (lane == 0) { L.nblk = k; L.next = p; L.done = done; }
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();
+    wg_barrier();
     const uint32_t nb = L.nblk;
     // ---- block sums of the window's blocks (groups past the stream end contribute 0;
     // their read error is reported by the tile pass)
     for (uint32_t q = tid; q < nb; q += 256) L.acc[q] = 0;
-    __syncthreads();
+    wg_barrier();
     for (uint32_t gi = tid; gi < nb * gpb; gi += 256) {
       const uint32_t k = gi / gpb, inb = (gi % gpb) * 8;
       if ((uint64_t)(j + k) * bs + inb >= limit) continue;
@@ -1437,14 +1473,14 @@ __global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *
       for (int e = 0; e < 8; e++) sum += d[e];
       atomicAdd(&L.acc[k], (unsigned long long)sum);
     }
-    __syncthreads();
+    wg_barrier();
     // ---- scan of the block sums -> block base values; complete block records
     for (uint32_t k0 = 0; k0 < nb; k0 += 256) {
       const uint32_t k = k0 + tid;
       const uint64_t v = k < nb ? (uint64_t)L.acc[k] : 0;
       const uint64_t incl = wave_incl_scan64(v);
       if (lane == 63) L.wsum[wv] = incl;
-      __syncthreads();
+      wg_barrier();
       uint64_t before = carry, total = 0;
       for (uint32_t q = 0; q < 4; q++) {
         if (q < wv) before += L.wsum[q];
@@ -1460,12 +1496,12 @@ __global__ void __launch_bounds__(256) k_delta_walk(BatchDev b, const uint32_t *
         tab[j + k] = blk;
       }
       carry += total;
-      __syncthreads();
+      wg_barrier();
     }
     j += nb;
     pos = L.next;
     stop = L.done || j >= need || (nb == 0 && pos >= n);
-    __syncthreads();
+    wg_barrier();
   }
   if (tid == 0) b.dblk_n[pi] = j;
 }
@@ -1482,8 +1518,8 @@ DEV void delta_group_at(const DeltaBlk &B, uint32_t inb, uint32_t mbvc, uint32_t
 // A group is w bytes; widths <= 16 read 5 aligned dwords once, wider ones per value.
 DEV void delta_unpack8(const uint8_t *s, uint32_t goff, uint32_t w, bool is64, int64_t md, uint64_t (&d)[8]) {
   if (w <= 16) {
-    const uint32_t *q = (const uint32_t *)((uintptr_t)(s + goff) & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)((uintptr_t)(s + goff) & 3);
+    const uint32_t *q = (const uint32_t *)(s + goff - sh);
     const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
     const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
     const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(x3, x2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x4, x3, sh) << 32);
@@ -1540,7 +1576,7 @@ DEV int32_t delta_stage_tile(const BatchDev &b, const WorkItem &wi, const PageDe
   const DeltaBlk last = tab[j1];
   const uint32_t lo = tab[j0].pos;
   const uint32_t hi = min((uint64_t)last.pos + (uint64_t)g8 * bytesum64(last.widths), (uint64_t)n);
-  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   const int32_t base = (int32_t)lo - (int32_t)(((uintptr_t)(s + lo)) & 15u);
   const int32_t end = (int32_t)max(hi, lo) + 16;  // the page padding keeps 16 B past n readable
   const uint32_t nv = (uint32_t)(end - base + 15) / 16;
@@ -1578,7 +1614,8 @@ DEV void delta_unpack8_lds(const uint32_t *stg, int32_t base, uint32_t goff, uin
   }
 }
 
-__global__ void __launch_bounds__(256) k_delta_sums(BatchDev b, const WorkItem *items) {
+__global__ void __launch_bounds__(256) k_delta_sums(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
   __shared__ uint32_t stg[kDtStageB / 4];
   __shared__ unsigned long long acc[kDeltaTileVals / 128];
   const WorkItem wi = items[blockIdx.x];
@@ -1591,7 +1628,7 @@ __global__ void __launch_bounds__(256) k_delta_sums(BatchDev b, const WorkItem *
   if (tid < nbt) acc[tid] = 0;
   if (wi.v0 >= limit) return;  // workgroup-uniform
   const int32_t base = delta_stage_tile(b, wi, pd, stg);
-  __syncthreads();
+  wg_barrier();
   DeltaBlk B;
   const DeltaGroup g = delta_tile_group(b, wi, pd, limit, tid, &B);
   if (g.valid && !g.err) {
@@ -1602,14 +1639,15 @@ __global__ void __launch_bounds__(256) k_delta_sums(BatchDev b, const WorkItem *
     for (int k = 0; k < 8; k++) sum += d[k];
     atomicAdd(&acc[(g.d0 - wi.v0) / bs], (unsigned long long)sum);
   }
-  __syncthreads();
+  wg_barrier();
   if (tid < nbt) {
     const uint32_t j = wi.v0 / bs + tid;
     if (j < b.dblk_n[wi.page]) b.dblk_sum[b.dblk_base[wi.page] + j] = acc[tid];
   }
 }
 
-__global__ void __launch_bounds__(256) k_delta_prefix(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(256) k_delta_prefix(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
   __shared__ uint64_t wsum[4];
   __shared__ uint64_t carry;
   const uint32_t pi = pages[blockIdx.x];
@@ -1619,22 +1657,22 @@ __global__ void __launch_bounds__(256) k_delta_prefix(BatchDev b, const uint32_t
   DeltaBlk *tab = b.dblk + b.dblk_base[pi];
   const unsigned long long *sums = b.dblk_sum + b.dblk_base[pi];
   if (tid == 0) carry = (uint64_t)pd.delta_first;
-  __syncthreads();
+  wg_barrier();
   for (uint32_t j0 = 0; j0 < nb; j0 += 256) {
     const uint32_t j = j0 + tid;
     const uint64_t v = j < nb ? sums[j] : 0;
     const uint64_t incl = wave_incl_scan64(v);
     if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
+    wg_barrier();
     uint64_t before = carry, total = 0;
     for (uint32_t k = 0; k < 4; k++) {
       if (k < wv) before += wsum[k];
       total += wsum[k];
     }
     if (j < nb) tab[j].base = (int64_t)(before + incl - v);
-    __syncthreads();
+    wg_barrier();
     if (tid == 0) carry += total;
-    __syncthreads();
+    wg_barrier();
   }
 }
 
@@ -1647,7 +1685,7 @@ DEV void do_delta_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
   const uint32_t limit = min(nn, (uint32_t)max(pd.delta_count, 0));
   if (wi.v0 >= limit) return;  // workgroup-uniform
   const int32_t base = delta_stage_tile(b, wi, pd, stg);
-  __syncthreads();
+  wg_barrier();
   DeltaBlk B;
   const DeltaGroup g = delta_tile_group(b, wi, pd, limit, tid, &B);
   uint64_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1661,12 +1699,12 @@ DEV void do_delta_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
   // exclusive scan of group sums over the tile; a block's values restart from its base
   const uint64_t incl = wave_incl_scan64(sum);
   if (lane == 63) scan[256 + wv] = incl;
-  __syncthreads();
+  wg_barrier();
   uint64_t before = 0;
   for (uint32_t k = 0; k < wv; k++) before += scan[256 + k];
   const uint64_t excl = before + incl - sum;
   scan[tid] = excl;
-  __syncthreads();
+  wg_barrier();
   // values of this group, staged in LDS (the payload stage is free after the scan barrier)
   // and stored with coalesced 16-B writes: a thread's 8 values are 64 contiguous bytes, so
   // storing them directly would make every store instruction write partial cache lines
@@ -1688,11 +1726,11 @@ DEV void do_delta_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     o[0] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
     o[1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
   }
-  __syncthreads();
+  wg_barrier();
   const uint32_t w = is64 ? 8u : 4u;
   const uint32_t cnt = min(kDeltaTileVals, limit - wi.v0);  // values of this tile before the limit
   const uint64_t vb = b.page_vbase[wi.page];
-  uint8_t *dst = (uint8_t *)cd.values + (vb + wi.v0) * w;
+  uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + wi.v0) * w;
   const uint32_t bytes = cnt * w;
   if (((uintptr_t)dst & 15) == 0) {
     for (uint32_t q = tid; q < bytes / 16; q += blockDim.x) ((uint4 *)dst)[q] = ((const uint4 *)stg)[q];
@@ -1705,12 +1743,355 @@ DEV void do_delta_tile(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
   }
 }
 
+// ---------------------------------------------------------------------------
+// DELTA_BINARY_PACKED, one workgroup per page, single pass (WI_DELTA_PAGE;
+// deltabp_decoder.go:113-174 / :272-333).
+//
+// The stream goes through an LDS window of kDeltaWinLoad bytes that starts at the next
+// block header. Per window:
+//  1. walk: wave 0 follows the block-header chain (position -> next position only:
+//     varint length from a byte mask, widths summed with SWAR) in scalar registers;
+//     headers the fast form cannot take go through the exact parser;
+//  2. the next window's loads are issued into registers (they land during 3-4);
+//  3. parse: one thread per walked block re-reads its header exactly (minDelta,
+//     widths, Go error class) and finds the first group io.ReadFull cannot read whole;
+//     the first error in value order (an LDS atomicMin over (position, class)) bounds the
+//     values written;
+//  4. batches of 256 groups of 8 deltas: unpack from LDS, wave64 DPP scan of the group
+//     sums plus a 4-wave combine, 8 values per thread written as 16-B stores.
+// Semantics as the tiled path above: value i = first + sum_{k<i} delta_k; returning value
+// i reads the group (and at a block start the header) holding delta i (Q1); positions >=
+// valuesCount fail with io.EOF.
+// ---------------------------------------------------------------------------
+struct DeltaPageLDS {
+  uint32_t win[kDeltaWinLoad / 4 + 8];  // stream bytes [win0, win0 + kDeltaWinLoad + 32)
+  uint32_t hpos[kDeltaMaxBlk];          // header position of each walked block
+  uint32_t ppos[kDeltaMaxBlk];          // payload position
+  int64_t md[kDeltaMaxBlk];
+  uint64_t wd[kDeltaMaxBlk];            // miniblock widths, 8 bits each
+  uint64_t wsum[2][4];                  // per-wave batch totals (double-buffered by batch parity)
+  uint4 xpose[4][256];                  // per-wave output transpose (64 lanes x 64 B)
+  unsigned long long stop;              // (value position << 4 | class) of the first error
+  uint32_t nb, next;
+};
+
+union ValuesLDS {
+  DictLDS dict;
+  DeltaTileLDS dtile;        // WI_DELTA_TILE
+  DeltaPageLDS dpage;        // WI_DELTA_PAGE
+  uint8_t slow_widths[256];
+};
+
+// Length of the block at stream position pos (scalar registers): header varint of at most
+// 8 - mbc bytes, widths from the same 8 bytes. 0 = take the exact parser.
+DEV uint32_t delta_blk_len_s(const uint32_t *win, int32_t win0, uint32_t pos, uint32_t mbc, uint32_t g8) {
+  const uint32_t off = (uint32_t)((int32_t)pos - win0), a = off >> 2, sh = off & 3;
+  const uint32_t w0 = sgpr(win[a]), w1 = sgpr(win[a + 1]), w2 = sgpr(win[a + 2]);
+  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
+  const uint64_t x = sh ? ((lo >> (8 * sh)) | ((uint64_t)w2 << (64 - 8 * sh))) : lo;  // bytes pos .. pos+7
+  const uint32_t t = ~(uint32_t)x & 0x80808080u;
+  if (!t) return 0;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t) >> 3) + 1;
+  if (L + mbc > 8) return 0;
+  const uint64_t ww = (x >> (8 * L)) & ((1ull << (8 * mbc)) - 1ull);
+  return L + mbc + g8 * bytesum64_swar(ww);
+}
+
+// The same on vector byte operations (wave-uniform inputs; the result goes back to a scalar
+// register): varint terminator by mask + ffbl, widths by a 64-bit funnel and one SAD. mbc <= 4.
+DEV uint32_t delta_blk_len_v(const uint32_t *win, int32_t win0, uint32_t pos, uint32_t mbc, uint32_t g8) {
+  const uint32_t off = (uint32_t)((int32_t)pos - win0), a = off >> 2, sh = off & 3;
+  uint32_t x0 = win[a], x1 = win[a + 1], x2 = win[a + 2];
+  // keep the byte work on the vector unit: a uniform LDS load would otherwise be moved to
+  // scalar registers word by word, and every VALU <-> SALU hand-off sits on the hop chain
+  asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2));
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(x1, x0, sh), u1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+  const uint32_t t = ~u0 & 0x80808080u;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;  // t == 0 -> 4: rejected below
+  const uint32_t ww = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * L)) & (mbc >= 4 ? ~0u : ((1u << (8 * mbc)) - 1u));
+  const uint32_t bl = __umul24(g8, __builtin_amdgcn_sad_u8(ww, 0u, 0u)) + L + mbc;
+  const uint32_t ok = (uint32_t)(t != 0) & (uint32_t)(L + mbc <= 8);
+  return sgpr(bl * ok);
+}
+
+// wave64 inclusive scan of 64-bit values (wrapping) with DPP row shifts / broadcasts
+DEV uint64_t wave_incl_scan64_dpp(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define PQ_SCAN_STEP(CTRL, ROWS)                                                  \
+  {                                                                               \
+    const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROWS, 0xf, false); \
+    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWS, 0xf, false); \
+    const uint64_t s = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2); \
+    lo = (uint32_t)s; hi = (uint32_t)(s >> 32);                                   \
+  }
+  PQ_SCAN_STEP(0x111, 0xf)
+  PQ_SCAN_STEP(0x112, 0xf)
+  PQ_SCAN_STEP(0x114, 0xf)
+  PQ_SCAN_STEP(0x118, 0xf)
+  PQ_SCAN_STEP(0x142, 0xa)
+  PQ_SCAN_STEP(0x143, 0xc)
+#undef PQ_SCAN_STEP
+  return ((uint64_t)hi << 32) | lo;
+}
+
+DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
+                       DeltaPageLDS &L) {
+  if (nn == 0) return;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
+  const uint32_t n = pd.val_len;
+  const bool is64 = pd.vkind == VK_DELTA64;
+  const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint64_t vb = b.page_vbase[wi.page];
+  uint32_t limit = nn;  // next() fails with io.EOF at positions >= the header's valuesCount
+  bool final_eof = false;
+  if ((uint32_t)max(pd.delta_count, 0) < nn) { limit = (uint32_t)max(pd.delta_count, 0); final_eof = true; }
+  const uint32_t need = (uint32_t)(((uint64_t)limit + bs - 1) / bs);  // blocks holding deltas 0 .. limit-1
+  uint64_t carry = (uint64_t)pd.delta_first;
+  uint32_t hdr = pd.delta_first_mb - pd.val_off, blk = 0;
+  const bool al16 = is64 ? (vb & 1) == 0 : (vb & 3) == 0;  // 8 values of a group: 16-B aligned stores
+  constexpr uint32_t kVec = (kDeltaWinLoad + 32 + 16 * 256 - 1) / (16 * 256);
+  uint4 pre[kVec];
+  auto fetch = [&](int32_t w0) {
+    const uint4 *src = (const uint4 *)(s + w0);
+    const int64_t lim = (int64_t)n + 16 - w0;  // the page padding keeps 16 B past n readable (zeros)
+#pragma unroll
+    for (uint32_t j = 0; j < kVec; j++) {
+      const uint32_t k = tid + j * 256;
+      pre[j] = (int64_t)k * 16 < lim && k < (kDeltaWinLoad + 32) / 16 ? src[k] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (uint32_t j = 0; j < kVec; j++) {
+      const uint32_t k = tid + j * 256;
+      if (k < (kDeltaWinLoad + 32) / 16) ((uint4 *)L.win)[k] = pre[j];
+    }
+  };
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
+  int32_t win0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
+  fetch(win0);
+  store();
+  if (tid == 0) L.stop = ~0ull;
+  wg_barrier();
+  st.lap(0);
+  while (blk < need) {
+    // ---- 1. walk (wave 0)
+    if (wv == 0) {
+      __builtin_amdgcn_s_setprio(3);
+      st.lap(1);
+      const int64_t lend = (int64_t)win0 + kDeltaWinLoad;
+      const bool tail = (int64_t)n + 24 <= lend;  // the window holds the stream end (zeros past it)
+      // a fast hop's block ends at or below lim: inside the stream, and the block plus the next
+      // header are staged
+      const uint32_t lim = tail ? n : (uint32_t)min((int64_t)n, lend - 24);
+      const uint32_t kmax = min(kDeltaMaxBlk, need - blk);
+      uint32_t p = sgpr(hdr), k = 0;
+      for (;;) {
+        // fast hops: position -> next position on vector byte ops (funnel shifts, SAD)
+        while (mbc <= 4 && k < kmax) {
+          const uint32_t bl = delta_blk_len_v(L.win, win0, p, mbc, g8);
+          if (!bl || p + bl > lim) break;
+          if (lane == 0) L.hpos[k] = p;
+          k++;
+          p += bl;
+        }
+        // one block by the exact rules (or the end of the walk)
+        if (k >= kmax) break;
+        if (p >= n) {  // next() reads this block's header at EOF: the parse reports it
+          if (lane == 0) L.hpos[k] = p;
+          k++;
+          break;
+        }
+        if (!tail && (int64_t)p + 24 > lend) break;
+        int64_t md;
+        uint64_t wdv;
+        uint32_t hl;
+        if (sgpr(delta_hdr_parse(L.win, (uint32_t)win0, s, n, p, is64, mbc, &md, &wdv, &hl))) {
+          if (lane == 0) L.hpos[k] = p;  // header error: the parse reports it
+          k++;
+          break;
+        }
+        const uint32_t bl = sgpr(hl + g8 * bytesum64_swar(wdv));
+        if (!tail && (int64_t)p + bl + 24 > lend && k > 0) break;  // block not staged whole
+        if (lane == 0) L.hpos[k] = p;
+        k++;
+        if ((uint64_t)p + bl > n) break;  // the stream ends inside this block: the parse reports it
+        p += bl;
+      }
+      if (lane == 0) { L.nb = k; L.next = p; }
+      __builtin_amdgcn_s_setprio(0);
+      st.lap(7);
+      st.add(5, k);
+    }
+    wg_barrier();
+    st.lap(1);
+    const uint32_t nb = sgpr(L.nb);
+    hdr = sgpr(L.next);
+    const bool more = blk + nb < need && nb > 0;
+    const int32_t nwin0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
+    if (more) fetch(nwin0);  // lands during the parse and the batches
+    // ---- 3. parse: thread k re-reads block k's header exactly, finds its first unreadable group
+    if (tid < nb) {
+      const uint32_t p = L.hpos[tid], j = blk + tid;
+      int64_t md = 0;
+      uint64_t wdv = 0;
+      uint32_t hl = 0;
+      unsigned long long key = ~0ull;
+      const uint32_t e = p >= n ? (uint32_t)PQ_ERR_EOF
+                                : delta_hdr_parse(L.win, (uint32_t)win0, s, n, p, is64, mbc, &md, &wdv, &hl);
+      if (e) {
+        key = ((unsigned long long)j * bs << 4) | e;  // read by next() at the block's first position
+      } else {
+        uint64_t start = (uint64_t)p + hl;
+        for (uint32_t m = 0; m < mbc; m++) {
+          const uint32_t w = (uint32_t)(wdv >> (8 * m)) & 0xffu;
+          const uint64_t mend = start + (uint64_t)g8 * w;
+          if (w && mend > n) {  // io.ReadFull of group q (:137-141): EOF if no byte is left
+            const uint32_t q = start >= n ? 0u : (uint32_t)((n - start) / w);
+            const uint32_t ec = start + (uint64_t)q * w >= n ? PQ_ERR_EOF : PQ_ERR_UNEXPECTED_EOF;
+            key = ((unsigned long long)((uint64_t)j * bs + m * mbvc + 8 * q) << 4) | ec;
+            break;
+          }
+          start = mend;
+        }
+      }
+      L.md[tid] = md;
+      L.wd[tid] = wdv;
+      L.ppos[tid] = p + hl;
+      if (key != ~0ull) atomicMin(&L.stop, key);
+    }
+    wg_barrier();
+    st.lap(6);
+    const unsigned long long sk = sgpr64(L.stop);
+    const uint64_t epos = sk >> 4;
+    const uint32_t stop = (uint32_t)min((uint64_t)limit, epos);
+    // ---- 4. batches of 256 groups
+    const uint32_t ng = nb * gpb;
+    uint32_t par = 0;
+    for (uint32_t g0 = 0; g0 < ng; g0 += 256, par ^= 1) {
+      const uint32_t g = g0 + tid;
+      const uint32_t k = g / gpb, inb = (g - k * gpb) * 8;
+      const uint32_t d0 = (blk + k) * bs + inb;
+      const bool valid = g < ng && d0 < stop;
+      uint64_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint64_t sum = 0;
+      if (valid && PQ_ABLATE(b, 1)) {  // diagnostic: no unpack
+#pragma unroll
+        for (int q = 0; q < 8; q++) d[q] = (uint64_t)L.md[k] + q;
+        sum = d[0] * 8;
+      } else if (valid) {
+        const uint32_t m = inb / mbvc, o = inb - m * mbvc;
+        const uint64_t wdv = L.wd[k];
+        const uint32_t w = (uint32_t)(wdv >> (8 * m)) & 0xffu;
+        const uint64_t below = m ? (wdv & ((1ull << (8 * m)) - 1ull)) : 0ull;
+        const uint32_t goff = L.ppos[k] + g8 * bytesum64(below) + (o / 8) * w;
+        delta_unpack8_lds(L.win, win0, goff, w, is64, L.md[k], d);
+#pragma unroll
+        for (int q = 0; q < 8; q++) sum += d[q];
+      }
+      st.lap(2);
+      const uint64_t incl = wave_incl_scan64_dpp(sum);
+      if (lane == 63) L.wsum[par][wv] = incl;
+      wg_barrier();
+      uint64_t before = 0, total = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t t = L.wsum[par][q];
+        before += q < wv ? t : 0ull;
+        total += t;
+      }
+      uint64_t run = carry + before + incl - sum;
+      carry += total;
+      st.lap(3);
+      uint64_t out[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) { out[q] = run; run += d[q]; }
+      if (PQ_ABLATE(b, 0)) {  // diagnostic: no stores (kept live by an impossible condition)
+        if (out[7] == 0x0123456789abcdefull && valid) gp_u64<uint64_t>(cd.values)[vb + d0] = out[0];
+      } else if (__ballot(valid && d0 + 8 <= stop) == ~0ull) {
+        // the wave's 64 groups are 512 consecutive values: transpose through LDS so that every
+        // store instruction writes 1 KiB contiguous (16 B per lane) instead of 64 B-strided pieces
+        uint4 *xw = L.xpose[wv];
+        const uint32_t vw = is64 ? 4u : 2u;  // uint4 per lane
+        if (is64) {
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            xw[lane * 4 + q] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
+                                          (uint32_t)(out[2 * q + 1] >> 32));
+        } else {
+          xw[lane * 2] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
+          xw[lane * 2 + 1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
+        }
+        asm volatile("" ::: "memory");  // same wave: LDS executes its accesses in order
+        const uint32_t wd0 = rdlane(d0, 0);
+        uint8_t *dst0 = gp_u64<uint8_t>(cd.values) + (vb + wd0) * (is64 ? 8 : 4);
+        if (al16) {
+          uint4 *dst = (uint4 *)dst0;
+          for (uint32_t q = 0; q < vw; q++) dst[q * 64 + lane] = xw[q * 64 + lane];
+        } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
+          const uint32_t bytes = vw * 1024, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
+          const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;
+          const uint32_t *xs = (const uint32_t *)xw;
+          uint4 *body = (uint4 *)(dst0 + adj);
+          for (uint32_t j = lane; j < nbody; j += 64) {
+            const uint32_t o = a4 + 4 * j;
+            body[j] = make_uint4(xs[o], xs[o + 1], xs[o + 2], xs[o + 3]);
+          }
+          const uint32_t nt = (bytes - adj - 16 * nbody) >> 2;
+          if (lane < a4) ((uint32_t *)dst0)[lane] = xs[lane];
+          if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xs[a4 + 4 * nbody + lane];
+        }
+      } else if (valid) {
+        if (d0 + 8 <= stop && al16) {
+          if (is64) {
+            uint4 *o4 = (uint4 *)(gp_u64<uint64_t>(cd.values) + vb + d0);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+              o4[q] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
+                                 (uint32_t)(out[2 * q + 1] >> 32));
+          } else {
+            uint4 *o4 = (uint4 *)(gp_u64<uint32_t>(cd.values) + vb + d0);
+            o4[0] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
+            o4[1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            if (d0 + q < stop) {
+              if (is64) (gp_u64<uint64_t>(cd.values))[vb + d0 + q] = out[q];
+              else (gp_u64<uint32_t>(cd.values))[vb + d0 + q] = (uint32_t)out[q];
+            }
+          }
+        }
+      }
+      st.lap(4);
+    }
+    blk += nb;
+    if (epos < limit) {  // the page fails at its first unreadable position
+      if (tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)epos, (uint32_t)(sk & 15));
+      st.flush(8);
+      return;
+    }
+    if (!more) break;
+    // ---- 2'. the prefetched window replaces the current one (every read of it is behind
+    // the last batch's barrier, or the parse barrier when there was no batch)
+    win0 = nwin0;
+    store();
+    wg_barrier();
+    st.lap(0);
+  }
+  st.flush(8);
+  if (final_eof && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, limit, PQ_ERR_EOF);
+}
+
 // Exact scalar restatement of deltaBitPackDecoder.next for pages whose miniblock
 // value count is not a multiple of 8 (deltabp_decoder.go:113-174).
 DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                        uint8_t *widths) {
   if (threadIdx.x != 0 || nn == 0) return;
-  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   const uint32_t n = pd.val_len;
   const bool is64 = pd.vkind == VK_DELTA64;
   const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc;
@@ -1763,8 +2144,8 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     uint64_t ret = prev;
     prev = prev + (uint64_t)mbv[pos % 8] + (uint64_t)md;
     if (!is64) prev = (uint64_t)(int64_t)(int32_t)(uint32_t)prev;
-    if (is64) ((uint64_t *)cd.values)[vb + pos] = ret;
-    else ((uint32_t *)cd.values)[vb + pos] = (uint32_t)ret;
+    if (is64) (gp_u64<uint64_t>(cd.values))[vb + pos] = ret;
+    else (gp_u64<uint32_t>(cd.values))[vb + pos] = (uint32_t)ret;
   }
 }
 
@@ -1772,7 +2153,7 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
 // one lane; records the source address and length of every value.
 DEV void do_plain_ba(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
   if (threadIdx.x != 0) return;
-  const uint8_t *s = (const uint8_t *)pd.data + pd.val_off;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   const uint32_t n = pd.val_len;
   const uint64_t vb = b.page_vbase[wi.page];
   const int32_t fixed = cd.type == T_FLBA ? cd.type_length : 0;
@@ -1788,13 +2169,14 @@ DEV void do_plain_ba(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, 
     }
     if (l > 0 && p >= n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_EOF); return; }
     if ((uint64_t)p + (uint64_t)l > n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_UNEXPECTED_EOF); return; }
-    ((uint64_t *)cd.ba_index)[vb + v] = (uint64_t)(s + p);
-    ((int32_t *)cd.offsets)[vb + v + 1] = (int32_t)l;
+    (gp_u64<uint64_t>(cd.ba_index))[vb + v] = (uint64_t)(s + p);
+    (gp_u64<int32_t>(cd.offsets))[vb + v + 1] = (int32_t)l;
     p += (uint32_t)l;
   }
 }
 
-__global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *items) {
+__global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
   __shared__ ValuesLDS lds;
   const WorkItem wi = items[blockIdx.x];
   const PageDesc &pd = b.pages[wi.page];
@@ -1806,6 +2188,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *item
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
     case WI_DELTA: do_delta_slow(b, wi, pd, cd, nn, lds.slow_widths); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
+    case WI_DELTA_PAGE: do_delta_page(b, wi, pd, cd, nn, lds.dpage); break;
     case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
   }
 }
@@ -1815,13 +2198,14 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b, const WorkItem *item
 // walk the length-prefixed entries; dict_offsets[2i], [2i+1] = start and end
 // byte position of entry i inside the dictionary page. One lane per page.
 // ---------------------------------------------------------------------------
-__global__ void k_dict_ba(BatchDev b, const uint32_t *chunks) {
+__global__ void k_dict_ba(BatchDev b_in, const uint32_t *chunks) {
+  const BatchDev b = global_view(b_in);
   if (threadIdx.x != 0) return;
   const uint32_t ci = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[ci];
-  const uint8_t *s = (const uint8_t *)cd.dict_raw;
+  const uint8_t *s = gp_u64<const uint8_t>(cd.dict_raw);
   const uint32_t n = cd.dict_raw_len;
-  int32_t *offs = (int32_t *)cd.dict_offsets;  // [2*count]: (start, end) of each entry
+  int32_t *offs = gp_u64<int32_t>(cd.dict_offsets);  // [2*count]: (start, end) of each entry
   const int32_t fixed = cd.type == T_FLBA ? cd.type_length : 0;
   uint32_t p = 0;
   for (uint32_t v = 0; v < cd.dict_count; v++) {
@@ -1846,7 +2230,8 @@ __global__ void k_dict_ba(BatchDev b, const uint32_t *chunks) {
 // Pass 1: per-tile sums. Pass 2 (one WG per chunk): scan of tile sums.
 // Pass 3: per-tile scan + write offsets.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ba_tile_sums(BatchDev b, const uint32_t *chunks, const uint64_t *tile_off) {
+__global__ void __launch_bounds__(256) k_ba_tile_sums(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off) {
+  const BatchDev b = global_view(b_in);
   const uint32_t ci = chunks[blockIdx.y];
   const ChunkDesc &cd = b.chunks[ci];
   const uint64_t nn = cd.nn_capacity;  // actual NN is page_vbase of last page + page_nn
@@ -1855,21 +2240,22 @@ __global__ void __launch_bounds__(256) k_ba_tile_sums(BatchDev b, const uint32_t
   (void)nn;
   const uint64_t t = blockIdx.x;
   if (t * kBaTile >= total && !(t == 0)) return;
-  const int32_t *len = (const int32_t *)cd.offsets + 1;
+  const int32_t *len = gp_u64<const int32_t>(cd.offsets) + 1;
   uint64_t s = 0;
   for (uint64_t v = t * kBaTile + threadIdx.x; v < min(total, (t + 1) * kBaTile); v += 256) s += (uint32_t)len[v];
   __shared__ uint64_t red[256];
   red[threadIdx.x] = s;
-  __syncthreads();
+  wg_barrier();
   for (uint32_t d = 128; d > 0; d >>= 1) {
     if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-    __syncthreads();
+    wg_barrier();
   }
   if (threadIdx.x == 0) b.ba_tile_sum[tile_off[blockIdx.y] + t] = (uint32_t)min(red[0], (uint64_t)0xffffffffu);
 }
 
-__global__ void __launch_bounds__(256) k_ba_tile_scan(BatchDev b, const uint32_t *chunks, const uint64_t *tile_off,
+__global__ void __launch_bounds__(256) k_ba_tile_scan(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off,
                                                       uint64_t *totals) {
+  const BatchDev b = global_view(b_in);
   const uint32_t ci = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
@@ -1879,33 +2265,34 @@ __global__ void __launch_bounds__(256) k_ba_tile_scan(BatchDev b, const uint32_t
   __shared__ uint64_t part[256];
   __shared__ uint64_t carry;
   if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
+  wg_barrier();
   for (uint64_t t0 = 0; t0 < ntiles; t0 += 256) {
     uint64_t t = t0 + threadIdx.x;
     uint64_t v = t < ntiles ? ts[t] : 0;
     part[threadIdx.x] = v;
-    __syncthreads();
+    wg_barrier();
     for (uint32_t d = 1; d < 256; d <<= 1) {
       uint64_t a = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-      __syncthreads();
+      wg_barrier();
       part[threadIdx.x] += a;
-      __syncthreads();
+      wg_barrier();
     }
     if (t < ntiles) ts[t] = (uint32_t)(carry + part[threadIdx.x] - v);  // exclusive tile base (< 2^31 checked on host)
-    __syncthreads();
+    wg_barrier();
     if (threadIdx.x == 255) carry += part[255];
-    __syncthreads();
+    wg_barrier();
   }
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-__global__ void __launch_bounds__(256) k_ba_apply(BatchDev b, const uint32_t *chunks, const uint64_t *tile_off) {
+__global__ void __launch_bounds__(256) k_ba_apply(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off) {
+  const BatchDev b = global_view(b_in);
   const uint32_t ci = chunks[blockIdx.y];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
   const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
   const uint64_t t = blockIdx.x;
-  int32_t *offs = (int32_t *)cd.offsets;
+  int32_t *offs = gp_u64<int32_t>(cd.offsets);
   if (t == 0 && threadIdx.x == 0) offs[0] = 0;
   if (t * kBaTile >= total) return;
   const uint32_t base = b.ba_tile_sum[tile_off[blockIdx.y] + t];
@@ -1920,15 +2307,15 @@ __global__ void __launch_bounds__(256) k_ba_apply(BatchDev b, const uint32_t *ch
   }
   __shared__ uint32_t part[256];
   part[threadIdx.x] = s;
-  __syncthreads();
+  wg_barrier();
   for (uint32_t d = 1; d < 256; d <<= 1) {
     uint32_t a = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
+    wg_barrier();
     part[threadIdx.x] += a;
-    __syncthreads();
+    wg_barrier();
   }
   uint32_t run = base + part[threadIdx.x] - s;
-  __syncthreads();
+  wg_barrier();
   for (uint64_t v = v0; v < v1; v++) {
     run += loc[v - v0];
     offs[v + 1] = (int32_t)run;
@@ -1936,15 +2323,16 @@ __global__ void __launch_bounds__(256) k_ba_apply(BatchDev b, const uint32_t *ch
 }
 
 // Payload gather: value v's bytes from ba_src[v] to payload + offsets[v]. One value per thread.
-__global__ void __launch_bounds__(256) k_ba_gather(BatchDev b, const uint32_t *chunks) {
+__global__ void __launch_bounds__(256) k_ba_gather(BatchDev b_in, const uint32_t *chunks) {
+  const BatchDev b = global_view(b_in);
   const uint32_t ci = chunks[blockIdx.y];
   const ChunkDesc &cd = b.chunks[ci];
   const uint32_t lp = cd.first_page + cd.num_pages - 1;
   const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
-  const int32_t *offs = (const int32_t *)cd.offsets;
-  uint8_t *pay = (uint8_t *)cd.payload;
+  const int32_t *offs = gp_u64<const int32_t>(cd.offsets);
+  uint8_t *pay = gp_u64<uint8_t>(cd.payload);
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (uint64_t)gridDim.x * 256) {
-    const uint8_t *src = (const uint8_t *)((const uint64_t *)cd.ba_index)[v];
+    const uint8_t *src = gp_u64<const uint8_t>((gp_u64<const uint64_t>(cd.ba_index))[v]);
     int32_t o0 = offs[v], o1 = offs[v + 1];
     uint8_t *dst = pay + o0;
     uint32_t l = (uint32_t)(o1 - o0);
@@ -1962,35 +2350,36 @@ __global__ void __launch_bounds__(256) k_ba_gather(BatchDev b, const uint32_t *c
 // rep == 0 (ColumnStore.get data_store.go:285-308: a new record starts when
 // rl < maxR ... at rl == 0 for the top level). One workgroup per page.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_records(BatchDev b, const uint32_t *pages) {
+__global__ void __launch_bounds__(256) k_records(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc &pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
-  const uint8_t *rep = (const uint8_t *)cd.rep_levels + pd.slot_base;
-  int32_t *lo = (int32_t *)cd.list_offsets;
+  const uint8_t *rep = gp_u64<const uint8_t>(cd.rep_levels) + pd.slot_base;
+  int32_t *lo = gp_u64<int32_t>(cd.list_offsets);
   uint64_t rbase = b.page_rbase[pi];
   __shared__ uint32_t part[256];
   __shared__ uint64_t carry;
   if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
+  wg_barrier();
   for (uint32_t s0 = 0; s0 < pd.num_slots; s0 += 256 * 16) {
     uint32_t a = s0 + threadIdx.x * 16, e = min(a + 16, pd.num_slots);
     uint32_t c = 0;
     for (uint32_t s = a; s < e; s++) c += rep[s] == 0;
     part[threadIdx.x] = c;
-    __syncthreads();
+    wg_barrier();
     for (uint32_t d = 1; d < 256; d <<= 1) {
       uint32_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-      __syncthreads();
+      wg_barrier();
       part[threadIdx.x] += x;
-      __syncthreads();
+      wg_barrier();
     }
     uint64_t r = rbase + carry + part[threadIdx.x] - c;
     for (uint32_t s = a; s < e; s++)
       if (rep[s] == 0) lo[r++] = (int32_t)(pd.slot_base + s);
-    __syncthreads();
+    wg_barrier();
     if (threadIdx.x == 255) carry += part[255];
-    __syncthreads();
+    wg_barrier();
   }
   // last page of the chunk writes the terminating offset
   if (threadIdx.x == 0 && pd.page_in_chunk == cd.num_pages - 1) {

@@ -114,7 +114,7 @@ enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED =
 
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,
-                 WI_DELTA_TILE = 6 };
+                 WI_DELTA_TILE = 6, WI_DELTA_PAGE = 7 };
 
 // DELTA_BINARY_PACKED block table entry (one per block of a page), written by the header
 // walk (k_delta_walk), completed by the per-page scan of block sums (k_delta_prefix).
@@ -126,6 +126,12 @@ struct DeltaBlk {        // 32 B
   uint32_t pos;          // stream offset of the block's first miniblock payload byte
   uint32_t sum_lo;       // scratch: low half of the block's delta sum (k_delta_sums); unused
 };
+// DELTA_BINARY_PACKED page decoder (WI_DELTA_PAGE): the stream is staged through an LDS
+// window of kDeltaWinLoad bytes; a block (header + payload) must fit in it with 48 bytes of
+// slack (host check, else PF_DELTA_SLOW). At most kDeltaMaxBlk blocks are walked per window.
+constexpr uint32_t kDeltaWin = 16384;
+constexpr uint32_t kDeltaWinLoad = kDeltaWin + 128;
+constexpr uint32_t kDeltaMaxBlk = 256;
 struct WorkItem {        // 16 B
   uint32_t page;         // global page index
   uint32_t v0;           // first value (within page) of this tile

@@ -37,7 +37,7 @@ for k, nm in enumerate(["p3_mask", "p3_desc_scan", "p3_rle", "p3_owner_shfl", "p
 for k, nm in enumerate(["w_first", "w_fetch_issue", "w_walk", "w_bar1", "w_store", "w_bar2", "w_reloads#", "w_windows#"]):
     v = int(d[24 + k])
     print(f"dwalk  {nm:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
-dn = ["reload", "hdr_walk", "unpack", "scan", "write", "batches#", "end_barrier", "-"]
+dn = ["reload", "walk_wait", "unpack", "scan", "write", "hops#x4", "parse", "walk_w0"]
 for k, n in enumerate(dn):
     v = int(d[8 + k])
     print(f"delta  {n:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
