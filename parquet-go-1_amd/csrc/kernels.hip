@@ -181,6 +181,26 @@ DEV uint32_t wave_incl_scan32(uint32_t x) {
   x += dpp0<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
   return x;
 }
+// wave64 inclusive scan of 64-bit values (wrapping) with DPP row shifts / broadcasts
+DEV uint64_t wave_incl_scan64_dpp(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define PQ_SCAN_STEP(CTRL, ROWS)                                                  \
+  {                                                                               \
+    const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROWS, 0xf, false); \
+    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWS, 0xf, false); \
+    const uint64_t s = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2); \
+    lo = (uint32_t)s; hi = (uint32_t)(s >> 32);                                   \
+  }
+  PQ_SCAN_STEP(0x111, 0xf)
+  PQ_SCAN_STEP(0x112, 0xf)
+  PQ_SCAN_STEP(0x114, 0xf)
+  PQ_SCAN_STEP(0x118, 0xf)
+  PQ_SCAN_STEP(0x142, 0xa)
+  PQ_SCAN_STEP(0x143, 0xc)
+#undef PQ_SCAN_STEP
+  return ((uint64_t)hi << 32) | lo;
+}
+
 DEV uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -411,6 +431,7 @@ struct LevelSink {
   uint32_t count;        // lane-local count of (level == cmp)
   uint32_t err_code, err_pos;
   uint32_t stage_len;    // bytes held by the LDS stage passed to window()/piece()
+  uint32_t ablate;       // diagnostic build: BatchDev::ablate
 
   DEV static void or_bits(uint32_t *dst, uint64_t g, uint64_t m) {
     if (!m) return;
@@ -490,49 +511,58 @@ struct LevelSink {
 };
 
 // ---------------------------------------------------------------------------
-// Level decoder: one workgroup per page with level streams.
+// Level decoder: one 256-thread workgroup per page with level streams.
 //
 // A hybrid stream (hybrid_decoder.go:81-165) is a chain of run headers: the position
 // of run k+1 is known only once run k's header is decoded. The stream is processed in
-// chunks of kLvChunk candidate header positions (the chunk plus the bytes past its end
-// are staged in LDS):
-//  P1  every position is decoded as if a run header started there. A header varint of
-//      at most 4 bytes whose run is well formed and complete inside the stream is a
-//      link p -> p + adv carrying the run's value count; anything else (errors, runs cut
-//      by EOF, longer varints) is a stop: a self-link with no values.
-//  P1b kLvRounds pointer-doubling rounds in LDS turn the links into >= 8-run jumps that
-//      carry the sum of the runs' value counts (saturating).
-//  P2  one lane follows the true chain from the chunk's entry by jumps, recording a
-//      checkpoint (position, value index) per jump; stops are decoded exactly
-//      (decode_hdr) and recorded as one-run checkpoints. The walk also finds where the
-//      reference's loop ends: the run that reaches num_values, an error run, or a
-//      bit-packed run cut by EOF.
-//  P3  one lane per checkpoint re-walks its runs and expands them. Bit width 1
-//      with validity output only (flat OPTIONAL columns) ORs whole 32-bit words of
-//      payload into the LDS bitmap; other widths go through LevelSink::piece.
-// Results equal the reference's decodePackedArray loop exactly, including the error
-// class and the value position of the first error.
+// chunks of kLvChunk candidate header positions, staged in LDS with the bytes past the
+// chunk end, by parallel list ranking:
+//  P1  links: every position is decoded as if a run header started there (fast_hdr). A
+//      header varint of at most 4 bytes whose run is well formed and complete inside the
+//      stream links p -> p + adv (EXIT when that leaves the chunk); anything else (errors,
+//      runs cut by EOF, longer varints) is a stop: a self-link.
+//  P2  doubling: J[j+1][p] = J[j][J[j][p]] for j < kLvLevels (jumps of 2^j runs, saturating
+//      at a stop or the chunk exit); every level is kept.
+//  P3  one lane follows the true chain from the chunk entry by 2^kLvLevels-run jumps and
+//      marks each node it lands on.
+//  P4  marking, top down: for j = kLvLevels-1 .. 0 every marked node marks J[j][node]. A
+//      chain node at distance d from the entry is reached through the binary digits of d,
+//      so afterwards exactly the chain's nodes are marked (a lane that sees a mark set in
+//      the same round only marks further chain nodes early).
+//  P5  value indices: a workgroup prefix sum, in position order, of the marked runs'
+//      value counts; the chain's last node gives the next chunk's entry.
+//  P6  fill: every marked run is expanded by the thread that owns its position (bit
+//      width 1 with validity output only ORs whole 32-bit words of payload into the LDS
+//      bitmap; other widths go through LevelSink::piece); runs longer than kLvLongRun
+//      values are expanded by the whole workgroup.
+// A stop on the chain is decoded exactly (decode_hdr, the reference's full header
+// semantics): an error or a bit-packed run cut by EOF ends the stream; a valid run the
+// fast form could not take (a long varint) is expanded and the next chunk starts after it.
+// Runs past the one that reaches num_values are never read, as in the reference's
+// decodePackedArray loop; results, error class and error value position are identical.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLvThreads = 64;             // one wave per page: no cross-wave barriers
-constexpr uint32_t kLvChunk = 1024;             // candidate header positions per chunk
-constexpr uint32_t kLvRounds = 3;               // doubling rounds: a jump spans >= 8 runs
+constexpr uint32_t kLvThreads = 256;
+constexpr uint32_t kLvChunk = 2048;             // candidate header positions per chunk
+#ifndef PQ_LV_LEVELS
+#define PQ_LV_LEVELS 5
+#endif
+constexpr uint32_t kLvLevels = PQ_LV_LEVELS;    // J[kLvLevels] jumps 2^kLvLevels runs
+constexpr uint32_t kLvPer = kLvChunk / kLvThreads;  // positions per thread (contiguous in P5/P6)
 constexpr uint32_t kLvStageB = kLvChunk + 256;  // staged bytes: the chunk + headers / payload past its end
-constexpr uint32_t kLvMaxCk = kLvThreads;       // checkpoints per chunk (one fill lane each)
-constexpr uint32_t kLvMaxSlow = 32;             // exactly decoded runs per chunk
 constexpr uint32_t kLvLongRun = 512;            // runs longer than this expand cooperatively
 constexpr uint32_t kLvMaxLong = 64;
-constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint16_t kLvExit = 0xffff;
+constexpr uint32_t kNoEntry = 0xffffffffu;
 enum : uint32_t { LV_RUN = 0, LV_STOP_NEED = 1, LV_STOP_ERR = 2, LV_STOP_TRUNC = 3 };
 
 struct LevelLDS {
   uint32_t stage[kLvStageB / 4 + 4];
-  uint2 JV[kLvChunk];        // x: link / jump target of each position (>= chunk end: leaves the chunk)
-                             // y: values of the runs the jump passes (saturating at 2^31 - 1)
-  uint32_t ck_pos[kLvMaxCk + 1], ck_cum[kLvMaxCk], ck_slow[kLvMaxCk];
-  uint32_t slow_adv[kLvMaxSlow], slow_nv[kLvMaxSlow], slow_ok[kLvMaxSlow], slow_val[kLvMaxSlow],
-      slow_bp[kLvMaxSlow];
+  uint16_t J[kLvLevels + 1][kLvChunk];  // J[j][i]: chunk offset 2^j runs after i; i = stop; kLvExit
+  uint8_t mark[kLvChunk];
+  uint64_t wsum[kLvThreads / 64];
   uint32_t long_f[kLvMaxLong], long_cnt[kLvMaxLong], long_bp[kLvMaxLong], long_val[kLvMaxLong];
-  uint32_t nck, nlong, stop_kind, stop_code, stop_vpos, next_e, done_out;
+  uint32_t nlong, stop_kind, stop_code, stop_vpos, next_e;
+  unsigned long long done_out;
   uint64_t cnt[16];
   uint32_t bits[kSegSlots / 32];
 };
@@ -622,11 +652,11 @@ DEV void lv_emit_run(LevelSink &sk, const uint32_t *stg, uint32_t sb, uint32_t s
   }
 }
 
-// A run found by a fill lane: short runs expand right away, long ones are queued for the
-// workgroup (the fill lanes would otherwise wait on the one lane holding a long run).
+// A run of the fill: short runs expand right away, long ones are queued for the workgroup.
 template <bool BW1>
 DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uint32_t f, uint32_t cnt, uint32_t bp,
                      uint32_t value) {
+  if (PQ_ABLATE(sk, 2)) return;  // diagnostic: no expansion
   if (cnt > kLvLongRun && !(BW1 && !bp && value != sk.cmp)) {
     const uint32_t slot = atomicAdd(&L.nlong, 1u);
     if (slot < kLvMaxLong) {
@@ -639,132 +669,201 @@ DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uin
 }
 
 // Decode `need` level values of one stream into the sink; every thread of the workgroup
-// calls this (control flow outside per-lane work is workgroup-uniform).
+// calls this (control flow outside per-lane work is workgroup-uniform). Chunks are fixed
+// stream ranges [k * kLvChunk, (k + 1) * kLvChunk); the chain enters chunk k where it left
+// chunk k - 1 (chunks a long run jumps over are skipped). Thread t owns chunk positions
+// [8t, 8t + 8): their headers are decoded once (P1) and kept in registers for the fill.
 template <bool BW1>
 DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
+  static_assert(kLvPer == 8, "8 positions per thread");
   const uint8_t *s = sk.s;
   const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  uint32_t pos0 = 0, done = 0;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t i0 = tid * kLvPer;
+  constexpr uint32_t kWords = kLvStageB / 4 + 4, kWpt = (kWords + kLvThreads - 1) / kLvThreads;
+  uint32_t pre[kWpt];
+  auto fetch = [&](uint32_t cs) {
+    const uint8_t *src = s + cs;
+    const uint32_t lim = n > cs ? n - cs : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kWpt; j++) {
+      const uint32_t k = tid + j * kLvThreads, o = 4 * k;
+      pre[j] = (k < kWords && o < lim) ? (o + 4 <= lim ? ld32(src + o) : ld32(src + o) & ((1u << (8 * (lim - o))) - 1u)) : 0u;
+    }
+  };
+  uint32_t entry = 0, done = 0, fetched = 0;  // fetched: chunk start the registers hold
+  fetch(0);
   for (;;) {
     if (done >= need) break;
-    if (pos0 >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
-    const uint32_t cs = pos0, sb = cs & ~3u;
-    const uint32_t clen = min(kLvChunk, n - cs), cend = cs + clen, send = sb + kLvStageB;
-    wg_barrier();
+    if (entry >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
+    const uint32_t cs = entry - entry % kLvChunk, e0 = entry - cs;
+    const uint32_t clen = min(kLvChunk, n - cs), send = cs + kLvStageB;
+    if (fetched != cs) { fetch(cs); fetched = cs; }
+    wg_barrier();  // the previous chunk's stage readers are done
     st.lap(7);
-    stage_load_blk(L.stage, s, sb, n, kLvStageB / 4 + 4);
+#pragma unroll
+    for (uint32_t j = 0; j < kWpt; j++) {
+      const uint32_t k = tid + j * kLvThreads;
+      if (k < kWords) L.stage[k] = pre[j];
+    }
+    if (tid == 0) { L.nlong = 0; L.stop_kind = LV_RUN; L.next_e = kNoEntry; }
+    if (cs + kLvChunk < n) { fetch(cs + kLvChunk); fetched = cs + kLvChunk; }  // lands during this chunk
     wg_barrier();
     st.lap(0);
-    // ---- P1: links
-    for (uint32_t i = tid; i < clen; i += nt) {
-      const FastHdr f = fast_hdr(L.stage, sb, cs + i, n, bw, rs);
-      L.JV[i] = make_uint2(cs + i + f.adv, f.nvals);
+    // ---- P1: links of positions [i0, i0 + 8) from five staged words; headers kept in registers
+    uint32_t nv[kLvPer], val[kLvPer], bpm = 0, stopm = 0;
+    {
+      uint32_t W[5];
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) W[q] = L.stage[2 * tid + q];
+      uint32_t jj[kLvPer];
+#pragma unroll
+      for (uint32_t k = 0; k < kLvPer; k++) {
+        const uint32_t i = i0 + k, c = cs + i, a = k >> 2, sh = k & 3;
+        const uint32_t u0 = __builtin_amdgcn_alignbyte(W[a + 1], W[a], sh), u1 = __builtin_amdgcn_alignbyte(W[a + 2], W[a + 1], sh);
+        // fast_hdr on register bytes: varint of <= 4 bytes, well-formed run complete in the stream
+        const uint32_t t = ~u0 & 0x80808080u;
+        const uint32_t Lv = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+        uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
+        const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+        const uint32_t cnt = h >> 1, isbp = h & 1;
+        const uint64_t adv = isbp ? Lv + (uint64_t)cnt * bw : (uint64_t)(Lv + rs);
+        const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
+        const uint32_t rval = rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u));
+        const bool ok = i < clen && t != 0 && cnt != 0 && (uint64_t)c + adv <= n && (isbp || bw >= 32 || (rval >> bw) == 0);
+        nv[k] = ok ? (isbp ? cnt * 8 : cnt) : 0u;
+        val[k] = isbp ? c + Lv : rval;
+        bpm |= (ok && isbp) ? 1u << k : 0u;
+        stopm |= ok ? 0u : 1u << k;
+        jj[k] = !ok ? i : ((uint64_t)i + adv >= clen ? (uint32_t)kLvExit : i + (uint32_t)adv);
+      }
+      *(uint4 *)&L.J[0][i0] = make_uint4(jj[0] | (jj[1] << 16), jj[2] | (jj[3] << 16), jj[4] | (jj[5] << 16), jj[6] | (jj[7] << 16));
+      *(uint2 *)&L.mark[i0] = make_uint2(0u, 0u);
     }
     wg_barrier();
     st.lap(1);
-    // ---- P1b: pointer doubling, in place. A (target, values) pair is read and written as
-    // one 8-byte LDS access, so a pair another lane already advanced this round is still a
-    // consistent (longer) jump: after the rounds every jump spans at least 2^kLvRounds runs
-    // (or ends on a stop / past the chunk), which is all P2 and P3 rely on.
-    for (uint32_t r = 0; r < kLvRounds; r++) {
-      for (uint32_t i = tid; i < clen; i += nt) {
-        const uint2 a = L.JV[i];
-        if (a.x < cend) {
-          const uint2 c2 = L.JV[a.x - cs];
-          L.JV[i] = make_uint2(c2.x, min(a.y + c2.y, 0x7fffffffu));
-        }
+    // ---- P2: doubling (every level kept for the marking)
+    const uint32_t levels = PQ_ABLATE(sk, 3) ? 0u : kLvLevels;  // diagnostic: serial walk of every run
+    for (uint32_t lv = 0; lv < levels; lv++) {
+      const uint4 A = *(const uint4 *)&L.J[lv][i0];
+      const uint32_t a[8] = {A.x & 0xffffu, A.x >> 16, A.y & 0xffffu, A.y >> 16, A.z & 0xffffu, A.z >> 16, A.w & 0xffffu, A.w >> 16};
+      uint32_t r[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        const bool fix = a[k] == kLvExit || a[k] == i0 + k;
+        const uint32_t b2 = L.J[lv][fix ? i0 + k : a[k]];
+        r[k] = fix ? a[k] : b2;
       }
+      *(uint4 *)&L.J[lv + 1][i0] = make_uint4(r[0] | (r[1] << 16), r[2] | (r[3] << 16), r[4] | (r[5] << 16), r[6] | (r[7] << 16));
+      wg_barrier();
     }
-    wg_barrier();
     st.lap(2);
-    // ---- P2: the true chain by jumps (one lane)
+    // ---- P3: the chain by 2^levels-run jumps (one lane)
     if (tid == 0) {
-      __builtin_amdgcn_s_setprio(3);  // the serial walk is the page's critical path
-      uint32_t p = cs, cum = done, kind = LV_RUN, code = 0, vpos = 0, nck = 0, ns = 0;
+      __builtin_amdgcn_s_setprio(3);
+      uint32_t p = e0;
       for (;;) {
-        if (p >= cend) break;
-        if (nck == kLvMaxCk) break;  // checkpoint table full: the next chunk starts at p
-        const uint2 jv = L.JV[p - cs];
-        const uint32_t j = jv.x, v = jv.y;
-        L.ck_pos[nck] = p;
-        L.ck_cum[nck] = cum;
-        if (j != p) {  // a jump over fast runs (it may end on a stop)
-          L.ck_slow[nck++] = kNone;
-          if ((uint64_t)cum + v >= need) { kind = LV_STOP_NEED; break; }
-          cum += v;
-          p = j;
-          continue;
-        }
-        // p is a stop: the exact decoder (hybrid_decoder.go:142-165)
-        if (ns == kLvMaxSlow) break;  // slow table full: the next chunk starts at p
-        const Hdr h = decode_hdr(L.stage, sb, s, p, n, bw, rs);
-        L.slow_adv[ns] = h.adv; L.slow_nv[ns] = h.err ? 0 : h.nvals; L.slow_ok[ns] = h.err ? 0 : h.okvals;
-        L.slow_val[ns] = h.value; L.slow_bp[ns] = h.bp;
-        L.ck_slow[nck++] = ns++;
-        if (h.err) {
-          kind = LV_STOP_ERR; vpos = cum;
-          code = h.err == kErrLongVarint ? resolve_long_varint(s, p, n) : h.err;
-          break;
-        }
-        if (h.okvals < h.nvals && h.okvals < need - cum) {
-          kind = LV_STOP_TRUNC; vpos = cum + h.okvals; code = PQ_ERR_EOF;
-          break;
-        }
-        if (h.nvals >= need - cum) { kind = LV_STOP_NEED; break; }
-        cum += h.nvals;
-        p += h.adv;
+        L.mark[p] = 1;
+        const uint32_t q = L.J[levels][p];
+        if (q == kLvExit || q == p) break;
+        p = q;
       }
-      L.ck_pos[nck] = kind == LV_RUN ? p : kNone;  // walk bound of the last checkpoint
-      L.nck = nck; L.stop_kind = kind; L.stop_code = code; L.stop_vpos = vpos;
-      L.next_e = p; L.done_out = cum; L.nlong = 0;
       __builtin_amdgcn_s_setprio(0);
     }
     wg_barrier();
-    st.lap(3);
-    // ---- P3: one lane per checkpoint re-walks its runs and expands them
-    const uint32_t nck = L.nck;
-    for (uint32_t k = tid; k < nck; k += nt) {
-      uint32_t p = L.ck_pos[k], C = L.ck_cum[k];
-      const uint32_t sl = L.ck_slow[k];
-      if (sl != kNone) {
-        const uint32_t nvv = L.slow_nv[sl], ok = L.slow_ok[sl];
-        if (C < need) lv_fill_run<BW1>(L, sk, sb, send, C, min(min(nvv, ok), need - C), L.slow_bp[sl], L.slow_val[sl]);
-        continue;
-      }
-      const uint32_t bound = min(L.ck_pos[k + 1], cend);
-      // software-pipelined: the next run's header is read before this run expands
-      FastHdr f = p < bound ? fast_hdr(L.stage, sb, p, n, bw, rs) : FastHdr{0, 0, 0, 0};
-      while (f.adv && C < need) {  // !f.adv: a stop (the next checkpoint) or the bound
-        const uint32_t pn = p + f.adv;
-        const FastHdr fn = pn < bound ? fast_hdr(L.stage, sb, pn, n, bw, rs) : FastHdr{0, 0, 0, 0};
-        lv_fill_run<BW1>(L, sk, sb, send, C, min(f.nvals, need - C), f.bp, f.value);
-        C += f.nvals;
-        p = pn;
-        f = fn;
-      }
+    // ---- P4: marking, top down
+    for (int lv = (int)levels - 1; lv >= 0; lv--) {
+      const uint2 M = *(const uint2 *)&L.mark[i0];
+      const uint4 A = *(const uint4 *)&L.J[lv][i0];
+      const uint32_t a[8] = {A.x & 0xffffu, A.x >> 16, A.y & 0xffffu, A.y >> 16, A.z & 0xffffu, A.z >> 16, A.w & 0xffffu, A.w >> 16};
+      const uint64_t m = ((uint64_t)M.y << 32) | M.x;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++)
+        if (((m >> (8 * k)) & 0xffu) && a[k] != kLvExit) L.mark[a[k]] = 1;
+      wg_barrier();
     }
+    st.lap(3);
+    // ---- P5: value counts of this thread's marked runs, workgroup scan
+    uint32_t mbits = 0;
+    {
+      const uint2 M = *(const uint2 *)&L.mark[i0];
+      const uint64_t m = ((uint64_t)M.y << 32) | M.x;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) mbits |= ((m >> (8 * k)) & 0xffu) ? 1u << k : 0u;
+    }
+    Hdr sh{0, 0, 0, 0, 1, 0, 0};  // the chain's stop, when this thread owns it
+    uint32_t sk_k = 32;
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) mine += (mbits >> k) & 1u ? nv[k] : 0u;
+    if (mbits & stopm) {  // a stop on the chain: the exact decoder (hybrid_decoder.go:142-165)
+      sk_k = __builtin_ctz(mbits & stopm);
+      sh = decode_hdr(L.stage, cs, s, cs + i0 + sk_k, n, bw, rs);
+      mine += sh.err ? 0u : min(sh.nvals, sh.okvals);
+    }
+    const uint64_t incl = wave_incl_scan64_dpp(mine);
+    if (lane == 63) L.wsum[wv] = incl;
+    wg_barrier();
+    uint64_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kLvThreads / 64; q++) {
+      const uint64_t t = L.wsum[q];
+      before += q < wv ? t : 0ull;
+      total += t;
+    }
+    uint64_t v = (uint64_t)done + before + incl - mine;  // value index of this thread's first marked run
     st.lap(4);
+    // ---- P6: fill (and the chain's end: exit position or the exact stop)
+    while (mbits) {
+      const uint32_t k = __builtin_ctz(mbits);
+      mbits &= mbits - 1;
+      const uint32_t p = cs + i0 + k;
+      if (v >= need) break;  // runs past the one that reaches num_values are never read
+      const uint32_t rem = (uint32_t)min((uint64_t)need - v, (uint64_t)0xffffffffu);
+      if (k == sk_k) {  // the chain's stop
+        if (sh.err) {
+          L.stop_kind = LV_STOP_ERR; L.stop_vpos = (uint32_t)v;
+          L.stop_code = sh.err == kErrLongVarint ? resolve_long_varint(s, p, n) : sh.err;
+        } else {
+          const uint32_t ok = min(sh.nvals, sh.okvals);
+          lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(ok, rem), sh.bp, sh.value);
+          if (ok < sh.nvals && ok < rem) {
+            L.stop_kind = LV_STOP_TRUNC; L.stop_vpos = (uint32_t)v + ok; L.stop_code = PQ_ERR_EOF;
+          } else {
+            L.next_e = p + sh.adv;  // a valid run the fast form could not take: continue after it
+          }
+        }
+        break;
+      }
+      lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(nv[k], rem), (bpm >> k) & 1u, val[k]);
+      if (L.J[0][i0 + k] == kLvExit) L.next_e = p + fast_hdr(L.stage, cs, p, n, bw, rs).adv;  // the chain's last node
+      v += nv[k];
+    }
+    st.lap(5);
     wg_barrier();
     // long runs: every thread expands 32-value pieces (64 for the generic sink)
     const uint32_t nlong = L.nlong;
     for (uint32_t r = 0; r < nlong; r++) {
-      const uint32_t f = L.long_f[r], cnt = L.long_cnt[r], bp = L.long_bp[r], val = L.long_val[r];
+      const uint32_t f = L.long_f[r], cnt = L.long_cnt[r], bp = L.long_bp[r], lval = L.long_val[r];
       constexpr uint32_t P = BW1 ? 32 : 64;
-      for (uint32_t q = tid * P; q < cnt; q += nt * P) {
+      for (uint32_t q = tid * P; q < cnt; q += kLvThreads * P) {
         const uint32_t m = min(P, cnt - q);
-        if constexpr (BW1) lv_emit_run<true>(sk, L.stage, sb, send, f + q, m, bp, bp ? val + q / 8 : val);
-        else sk.piece(bp != 0, val, f + q, q, m, L.stage, sb);
+        if constexpr (BW1) lv_emit_run<true>(sk, L.stage, cs, send, f + q, m, bp, bp ? lval + q / 8 : lval);
+        else sk.piece(bp != 0, lval, f + q, q, m, L.stage, cs);
       }
     }
     if (nlong) wg_barrier();
-    st.lap(5);
-    if (L.stop_kind != LV_RUN) {
-      if (L.stop_kind != LV_STOP_NEED) sk.error(L.stop_vpos, L.stop_code);
+    st.lap(6);
+    const uint32_t kind = L.stop_kind;
+    const uint64_t ndone = (uint64_t)done + total;
+    if (kind != LV_RUN) {
+      if (kind == LV_STOP_ERR || kind == LV_STOP_TRUNC) sk.error(L.stop_vpos, L.stop_code);
       break;
     }
-    done = L.done_out;
-    pos0 = L.next_e;
+    if (ndone >= need) break;
+    done = (uint32_t)ndone;
+    entry = L.next_e;  // kNoEntry cannot happen: a chain that needs more values exits or stops
+    if (entry == kNoEntry) { sk.error(done, PQ_ERR_INVALID); break; }
   }
 }
 
@@ -802,6 +901,7 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b_in, const uint32_t *
     sk.err_code = 0;
     sk.err_pos = 0;
     sk.stage_len = kLvStageB;
+    sk.ablate = b.ablate;
     wg_barrier();
     if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
       if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
@@ -1812,26 +1912,6 @@ DEV uint32_t delta_blk_len_v(const uint32_t *win, int32_t win0, uint32_t pos, ui
   const uint32_t bl = __umul24(g8, __builtin_amdgcn_sad_u8(ww, 0u, 0u)) + L + mbc;
   const uint32_t ok = (uint32_t)(t != 0) & (uint32_t)(L + mbc <= 8);
   return sgpr(bl * ok);
-}
-
-// wave64 inclusive scan of 64-bit values (wrapping) with DPP row shifts / broadcasts
-DEV uint64_t wave_incl_scan64_dpp(uint64_t v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#define PQ_SCAN_STEP(CTRL, ROWS)                                                  \
-  {                                                                               \
-    const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROWS, 0xf, false); \
-    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWS, 0xf, false); \
-    const uint64_t s = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2); \
-    lo = (uint32_t)s; hi = (uint32_t)(s >> 32);                                   \
-  }
-  PQ_SCAN_STEP(0x111, 0xf)
-  PQ_SCAN_STEP(0x112, 0xf)
-  PQ_SCAN_STEP(0x114, 0xf)
-  PQ_SCAN_STEP(0x118, 0xf)
-  PQ_SCAN_STEP(0x142, 0xa)
-  PQ_SCAN_STEP(0x143, 0xc)
-#undef PQ_SCAN_STEP
-  return ((uint64_t)hi << 32) | lo;
 }
 
 DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
