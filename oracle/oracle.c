@@ -1354,8 +1354,12 @@ static int vdec_decode(vdec *v, int64_t nn, acc_t *a) {
         v->r.i += size;
         v->pos++;
         int64_t pl = v->prefix[v->pos - 1];
+        /* make([]byte, 0, prefixLen+len(suffix)) panics on a negative capacity (reported as
+           invalid); a negative prefix with a long enough suffix appends nothing of the
+           previous value (:224-235) */
+        if (pl + size < 0) return OR_ERR_INVALID;
         if (v->prevlen < pl) return OR_ERR_INVALID;
-        if (pl < 0) return OR_ERR_INVALID;
+        if (pl < 0) pl = 0;
         int64_t nl = pl + size;
         uint8_t *nv = (uint8_t *)malloc((size_t)(nl ? nl : 1));
         if (!nv) return OR_ERR_NOMEM;

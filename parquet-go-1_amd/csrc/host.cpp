@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <vector>
@@ -121,6 +122,79 @@ struct GoReader {
   }
 };
 
+// deltaBitPackDecoder32.init + decodeInt32 of all valuesCount values, as the DELTA_LENGTH /
+// DELTA_BYTE_ARRAY decoders run it at init (type_bytearray.go:104-115, :195-214;
+// deltabp_decoder.go:35-174; helpers.go:121-131) — structure only: block and miniblock
+// headers, group reads (io.ReadFull: EOF / ErrUnexpectedEOF), the look-ahead (Q1) and the
+// padding skip after the last group (Q2, skip errors ignored). The reader ends where the
+// next section starts. Groups between miniblock checks are consumed in one step.
+struct DeltaWalk { int64_t hdr; int32_t first, count, mbc, mbvc, bs; };
+int delta32_walk(GoReader &r, DeltaWalk *w, std::string *msg) {
+  int e;
+  int32_t bs, mbc, vc, f32;
+  if ((e = r.uvariant32(&bs))) { *msg = "failed to read block size"; return e; }
+  if ((e = r.uvariant32(&mbc))) { *msg = "failed to read number of mini blocks"; return e; }
+  if (mbc <= 0 || bs % mbc != 0) { *msg = "int/delta: invalid number of mini blocks"; return PQ_ERR_INVALID; }
+  const int32_t mbvc = bs / mbc;
+  if (mbvc == 0) { *msg = "invalid mini block value count, it can't be zero"; return PQ_ERR_INVALID; }
+  if ((e = r.uvariant32(&vc))) { *msg = "failed to read total value count"; return e; }
+  if ((e = r.variant32(&f32))) { *msg = "failed to read first value"; return e; }
+  if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
+  w->hdr = r.i; w->first = f32; w->count = vc; w->mbc = mbc; w->mbvc = mbvc; w->bs = bs;
+  uint8_t widths[256];
+  auto mb_header = [&]() -> int {
+    int32_t m32;
+    int er;
+    if ((er = r.variant32(&m32))) { *msg = "failed to read min delta"; return er; }
+    const int64_t ws = r.i;
+    if ((er = r.readfull(mbc))) { *msg = "not enough data to read all miniblock bit widths"; return er; }
+    for (int32_t k = 0; k < mbc; k++) {
+      widths[k] = r.p[ws + k];
+      if (widths[k] > 32) { *msg = "invalid miniblock bit width"; return PQ_ERR_INVALID; }
+    }
+    return PQ_OK;
+  };
+  if ((e = mb_header())) return e;
+  const int64_t l8 = (int64_t)std::lcm<int64_t>(8, mbvc);  // group starts where next() checks the miniblock
+  const int64_t last = vc > 0 ? ((int64_t)(vc - 1) / 8) * 8 : 0;  // start of the group holding value vc-1
+  int64_t pos = 0, cur_w = 0, mb_pos = 0;
+  int32_t cur_mb = 0;
+  while (pos < vc) {
+    if (pos % mbvc == 0) {
+      if (cur_mb >= mbc) {
+        if ((e = mb_header())) return e;
+        cur_mb = 0;
+      }
+      cur_w = widths[cur_mb];
+      mb_pos = 0;
+      cur_mb++;
+    }
+    int64_t g = 1;  // groups read before the next rule applies (a miniblock check or the last group)
+    if (pos < last) g = std::max<int64_t>(1, std::min((last - pos) / 8, ((pos / l8 + 1) * l8 - pos) / 8));
+    if (cur_w > 0) {
+      const int64_t avail = r.n - r.i, need = g * cur_w;
+      if (avail < need) {
+        const int64_t rem = avail - (avail / cur_w) * cur_w;  // bytes of the first group cut short
+        *msg = "delta lengths";
+        return rem == 0 ? PQ_ERR_EOF : PQ_ERR_UNEXPECTED_EOF;
+      }
+      r.i += need;
+      mb_pos += need;
+    }
+    if (pos + 8 * (g - 1) == last) {  // the last group: skip the padding (:149-164)
+      const int64_t l = (int64_t)(mbvc / 8) * cur_w - mb_pos;
+      if (l < 0) { *msg = "invalid stream"; return PQ_ERR_INVALID; }
+      r.i += std::min(l, r.n - r.i);
+      for (int32_t i = cur_mb; i < mbc; i++) {
+        const int64_t w2 = widths[cur_mb];  // sic: the reference indexes currentMiniBlock (Q2)
+        if (w2) r.i += std::min((int64_t)(mbvc / 8) * w2, r.n - r.i);
+      }
+    }
+    pos += 8 * g;
+  }
+  return PQ_OK;
+}
+
 struct HostChunk {
   pqgpu_column_info col{};
   pqgpu_chunk_meta meta{};
@@ -149,7 +223,7 @@ int pick_vkind(int32_t enc, int32_t type, int32_t type_length, uint8_t *vk, std:
     return PQ_ERR_UNSUPPORTED;
   };
   auto gpu_gap = [&]() {
-    *msg = "DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY are not implemented by the GPU decoder yet";
+    *msg = "DELTA_BYTE_ARRAY for FIXED_LEN_BYTE_ARRAY is not implemented by the GPU decoder yet";
     return PQ_ERR_UNSUPPORTED;
   };
   switch (type) {
@@ -159,7 +233,8 @@ int pick_vkind(int32_t enc, int32_t type, int32_t type_length, uint8_t *vk, std:
       return unsup("boolean");
     case T_BYTE_ARRAY:
       if (enc == ENC_PLAIN) { *vk = VK_PLAIN_BA; return PQ_OK; }
-      if (enc == ENC_DELTA_LENGTH_BYTE_ARRAY || enc == ENC_DELTA_BYTE_ARRAY) return gpu_gap();
+      if (enc == ENC_DELTA_LENGTH_BYTE_ARRAY) { *vk = VK_DLBA; return PQ_OK; }
+      if (enc == ENC_DELTA_BYTE_ARRAY) { *vk = VK_DBA; return PQ_OK; }
       if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
       return unsup("binary");
     case T_FLBA:
@@ -257,6 +332,9 @@ struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
   std::vector<HostChunk> chunks;
   std::vector<PageDesc> pages;
+  std::vector<BaDelta> ba_delta;          // DELTA_LENGTH / DELTA_BYTE_ARRAY pages (PageDesc::ba_delta)
+  std::vector<uint64_t> ba_delta_scratch; // arena offset of each entry's scratch
+  uint64_t o_ba_delta = 0;
   std::vector<uint8_t> stage;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
@@ -316,6 +394,7 @@ static int chunk_fail(pqgpu_batch *b, HostChunk &hc, int32_t id, int code, int p
   if (err) *err = hc.err;
   // drop the pages staged for this chunk: the reference returns before any readValues
   b->pages.resize(hc.first_page);
+  while (!b->ba_delta.empty() && b->ba_delta.back().page >= hc.first_page) b->ba_delta.pop_back();
   hc.num_pages = 0;
   return code;
 }
@@ -367,7 +446,7 @@ static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *
 }
 
 // Values decoder init() (reference: valuesDecoder.init called from page read()).
-static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_t vk, PageDesc *pd,
+static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_t vk, PageDesc *pd, BaDelta *bd,
                        std::string *msg) {
   GoReader r{page + vstart, plen - vstart};
   pd->val_off = (uint32_t)vstart;
@@ -390,6 +469,36 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     pd->dict_bw = 1;
     pd->val_off += 4;
     pd->val_len = (uint32_t)std::min<int64_t>(size, rem);
+    return PQ_OK;
+  }
+  if (vk == VK_DLBA || vk == VK_DBA) {  // byteArrayDeltaLengthDecoder / byteArrayDeltaDecoder init
+    *bd = BaDelta{};
+    int e;
+    auto stream = [&](BaDeltaStream *st, DeltaWalk *dw) {
+      const int64_t start = r.i;
+      GoReader rs{r.p + start, r.n - start};
+      int er = delta32_walk(rs, dw, msg);
+      st->off = (uint32_t)(vstart + start);
+      st->len = (uint32_t)(r.n - start);
+      st->hdr = (uint32_t)dw->hdr;
+      st->first = dw->first;
+      st->count = dw->count;
+      st->mbc = (uint16_t)dw->mbc;
+      st->mbvc = (uint32_t)dw->mbvc;
+      const uint64_t max_blk = 10 + (uint64_t)dw->mbc + (uint64_t)dw->bs * 4;
+      st->slow = (dw->mbvc % 8 == 0 && dw->mbc <= 8 && max_blk + 48 <= kDeltaWinLoad) ? 0 : 1;
+      r.i = start + rs.i;
+      return er;
+    };
+    DeltaWalk pw{}, sw{};
+    if (vk == VK_DBA && (e = stream(&bd->st[1], &pw))) return e;  // prefix lengths first (:195-201)
+    if ((e = stream(&bd->st[0], &sw))) return e;
+    if (vk == VK_DBA && pw.count != sw.count) {
+      *msg = "bytearray/delta: different number of suffixes and prefixes";
+      return PQ_ERR_INVALID;
+    }
+    bd->pay_off = (uint32_t)(vstart + r.i);
+    bd->pay_len = (uint32_t)(r.n - r.i);
     return PQ_OK;
   }
   if (vk == VK_DELTA32 || vk == VK_DELTA64) {  // deltaBitPackDecoder.init deltabp_decoder.go:35-111
@@ -517,6 +626,7 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
     int pi = (int)b->pages.size() - (int)hc.first_page;
     PageDesc pd;
     memset(&pd, 0, sizeof(pd));
+    BaDelta bd{};
     pd.chunk = (uint32_t)id;
     pd.page_in_chunk = (uint32_t)pi;
     block.clear();
@@ -557,7 +667,7 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         pd.flags |= PF_DEF;
         r.i += take;
       }
-      if ((e = init_values(block.data(), (int64_t)block.size(), r.i, vk, &pd, &msg)))
+      if ((e = init_values(block.data(), (int64_t)block.size(), r.i, vk, &pd, &bd, &msg)))
         return chunk_fail(b, hc, id, e, pi, msg, err);
     } else {
       // dataPageReaderV2.read page_v2.go:79-131
@@ -587,12 +697,17 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         pd.def_len = (uint32_t)ph.dph2.def_len;
         pd.flags |= PF_DEF;
       }
-      if ((e = init_values(block.data(), (int64_t)block.size(), levels, vk, &pd, &msg)))
+      if ((e = init_values(block.data(), (int64_t)block.size(), levels, vk, &pd, &bd, &msg)))
         return chunk_fail(b, hc, id, e, pi, msg, err);
     }
     if (hc.num_slots + pd.num_slots > 0x7fffffffULL)
       return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "more than 2^31-1 level slots in one chunk", err);
     pd.vkind = vk;
+    if (vk == VK_DLBA || vk == VK_DBA) {
+      bd.page = (uint32_t)b->pages.size();
+      pd.ba_delta = (uint32_t)b->ba_delta.size();
+      b->ba_delta.push_back(bd);
+    }
     pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
     pd.slot_base = hc.num_slots;
     hc.num_slots += pd.num_slots;
@@ -613,6 +728,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->items.clear();
   b->level_pages.clear();
   b->level_pages_bw1.clear();
+  b->ba_delta_scratch.assign(b->ba_delta.size(), 0);
   b->delta_pages.clear();
   b->dblk_base.assign(np, 0);
   b->dblk_total = 0;
@@ -713,6 +829,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         case VK_PLAIN_BA:
           if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_PLAIN_BA, {0, 0, 0}});
           break;
+        case VK_DLBA: case VK_DBA: {
+          BaDelta &bd = b->ba_delta[pd.ba_delta];
+          bd.cap = (uint32_t)std::min<int64_t>(std::max(bd.st[0].count, 0), (int64_t)ns_p);
+          b->ba_delta_scratch[pd.ba_delta] = take((uint64_t)bd.cap * 16);  // suffix, prefix, offset, ancestor
+          if (bd.cap) {
+            b->items.push_back(WorkItem{p, 0, bd.cap, WI_DLENS, {0, 0, 0}});
+            if (pd.vkind == VK_DBA) b->items.push_back(WorkItem{p, 1, bd.cap, WI_DLENS, {0, 0, 0}});
+          }
+          break;
+        }
       }
     }
   }
@@ -767,6 +893,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_tile_off = take(b->ba_tile_off.size() * 8);
   b->o_ba_totals = take(b->ba_chunks.size() * 8);
   b->o_dbg = take(64 * 8);
+  b->o_ba_delta = take(b->ba_delta.size() * sizeof(BaDelta));
   b->o_dblk = take(b->dblk_total * sizeof(DeltaBlk));
   b->o_dblk_sum = take(b->dblk_total * 8);
   b->o_dblk_base = take((uint64_t)np * 8);
@@ -850,6 +977,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     return hipMemcpyAsync(A + o, src, n, hipMemcpyHostToDevice, s);
   };
   HIPCHECK(up(b->o_pages, pages.data(), pages.size() * sizeof(PageDesc)), err);
+  std::vector<BaDelta> bad = b->ba_delta;
+  for (size_t k = 0; k < bad.size(); k++) bad[k].scratch = (uint64_t)(A + b->ba_delta_scratch[k]);
+  HIPCHECK(up(b->o_ba_delta, bad.data(), bad.size() * sizeof(BaDelta)), err);
   HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
   HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
   HIPCHECK(up(b->o_nn, b->page_nn_init.data(), np * 4), err);
@@ -896,6 +1026,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.spec = b->spec ? 1u : 0u;
   d.ablate = getenv("PQ_ABLATE") ? (uint32_t)atoi(getenv("PQ_ABLATE")) : 0u;
   d.page_rec = (uint32_t *)(A + b->o_rec);
+  d.ba_delta = (const BaDelta *)(A + b->o_ba_delta);
   d.page_vbase = (uint64_t *)(A + b->o_vbase);
   d.page_rbase = (uint64_t *)(A + b->o_rbase);
   d.runs = (HybRun *)(A + b->o_runs);
@@ -917,6 +1048,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_level_pages = (uint32_t)b->level_pages.size();
   l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
+  l.n_ba_delta = (uint32_t)b->ba_delta.size();
   l.scan_pages = (const uint32_t *)(A + b->l_scan);
   l.n_scan_pages = (uint32_t)b->scan_pages.size();
   l.base_chunks = (const uint32_t *)(A + b->l_base);
@@ -983,6 +1115,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 2, v, [&] { return launch_scan_runs(d, l, v); }), err);
     HIPCHECK(timed(b, 10, v, [&] { return launch_delta_prep(d, l, v); }), err);
     HIPCHECK(timed(b, 9, v, [&] { return launch_values(d, l, v); }), err);
+    HIPCHECK(launch_ba_delta(d, l, v), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
     HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
@@ -1001,6 +1134,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       // are dispatched first and the bandwidth-bound tiles fill the CUs around them
       HIPCHECK(timed(b, 9, s, [&] { return launch_values(d, l, s); }), err);
     }
+    HIPCHECK(launch_ba_delta(d, l, s), err);  // DELTA_LENGTH / DELTA_BYTE_ARRAY: lengths -> values
   }
   if (!b->ba_chunks.empty()) {
     HIPCHECK(timed(b, 5, s, [&] {
@@ -1049,6 +1183,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                  return launch_ba_gather_impl(d, (const uint32_t *)(A + b->l_ba), (uint32_t)gather.size(), gx, s);
                }),
                err);
+      HIPCHECK(launch_dba_gather(d, l, s), err);
     }
     HIPCHECK(hipStreamSynchronize(s), err);  // host vectors above stay valid until here
   }
@@ -1315,6 +1450,7 @@ int pqgpu_batch_reset(pqgpu_batch *b) {
   }
   b->chunks.clear();
   b->pages.clear();
+  b->ba_delta.clear();
   b->stage.clear();
   b->uploaded = b->decoded = false;
   b->force_serial = spec_disabled();

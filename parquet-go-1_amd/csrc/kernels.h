@@ -30,6 +30,7 @@ struct BatchDev {
   const uint64_t *dblk_base;      // [npages] first DeltaBlk of the page
   uint32_t *dblk_n;               // [npages] blocks the header walk produced
   unsigned long long *dblk_sum;   // [total blocks] sum of each block's deltas (wrapping)
+  const BaDelta *ba_delta;         // DELTA_LENGTH / DELTA_BYTE_ARRAY pages
   unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
   uint32_t spec;                  // 1: value bases came from the page headers (see k_bases)
@@ -43,6 +44,7 @@ constexpr uint32_t kBaTile = 4096;     // values per BYTE_ARRAY scan tile
 struct LaunchLists {
   const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams (generic)
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
+  uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
   const WorkItem *items; uint32_t n_items;               // values work items
@@ -61,6 +63,8 @@ hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s)
 hipError_t launch_ba_offsets(const BatchDev &b, const LaunchLists &l, uint64_t *payload_totals_dev, hipStream_t s);
 hipError_t launch_ba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
+hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // walk + sums + prefix
 
 // Names of the kernels, for the timing hook.

@@ -100,6 +100,7 @@ DEV BatchDev global_view(BatchDev b) {
   b.runs = gp(b.runs); b.run_base = gp(b.run_base); b.run_count = gp(b.run_count);
   b.tile_first = gp(b.tile_first); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
   b.dblk = gp(b.dblk); b.dblk_base = gp(b.dblk_base); b.dblk_n = gp(b.dblk_n); b.dblk_sum = gp(b.dblk_sum);
+  b.ba_delta = gp(b.ba_delta);
   if (b.dbg) b.dbg = gp(b.dbg);
   return b;
 }
@@ -1914,22 +1915,50 @@ DEV uint32_t delta_blk_len_v(const uint32_t *win, int32_t win0, uint32_t pos, ui
   return sgpr(bl * ok);
 }
 
-DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
-                       DeltaPageLDS &L) {
+// One DELTA_BINARY_PACKED stream to decode: an INT32/INT64 page's values section, or a
+// lengths stream of a DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (validated on the host).
+struct DeltaStream {
+  const uint8_t *s;      // stream bytes
+  uint32_t n;            // stream length
+  uint32_t hdr;          // first miniblock header, relative to s
+  int64_t first;         // first value (block header)
+  int32_t count;         // valuesCount (block header)
+  uint32_t mbc, mbvc;
+  bool is64;
+  uint8_t *out;          // value 0 of the output (int64 or int32 array)
+  uint32_t chunk, page;  // error reporting: chunk index and data-page index within it
+};
+
+DEV DeltaStream page_stream(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd) {
+  DeltaStream ds;
+  ds.s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
+  ds.n = pd.val_len;
+  ds.hdr = pd.delta_first_mb - pd.val_off;
+  ds.first = pd.delta_first;
+  ds.count = pd.delta_count;
+  ds.mbc = pd.delta_mbc;
+  ds.mbvc = pd.delta_mbvc;
+  ds.is64 = pd.vkind == VK_DELTA64;
+  ds.out = gp_u64<uint8_t>(cd.values) + b.page_vbase[wi.page] * (ds.is64 ? 8 : 4);
+  ds.chunk = pd.chunk;
+  ds.page = pd.page_in_chunk;
+  return ds;
+}
+
+DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, DeltaPageLDS &L) {
   if (nn == 0) return;
-  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
-  const uint32_t n = pd.val_len;
-  const bool is64 = pd.vkind == VK_DELTA64;
-  const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
+  const uint8_t *s = ds.s;
+  const uint32_t n = ds.n;
+  const bool is64 = ds.is64;
+  const uint32_t mbc = ds.mbc, mbvc = ds.mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const uint64_t vb = b.page_vbase[wi.page];
   uint32_t limit = nn;  // next() fails with io.EOF at positions >= the header's valuesCount
   bool final_eof = false;
-  if ((uint32_t)max(pd.delta_count, 0) < nn) { limit = (uint32_t)max(pd.delta_count, 0); final_eof = true; }
+  if ((uint32_t)max(ds.count, 0) < nn) { limit = (uint32_t)max(ds.count, 0); final_eof = true; }
   const uint32_t need = (uint32_t)(((uint64_t)limit + bs - 1) / bs);  // blocks holding deltas 0 .. limit-1
-  uint64_t carry = (uint64_t)pd.delta_first;
-  uint32_t hdr = pd.delta_first_mb - pd.val_off, blk = 0;
-  const bool al16 = is64 ? (vb & 1) == 0 : (vb & 3) == 0;  // 8 values of a group: 16-B aligned stores
+  uint64_t carry = (uint64_t)ds.first;
+  uint32_t hdr = ds.hdr, blk = 0;
+  const bool al16 = ((uintptr_t)ds.out & 15) == 0;  // 8 values of a group: 16-B aligned stores
   constexpr uint32_t kVec = (kDeltaWinLoad + 32 + 16 * 256 - 1) / (16 * 256);
   uint4 pre[kVec];
   auto fetch = [&](int32_t w0) {
@@ -2089,7 +2118,7 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
 #pragma unroll
       for (int q = 0; q < 8; q++) { out[q] = run; run += d[q]; }
       if (PQ_ABLATE(b, 0)) {  // diagnostic: no stores (kept live by an impossible condition)
-        if (out[7] == 0x0123456789abcdefull && valid) gp_u64<uint64_t>(cd.values)[vb + d0] = out[0];
+        if (out[7] == 0x0123456789abcdefull && valid) ((uint64_t *)ds.out)[d0] = out[0];
       } else if (__ballot(valid && d0 + 8 <= stop) == ~0ull) {
         // the wave's 64 groups are 512 consecutive values: transpose through LDS so that every
         // store instruction writes 1 KiB contiguous (16 B per lane) instead of 64 B-strided pieces
@@ -2106,7 +2135,7 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
         }
         asm volatile("" ::: "memory");  // same wave: LDS executes its accesses in order
         const uint32_t wd0 = rdlane(d0, 0);
-        uint8_t *dst0 = gp_u64<uint8_t>(cd.values) + (vb + wd0) * (is64 ? 8 : 4);
+        uint8_t *dst0 = ds.out + (uint64_t)wd0 * (is64 ? 8 : 4);
         if (al16) {
           uint4 *dst = (uint4 *)dst0;
           for (uint32_t q = 0; q < vw; q++) dst[q * 64 + lane] = xw[q * 64 + lane];
@@ -2126,13 +2155,13 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
       } else if (valid) {
         if (d0 + 8 <= stop && al16) {
           if (is64) {
-            uint4 *o4 = (uint4 *)(gp_u64<uint64_t>(cd.values) + vb + d0);
+            uint4 *o4 = (uint4 *)((uint64_t *)ds.out + d0);
 #pragma unroll
             for (int q = 0; q < 4; q++)
               o4[q] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
                                  (uint32_t)(out[2 * q + 1] >> 32));
           } else {
-            uint4 *o4 = (uint4 *)(gp_u64<uint32_t>(cd.values) + vb + d0);
+            uint4 *o4 = (uint4 *)((uint32_t *)ds.out + d0);
             o4[0] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
             o4[1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
           }
@@ -2140,8 +2169,8 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
 #pragma unroll
           for (int q = 0; q < 8; q++) {
             if (d0 + q < stop) {
-              if (is64) (gp_u64<uint64_t>(cd.values))[vb + d0 + q] = out[q];
-              else (gp_u64<uint32_t>(cd.values))[vb + d0 + q] = (uint32_t)out[q];
+              if (is64) ((uint64_t *)ds.out)[d0 + q] = out[q];
+              else ((uint32_t *)ds.out)[d0 + q] = (uint32_t)out[q];
             }
           }
         }
@@ -2150,7 +2179,7 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     }
     blk += nb;
     if (epos < limit) {  // the page fails at its first unreadable position
-      if (tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)epos, (uint32_t)(sk & 15));
+      if (tid == 0) report(b, ds.chunk, 1, ds.page, ST_VALUES, (uint32_t)epos, (uint32_t)(sk & 15));
       st.flush(8);
       return;
     }
@@ -2163,40 +2192,38 @@ DEV void do_delta_page(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
     st.lap(0);
   }
   st.flush(8);
-  if (final_eof && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, limit, PQ_ERR_EOF);
+  if (final_eof && tid == 0) report(b, ds.chunk, 1, ds.page, ST_VALUES, limit, PQ_ERR_EOF);
 }
 
 // Exact scalar restatement of deltaBitPackDecoder.next for pages whose miniblock
 // value count is not a multiple of 8 (deltabp_decoder.go:113-174).
-DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
-                       uint8_t *widths) {
+DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn, uint8_t *widths) {
   if (threadIdx.x != 0 || nn == 0) return;
-  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
-  const uint32_t n = pd.val_len;
-  const bool is64 = pd.vkind == VK_DELTA64;
-  const uint32_t mbc = pd.delta_mbc, mbvc = pd.delta_mbvc;
-  const uint64_t vb = b.page_vbase[wi.page];
-  uint32_t rpos = pd.delta_first_mb - pd.val_off;
+  const uint8_t *s = ds.s;
+  const uint32_t n = ds.n;
+  const bool is64 = ds.is64;
+  const uint32_t mbc = ds.mbc, mbvc = ds.mbvc;
+  uint32_t rpos = ds.hdr;
   int64_t md = 0;
   uint32_t hl, e = 0;
-  if (mbc > 256) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, 0, PQ_ERR_UNSUPPORTED); return; }
+  if (mbc > 256) { report(b, ds.chunk, 1, ds.page, ST_VALUES, 0, PQ_ERR_UNSUPPORTED); return; }
   // init(): the first miniblock header was validated on the host; re-read it here
   if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
-    report(b, pd.chunk, 0, 0, ST_VALUES, 0, e);
+    report(b, ds.chunk, 0, 0, ST_VALUES, 0, e);
     return;
   }
   rpos += hl;
   uint32_t cur_mb = 0, cur_w = 0, mb_pos = 0;  // mb_pos: miniBlockPosition (bytes read in the miniblock)
   int64_t mbv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t prev = (uint64_t)pd.delta_first;
-  const int32_t vcount = pd.delta_count;
+  uint64_t prev = (uint64_t)ds.first;
+  const int32_t vcount = ds.count;
   for (uint32_t pos = 0; pos < nn; pos++) {
-    if ((int32_t)pos >= vcount) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_EOF); return; }
+    if ((int32_t)pos >= vcount) { report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, PQ_ERR_EOF); return; }
     if (pos % 8 == 0) {
       if (pos % mbvc == 0) {
         if (cur_mb >= mbc) {
           if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
-            report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, e);
+            report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, e);
             return;
           }
           rpos += hl;
@@ -2206,8 +2233,8 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
         mb_pos = 0;
         cur_mb++;
       }
-      if (cur_w > 0 && rpos >= n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_EOF); return; }
-      if (rpos + cur_w > n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_UNEXPECTED_EOF); return; }
+      if (cur_w > 0 && rpos >= n) { report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, PQ_ERR_EOF); return; }
+      if (rpos + cur_w > n) { report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, PQ_ERR_UNEXPECTED_EOF); return; }
       for (int j = 0; j < 8; j++)
         mbv[j] = is64 ? (int64_t)bits64(s + rpos, (uint64_t)j * cur_w, cur_w)
                       : (int64_t)(int32_t)bits32(s + rpos, (uint64_t)j * cur_w, cur_w);
@@ -2217,15 +2244,15 @@ DEV void do_delta_slow(const BatchDev &b, const WorkItem &wi, const PageDesc &pd
       // follows an INT page), but a negative remainder — miniblocks of fewer than 8 values —
       // is "invalid stream"
       if ((int64_t)pos + 8 >= (int64_t)vcount && (int64_t)(mbvc / 8) * cur_w < (int64_t)mb_pos) {
-        report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, pos, PQ_ERR_INVALID);
+        report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, PQ_ERR_INVALID);
         return;
       }
     }
     uint64_t ret = prev;
     prev = prev + (uint64_t)mbv[pos % 8] + (uint64_t)md;
     if (!is64) prev = (uint64_t)(int64_t)(int32_t)(uint32_t)prev;
-    if (is64) (gp_u64<uint64_t>(cd.values))[vb + pos] = ret;
-    else (gp_u64<uint32_t>(cd.values))[vb + pos] = (uint32_t)ret;
+    if (is64) ((uint64_t *)ds.out)[pos] = ret;
+    else ((uint32_t *)ds.out)[pos] = (uint32_t)ret;
   }
 }
 
@@ -2266,10 +2293,29 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
     case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
-    case WI_DELTA: do_delta_slow(b, wi, pd, cd, nn, lds.slow_widths); break;
+    case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn, lds.slow_widths); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
-    case WI_DELTA_PAGE: do_delta_page(b, wi, pd, cd, nn, lds.dpage); break;
+    case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
     case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
+    case WI_DLENS: {  // a DELTA lengths stream of a DELTA_LENGTH / DELTA_BYTE_ARRAY page
+      const BaDelta &bd = b.ba_delta[pd.ba_delta];
+      const BaDeltaStream &st = bd.st[wi.v0];
+      DeltaStream ds;
+      ds.s = gp_u64<const uint8_t>(pd.data) + st.off;
+      ds.n = st.len;
+      ds.hdr = st.hdr;
+      ds.first = st.first;
+      ds.count = st.count;
+      ds.mbc = st.mbc;
+      ds.mbvc = st.mbvc;
+      ds.is64 = false;
+      ds.out = (uint8_t *)(gp_u64<int32_t>(bd.scratch) + (wi.v0 ? bd.cap : 0u));
+      ds.chunk = pd.chunk;
+      ds.page = pd.page_in_chunk;
+      if (st.slow) do_delta_slow(b, ds, wi.v1, lds.slow_widths);
+      else do_delta_page(b, ds, wi.v1, lds.dpage);
+      break;
+    }
   }
 }
 
@@ -2412,7 +2458,9 @@ __global__ void __launch_bounds__(256) k_ba_gather(BatchDev b_in, const uint32_t
   const int32_t *offs = gp_u64<const int32_t>(cd.offsets);
   uint8_t *pay = gp_u64<uint8_t>(cd.payload);
   for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (uint64_t)gridDim.x * 256) {
-    const uint8_t *src = gp_u64<const uint8_t>((gp_u64<const uint64_t>(cd.ba_index))[v]);
+    const uint64_t sa = (gp_u64<const uint64_t>(cd.ba_index))[v];
+    if (!sa) continue;  // DELTA_BYTE_ARRAY values: k_dba_gather
+    const uint8_t *src = gp_u64<const uint8_t>(sa);
     int32_t o0 = offs[v], o1 = offs[v + 1];
     uint8_t *dst = pay + o0;
     uint32_t l = (uint32_t)(o1 - o0);
@@ -2422,6 +2470,178 @@ __global__ void __launch_bounds__(256) k_ba_gather(BatchDev b_in, const uint32_t
       dst[k] = (uint8_t)x; dst[k + 1] = (uint8_t)(x >> 8); dst[k + 2] = (uint8_t)(x >> 16); dst[k + 3] = (uint8_t)(x >> 24);
     }
     for (; k < l; k++) dst[k] = src[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY values (type_bytearray.go:117-140, :216-240).
+// The lengths streams were decoded into the page's scratch by WI_DLENS items (k_values);
+// one workgroup per page turns them into value lengths (offsets[v+1], scanned later by the
+// BYTE_ARRAY offsets kernels) and sources (ba_index), and finds the first error the
+// reference's value loop meets:
+//   value i >= len(lens)                      -> io.EOF            (next(), :118-120)
+//   suffix length < 0                         -> invalid (Go: make() panics)
+//   io.ReadFull of the suffix                 -> EOF / ErrUnexpectedEOF (:123-125)
+//   DBA: prefix > length of value i-1         -> invalid (:227-230)
+//   DBA: prefix < 0 and prefix + suffix < 0   -> invalid (Go: make() panics); a negative prefix
+//        with a long enough suffix yields the suffix alone, as in the reference
+// DELTA_BYTE_ARRAY values share bytes with their predecessors: value i = value(i-1)[:p_i] +
+// suffix_i. Byte j < p_i of value i is byte j of the last earlier value whose suffix wrote it,
+// so each value is rebuilt from the chain of previous-smaller-prefix values (a_1 = the last
+// k < i with p_k < p_i, a_2 the same below a_1, ...: value a_t contributes [p_{a_t},
+// p_{a_(t-1)}) from its suffix). The links come from pointer jumping over the page's values
+// (k_ba_delta); k_dba_gather copies the pieces after the payload offsets are known.
+// ---------------------------------------------------------------------------
+DEV uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, uint64_t *total) {
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t incl = wave_incl_scan64_dpp(v);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+  for (uint32_t q = 0; q < nw; q++) {
+    const uint64_t t = wsum[q];
+    before += q < wv ? t : 0ull;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
+}
+
+__global__ void __launch_bounds__(256) k_ba_delta(BatchDev b_in) {
+  const BatchDev b = global_view(b_in);
+  __shared__ uint64_t wsum[4];
+  __shared__ unsigned long long ekey;
+  __shared__ uint32_t changed;
+  const BaDelta &bd = b.ba_delta[blockIdx.x];
+  const uint32_t pi = bd.page;
+  const PageDesc &pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const bool dba = pd.vkind == VK_DBA;
+  const uint32_t nn = b.page_nn_v[pi], cap = bd.cap, count = (uint32_t)max(bd.st[0].count, 0);
+  const uint64_t vb = b.page_vbase[pi];
+  int32_t *suf = gp_u64<int32_t>(bd.scratch), *pre = suf + cap, *anc = suf + 3 * (uint64_t)cap;
+  uint32_t *soff = (uint32_t *)(suf + 2 * (uint64_t)cap);
+  const uint8_t *pay = gp_u64<const uint8_t>(pd.data) + bd.pay_off;
+  const uint64_t plen = bd.pay_len;
+  int32_t *offs = gp_u64<int32_t>(cd.offsets);
+  uint64_t *srcs = gp_u64<uint64_t>(cd.ba_index);
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) ekey = ~0ull;
+  __syncthreads();
+  const uint32_t nv = min(nn, cap);  // values with a decoded length
+  constexpr uint32_t kPer = 8, kTile = 256 * kPer;
+  // ---- pass 1: the first error in value order
+  uint64_t carry = 0;
+  for (uint32_t t0 = 0; t0 < nn; t0 += kTile) {
+    const uint32_t i0 = t0 + tid * kPer;
+    uint64_t mine = 0;
+    for (uint32_t q = 0; q < kPer; q++) {
+      const uint32_t i = i0 + q;
+      if (i < nv) mine += (uint64_t)max(suf[i], 0);
+    }
+    uint64_t total;
+    uint64_t off = carry + block_excl_scan64(mine, wsum, &total);
+    carry += total;
+    unsigned long long key = ~0ull;
+    for (uint32_t q = 0; q < kPer && key == ~0ull; q++) {
+      const uint32_t i = i0 + q;
+      if (i >= nn) break;
+      if (i >= count) { key = ((unsigned long long)i << 4) | PQ_ERR_EOF; break; }
+      const int32_t sl = suf[i];
+      if (sl < 0) key = ((unsigned long long)i << 4) | PQ_ERR_INVALID;
+      else if (sl > 0 && off >= plen) key = ((unsigned long long)i << 4) | PQ_ERR_EOF;
+      else if (off + (uint64_t)sl > plen) key = ((unsigned long long)i << 4) | PQ_ERR_UNEXPECTED_EOF;
+      else if (dba) {
+        const int64_t prev = i == 0 ? 0 : (int64_t)max(pre[i - 1], 0) + suf[i - 1];
+        const int32_t p = pre[i];
+        if (prev < p || (p < 0 && (int64_t)p + sl < 0)) key = ((unsigned long long)i << 4) | PQ_ERR_INVALID;
+      }
+      off += (uint64_t)max(sl, 0);
+    }
+    if (key != ~0ull) atomicMin(&ekey, key);
+  }
+  __syncthreads();
+  const unsigned long long ek = ekey;
+  const uint32_t stop = ek == ~0ull ? nn : (uint32_t)min((uint64_t)nn, (uint64_t)(ek >> 4));
+  if (ek != ~0ull && tid == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)(ek >> 4), (uint32_t)(ek & 15));
+  // ---- pass 2: lengths and sources of the values before the error
+  carry = 0;
+  for (uint32_t t0 = 0; t0 < nn; t0 += kTile) {
+    const uint32_t i0 = t0 + tid * kPer;
+    uint64_t mine = 0;
+    for (uint32_t q = 0; q < kPer; q++) {
+      const uint32_t i = i0 + q;
+      if (i < stop) mine += (uint64_t)suf[i];
+    }
+    uint64_t total;
+    uint64_t off = carry + block_excl_scan64(mine, wsum, &total);
+    carry += total;
+    for (uint32_t q = 0; q < kPer; q++) {
+      const uint32_t i = i0 + q;
+      if (i >= nn) break;
+      if (i < stop) {
+        const int32_t sl = suf[i];
+        const uint32_t len = dba ? (uint32_t)(max(pre[i], 0) + sl) : (uint32_t)sl;
+        offs[vb + i + 1] = (int32_t)len;
+        srcs[vb + i] = dba ? 0ull : (uint64_t)(pay + off);
+        if (dba) soff[i] = (uint32_t)off;
+        off += (uint64_t)sl;
+      } else {
+        offs[vb + i + 1] = 0;
+        srcs[vb + i] = 0;
+      }
+    }
+  }
+  if (!dba) return;
+  // ---- pass 3 (DBA): previous-smaller-prefix links by pointer jumping
+  for (uint32_t i = tid; i < stop; i += blockDim.x) anc[i] = max(pre[i], 0) == 0 ? -1 : (int32_t)i - 1;
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) changed = 0;
+    __syncthreads();
+    uint32_t ch = 0;
+    for (uint32_t i = tid; i < stop; i += blockDim.x) {
+      const int32_t a = anc[i];
+      if (a >= 0 && max(pre[a], 0) >= max(pre[i], 0)) { anc[i] = anc[a]; ch = 1; }
+    }
+    if (ch) changed = 1;
+    __syncthreads();
+    if (!changed) break;
+  }
+}
+
+// DELTA_BYTE_ARRAY payload: one workgroup per page (chunks without a decode error).
+__global__ void __launch_bounds__(256) k_dba_gather(BatchDev b_in) {
+  const BatchDev b = global_view(b_in);
+  const BaDelta &bd = b.ba_delta[blockIdx.x];
+  const uint32_t pi = bd.page;
+  const PageDesc &pd = b.pages[pi];
+  if (pd.vkind != VK_DBA) return;
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  if (b.chunk_err[pd.chunk] != ~0ull || !cd.payload) return;
+  const uint32_t nn = min(b.page_nn_v[pi], bd.cap), cap = bd.cap;
+  const uint64_t vb = b.page_vbase[pi];
+  const int32_t *pre = gp_u64<const int32_t>(bd.scratch) + cap, *anc = pre + 2 * (uint64_t)cap;
+  const uint32_t *soff = (const uint32_t *)(pre + cap);
+  const uint8_t *pay = gp_u64<const uint8_t>(pd.data) + bd.pay_off;
+  const int32_t *offs = gp_u64<const int32_t>(cd.offsets);
+  uint8_t *out = gp_u64<uint8_t>(cd.payload);
+  for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) {
+    const int32_t o0 = offs[vb + i], o1 = offs[vb + i + 1];
+    uint8_t *dst = out + o0;
+    const uint32_t p = (uint32_t)max(pre[i], 0), len = (uint32_t)(o1 - o0);
+    const uint8_t *src = pay + soff[i];
+    for (uint32_t k = p; k < len; k++) dst[k] = src[k - p];
+    uint32_t hi = p;
+    int32_t a = anc[i];
+    while (hi > 0 && a >= 0) {
+      const uint32_t lo = (uint32_t)max(pre[a], 0);
+      const uint8_t *sa = pay + soff[a];
+      for (uint32_t k = lo; k < hi; k++) dst[k] = sa[k - lo];
+      hi = lo;
+      a = anc[a];
+    }
   }
 }
 
@@ -2503,6 +2723,16 @@ hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s)
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_delta_pages) return hipSuccess;
   hipLaunchKernelGGL(k_delta_walk, dim3(l.n_delta_pages), dim3(256), 0, s, b, l.delta_pages);
+  return hipGetLastError();
+}
+hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_ba_delta) return hipSuccess;
+  hipLaunchKernelGGL(k_ba_delta, dim3(l.n_ba_delta), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_ba_delta) return hipSuccess;
+  hipLaunchKernelGGL(k_dba_gather, dim3(l.n_ba_delta), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

@@ -33,6 +33,8 @@ enum : uint8_t {
   VK_DELTA32 = 5,      // DELTA_BINARY_PACKED INT32
   VK_DELTA64 = 6,      // DELTA_BINARY_PACKED INT64
   VK_PLAIN_BA = 7,     // BYTE_ARRAY PLAIN (length-prefixed)
+  VK_DLBA = 8,         // BYTE_ARRAY DELTA_LENGTH_BYTE_ARRAY: DELTA lengths + concatenated payload
+  VK_DBA = 9,          // BYTE_ARRAY DELTA_BYTE_ARRAY: DELTA prefix lengths + DLBA suffixes
 };
 
 // Page flags
@@ -78,7 +80,7 @@ struct PageDesc {        // 96 B
   uint16_t delta_mbc;    // DELTA: miniblocks per block
   uint16_t pad0;
   uint32_t delta_mbvc;   // DELTA: values per miniblock
-  uint32_t pad1;
+  uint32_t ba_delta;     // VK_DLBA / VK_DBA: index of the page's BaDelta entry
 };
 
 struct ChunkDesc {       // 192 B
@@ -114,7 +116,7 @@ enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED =
 
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,
-                 WI_DELTA_TILE = 6, WI_DELTA_PAGE = 7 };
+                 WI_DELTA_TILE = 6, WI_DELTA_PAGE = 7, WI_DLENS = 8 };
 
 // DELTA_BINARY_PACKED block table entry (one per block of a page), written by the header
 // walk (k_delta_walk), completed by the per-page scan of block sums (k_delta_prefix).
@@ -132,6 +134,26 @@ struct DeltaBlk {        // 32 B
 constexpr uint32_t kDeltaWin = 16384;
 constexpr uint32_t kDeltaWinLoad = kDeltaWin + 128;
 constexpr uint32_t kDeltaMaxBlk = 256;
+// DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (type_bytearray.go:98-240). The host walks
+// the DELTA lengths streams' headers at init (the reference decodes every length in init():
+// its errors and where the payload starts follow from the stream layout alone, SURVEY.md
+// App. A Q1/Q2); the GPU decodes the lengths (WI_DLENS) into scratch, then k_ba_delta turns
+// them into value lengths, sources and the reference's value errors.
+struct BaDeltaStream {   // a DELTA INT32 lengths stream
+  uint32_t off;          // stream start, relative to the page data
+  uint32_t len;          // bytes up to the end of the page data
+  uint32_t hdr;          // first miniblock header, relative to the stream start
+  int32_t first, count;  // first value, valuesCount
+  uint16_t mbc, slow;    // miniblocks per block; 1: exact scalar decode (shape outside the page kernel's)
+  uint32_t mbvc;
+};
+struct BaDelta {
+  BaDeltaStream st[2];   // [0] lengths (DLBA) / suffix lengths (DBA); [1] prefix lengths (DBA)
+  uint64_t scratch;      // device int32[3 * cap]: suffix lengths, prefix lengths, DBA ancestor links
+  uint32_t cap;          // lengths decoded per stream: min(count, num_values)
+  uint32_t pay_off, pay_len;  // payload (suffix bytes), relative to the page data
+  uint32_t page;         // global page index
+};
 struct WorkItem {        // 16 B
   uint32_t page;         // global page index
   uint32_t v0;           // first value (within page) of this tile

@@ -219,6 +219,33 @@ def edge_cases():
     return files
 
 
+def delta_ba():
+    """DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY columns as pyarrow writes them (lengths in
+    128-value blocks). Page non-null counts avoid N = 1 (mod 128) (App. A Q1)."""
+    rng = np.random.default_rng(21)
+    n = 12_000
+    w = words(rng, 2000)
+    keys = sorted(f"user/{int(i):08d}/" + w[int(i) % len(w)] for i in rng.integers(0, 10**7, n))
+    vals = [w[int(i)] for i in rng.integers(0, len(w), n)]
+    m = rng.random(n) < 0.1
+    page_rows = 3000
+    pages = m.reshape(-1, page_rows)
+    for p in np.flatnonzero((page_rows - pages.sum(1)) % 128 == 1):
+        pages[p, np.flatnonzero(pages[p])[0]] = False
+    files = {}
+    t = pa.table({"s": pa.array(vals, mask=m), "k": pa.array(keys)})
+    files["dlba_v1"] = write(t, use_dictionary=False, data_page_version="1.0", compression="NONE",
+                             column_encoding={"s": "DELTA_LENGTH_BYTE_ARRAY", "k": "DELTA_LENGTH_BYTE_ARRAY"},
+                             max_rows_per_page=page_rows)
+    files["dba_v2"] = write(t, use_dictionary=False, data_page_version="2.0", compression="NONE",
+                            column_encoding={"s": "DELTA_BYTE_ARRAY", "k": "DELTA_BYTE_ARRAY"},
+                            max_rows_per_page=page_rows)
+    files["dba_v1_snappy"] = write(t, use_dictionary=False, data_page_version="1.0", compression="SNAPPY",
+                                   column_encoding={"s": "DELTA_BYTE_ARRAY", "k": "DELTA_LENGTH_BYTE_ARRAY"},
+                                   max_rows_per_page=page_rows)
+    return files
+
+
 def pqinspect_uvar_bytes(x):
     out = bytearray()
     while True:
@@ -304,6 +331,7 @@ def main():
         "types_dict": types_dict(),
     }
     files.update(edge_cases())
+    files.update(delta_ba())
     files.update(corrupt(files))
     manifest = {}
     for name, data in sorted(files.items()):

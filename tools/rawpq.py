@@ -141,8 +141,8 @@ def delta_encode(vals, bs=128, mbc=4, bits=64, trailing_width=0, min_delta_overr
 
 # ---------------------------------------------------------------- file framing
 
-TYPES = {"INT32": 1, "INT64": 2, "DOUBLE": 5}
-ENC = {"PLAIN": 0, "RLE": 3, "DELTA_BINARY_PACKED": 5}
+TYPES = {"INT32": 1, "INT64": 2, "DOUBLE": 5, "BYTE_ARRAY": 6}
+ENC = {"PLAIN": 0, "RLE": 3, "DELTA_BINARY_PACKED": 5, "DELTA_LENGTH_BYTE_ARRAY": 6, "DELTA_BYTE_ARRAY": 7}
 
 
 def page_v1(values_bytes, num_values, encoding, def_bytes=b""):
@@ -210,3 +210,34 @@ def random_walk(rng, n, step_bits, signed=True):
     lo = -(1 << (step_bits - 1)) if signed else 0
     d = rng.integers(lo, 1 << (step_bits - 1), n, dtype=np.int64)
     return [int(x) for x in np.cumsum(d)]
+
+
+def dlba_stream(lens, payload, bs=128, mbc=4, **kw):
+    """DELTA_LENGTH_BYTE_ARRAY values section: DELTA INT32 lengths, then the bytes."""
+    return delta_encode(list(lens), bs, mbc, 32, **kw) + bytes(payload)
+
+
+def dba_stream(prefixes, suffix_lens, payload, bs=128, mbc=4, **kw):
+    """DELTA_BYTE_ARRAY values section: DELTA prefix lengths, DELTA suffix lengths, suffix bytes."""
+    return delta_encode(list(prefixes), bs, mbc, 32, **kw) + delta_encode(list(suffix_lens), bs, mbc, 32, **kw) + bytes(payload)
+
+
+def dba_encode(values):
+    """(prefix lengths, suffix lengths, suffix bytes) of a list of bytes values."""
+    pre, sl, pay, prev = [], [], bytearray(), b""
+    for v in values:
+        k = 0
+        while k < min(len(v), len(prev)) and v[k] == prev[k]:
+            k += 1
+        pre.append(k)
+        sl.append(len(v) - k)
+        pay += v[k:]
+        prev = v
+    return pre, sl, bytes(pay)
+
+
+def ba_column_file(pages, encoding, v2=False):
+    """A one-column REQUIRED BYTE_ARRAY file: pages = [(values section bytes, num_values)]."""
+    ps = [page_v2(st, n, 0, n, encoding) if v2 else page_v1(st, n, encoding) for st, n in pages]
+    n = sum(k for _, k in pages)
+    return write_file([("s", "BYTE_ARRAY", False)], [(n, [ps], [n])])
