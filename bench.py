@@ -261,6 +261,8 @@ def kernel_bytes(b, name, st):
         return int(st.values_kernel_bytes)
     if name == "k_levels":
         return int(st.levels_kernel_bytes)
+    if name == "k_snappy":
+        return int(st.snappy_kernel_bytes)
     return None
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 1
+#define PQGPU_ABI_VERSION 2
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -130,10 +130,12 @@ typedef struct {
   int64_t output_bytes;      /* values + levels + validity + offsets + payload materialised */
   int64_t staged_bytes;      /* bytes resident in HBM as the decoder's input */
   double host_plan_ms;       /* page-header walk + descriptor build (host) */
-  double host_decompress_ms; /* SNAPPY/GZIP on host threads */
+  double host_decompress_ms; /* GZIP (and PQ_HOST_SNAPPY=1 SNAPPY) pages on the host */
   int64_t levels_kernel_bytes; /* algorithmic bytes of k_levels: level sections + validity/levels written */
   int64_t values_kernel_bytes; /* algorithmic bytes of k_values: value sections + values/offsets written */
   int64_t delta_kernel_bytes;  /* the DELTA_BINARY_PACKED pages' share of values_kernel_bytes */
+  int64_t snappy_pages;        /* SNAPPY data pages decompressed on the device (k_snappy) */
+  int64_t snappy_kernel_bytes; /* algorithmic bytes of k_snappy: blocks + raw level bytes read, pages written */
 } pqgpu_batch_stats;
 
 /* ---- version / device ---------------------------------------------- */
@@ -218,7 +220,7 @@ int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
 int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
 /* The same for every timed launch slot (0 <= slot < PQGPU_TIMER_SLOTS); PQ_ERR_ARG past the end. */
-#define PQGPU_TIMER_SLOTS 11
+#define PQGPU_TIMER_SLOTS 12
 int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
                             size_t name_len);
 

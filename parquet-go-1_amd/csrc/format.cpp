@@ -358,15 +358,11 @@ bool SnappyDecodedLen(const uint8_t *src, int64_t n, int64_t *len) {
   return false;
 }
 
-// Raw snappy block (golang/snappy decode.go semantics: any inconsistency is ErrCorrupt).
-Status SnappyDecode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t dst_cap, int64_t *dst_len) {
-  int64_t dlen, s = 0;
-  if (!SnappyDecodedLen(src, n, &dlen)) return Status::Err(PQ_ERR_DECOMPRESS, "snappy: corrupt input");
-  while (s < n && (src[s] & 0x80)) s++;
-  s++;
-  if (dlen > dst_cap) return Status::Err(PQ_ERR_DECOMPRESS, "snappy: output too large");
-  int64_t d = 0;
-  while (s < n) {
+// Raw snappy block elements (golang/snappy v0.0.1 decode_other.go:20-96 semantics: any
+// inconsistency is ErrCorrupt), resumable so the planner can decode just a page's head.
+bool SnappyPrefix::Extend(int64_t want) {
+  if (want > dlen) want = dlen;
+  while (d < want && s < n) {
     uint8_t tag = src[s];
     int64_t length, offset;
     if ((tag & 3) == 0) {
@@ -374,35 +370,35 @@ Status SnappyDecode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t dst_cap
       if (x < 60) s += 1;
       else {
         int nb = (int)x - 59;
-        if (s + 1 + nb > n) goto corrupt;
+        if (s + 1 + nb > n) return false;
         x = 0;
         for (int k = 0; k < nb; k++) x |= (uint32_t)src[s + 1 + k] << (8 * k);
         s += 1 + nb;
       }
       length = (int64_t)x + 1;
-      if (length > dlen - d || length > n - s) goto corrupt;
+      if (length > dlen - d || length > n - s) return false;
       memcpy(dst + d, src + s, (size_t)length);
       d += length;
       s += length;
       continue;
     }
     if ((tag & 3) == 1) {
-      if (s + 2 > n) goto corrupt;
+      if (s + 2 > n) return false;
       length = 4 + ((tag >> 2) & 7);
       offset = ((int64_t)(tag & 0xe0) << 3) | src[s + 1];
       s += 2;
     } else if ((tag & 3) == 2) {
-      if (s + 3 > n) goto corrupt;
+      if (s + 3 > n) return false;
       length = 1 + (tag >> 2);
       offset = src[s + 1] | ((int64_t)src[s + 2] << 8);
       s += 3;
     } else {
-      if (s + 5 > n) goto corrupt;
+      if (s + 5 > n) return false;
       length = 1 + (tag >> 2);
       offset = src[s + 1] | ((int64_t)src[s + 2] << 8) | ((int64_t)src[s + 3] << 16) | ((int64_t)src[s + 4] << 24);
       s += 5;
     }
-    if (offset <= 0 || d < offset || length > dlen - d) goto corrupt;
+    if (offset <= 0 || d < offset || length > dlen - d) return false;
     if (offset >= length) {
       memcpy(dst + d, dst + d - offset, (size_t)length);
     } else {
@@ -410,11 +406,28 @@ Status SnappyDecode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t dst_cap
     }
     d += length;
   }
-  if (d != dlen) goto corrupt;
-  *dst_len = dlen;
+  return true;
+}
+
+bool SnappyPrefix::Init(const uint8_t *block, int64_t len, uint8_t *out, int64_t cap) {
+  if (!SnappyDecodedLen(block, len, &dlen)) return false;
+  int64_t v = 0;
+  while (v < len && (block[v] & 0x80)) v++;
+  v++;
+  src = block + v;
+  n = len - v;
+  s = d = 0;
+  dst = out;
+  return dlen <= cap;
+}
+
+Status SnappyDecode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t dst_cap, int64_t *dst_len) {
+  SnappyPrefix sp;
+  if (!sp.Init(src, n, dst, dst_cap)) return Status::Err(PQ_ERR_DECOMPRESS, "snappy: corrupt input");
+  // trailing elements after the last byte would each overflow dst: corrupt
+  if (!sp.Extend(sp.dlen) || sp.s != sp.n || sp.d != sp.dlen) return Status::Err(PQ_ERR_DECOMPRESS, "snappy: corrupt input");
+  *dst_len = sp.dlen;
   return Status::Ok();
-corrupt:
-  return Status::Err(PQ_ERR_DECOMPRESS, "snappy: corrupt input");
 }
 
 static Status gzip_decode(const uint8_t *src, int64_t n, std::vector<uint8_t> *out) {

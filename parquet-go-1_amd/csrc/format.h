@@ -96,5 +96,17 @@ Status OpenFile(const uint8_t *buf, int64_t len, FileMeta *out);
 Status Decompress(int32_t codec, const uint8_t *src, int64_t n, std::vector<uint8_t> *out);
 Status SnappyDecode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t dst_cap, int64_t *dst_len);
 bool SnappyDecodedLen(const uint8_t *src, int64_t n, int64_t *len);
+// Resumable decode of a raw snappy block's leading bytes: the planner reads page headers,
+// level lengths and value-decoder headers from them while the device decompresses the page.
+struct SnappyPrefix {
+  const uint8_t *src = nullptr;  // elements (after the length preamble)
+  int64_t n = 0, s = 0;          // element bytes, next element
+  uint8_t *dst = nullptr;
+  int64_t dlen = 0, d = 0;       // decoded length (preamble), bytes decoded so far
+  // Parse the preamble; false if it is corrupt or dlen > cap.
+  bool Init(const uint8_t *block, int64_t len, uint8_t *out, int64_t cap);
+  // Decode whole elements until d >= want (or the end of the elements). false: corrupt.
+  bool Extend(int64_t want);
+};
 
 }  // namespace pq

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -326,7 +327,7 @@ struct KernelTimer {
 };
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_dict_ba", "k_ba_offsets",
-    "k_ba_gather", "k_records", "k_values[other]", "k_values", "k_delta_prep"};
+    "k_ba_gather", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy"};
 
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
@@ -336,6 +337,19 @@ struct pqgpu_batch {
   std::vector<uint64_t> ba_delta_scratch; // arena offset of each entry's scratch
   uint64_t o_ba_delta = 0;
   std::vector<uint8_t> stage;
+  // SNAPPY data pages decompressed on the device by k_snappy (default; PQ_HOST_SNAPPY=1
+  // decompresses them on the host like GZIP). Pages carry PF_DEV_SNAPPY and `data` = job index
+  // until upload, which places their output in a region after the stage.
+  struct DevSnappy {
+    uint64_t comp_off, raw_off;  // stage offsets: the block (then >= 128 zero bytes), the raw prefix
+    uint32_t comp_len, vlen;     // block bytes, preamble bytes
+    uint32_t raw_len, dlen;      // V2 level bytes, decoded length
+    uint32_t page;               // global page index
+  };
+  bool dev_snappy = !(getenv("PQ_HOST_SNAPPY") && atoi(getenv("PQ_HOST_SNAPPY")) != 0);
+  std::vector<DevSnappy> snappy;
+  std::vector<uint8_t> pagebuf;  // the planner's copy of a device-decompressed page's head
+  uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
   std::vector<uint32_t> delta_pages;      // tiled DELTA pages
@@ -390,11 +404,26 @@ struct pqgpu_batch {
 // ---------------------------------------------------------------------------
 static int chunk_fail(pqgpu_batch *b, HostChunk &hc, int32_t id, int code, int page, const std::string &msg,
                       pqgpu_error *err) {
-  set_err(&hc.err, code, id, page, msg);
+  // SNAPPY blocks staged for the device were read (readPages order) before this failure: the
+  // reference decompresses each as it reads it, so the first corrupt one is the chunk's error.
+  // Error path only: the full host decode here decides which error the reference reports.
+  std::string m = msg;
+  for (const auto &j : b->snappy) {
+    if (j.page < hc.first_page) continue;
+    std::vector<uint8_t> tmp;
+    if (!Decompress(1, b->stage.data() + j.comp_off, j.comp_len, &tmp).ok() || tmp.size() != j.dlen) {
+      code = PQ_ERR_DECOMPRESS;
+      page = (int)(j.page - hc.first_page);
+      m = "decompression failed: snappy: corrupt input";
+      break;
+    }
+  }
+  set_err(&hc.err, code, id, page, m);
   if (err) *err = hc.err;
   // drop the pages staged for this chunk: the reference returns before any readValues
   b->pages.resize(hc.first_page);
   while (!b->ba_delta.empty() && b->ba_delta.back().page >= hc.first_page) b->ba_delta.pop_back();
+  while (!b->snappy.empty() && b->snappy.back().page >= hc.first_page) b->snappy.pop_back();
   hc.num_pages = 0;
   return code;
 }
@@ -406,10 +435,16 @@ static uint64_t stage_append(pqgpu_batch *b, const uint8_t *src, int64_t n) {
   return off;
 }
 
+// A SNAPPY block left for k_snappy (read_block with `defer`): where it is and its decoded length.
+struct SnappyDefer { const uint8_t *blk = nullptr; int64_t len = 0, dlen = 0; };
+
 // readPageBlock (chunk_reader.go:161-180) + newBlockReader (compress.go:102-123) for a whole block.
+// With `defer` a SNAPPY block whose preamble gives the expected size is not decompressed here
+// (k_snappy does it; a corrupt body is found there); anything else decodes on the host, whose
+// error is the reference's.
 static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *count, int32_t csize, int32_t usize,
                       int validate_crc, const PageHeader &ph, int32_t codec, std::vector<uint8_t> *out,
-                      int64_t skip_levels, std::string *msg) {
+                      int64_t skip_levels, std::string *msg, SnappyDefer *defer = nullptr) {
   if (csize < 0 || usize < 0) { *msg = "invalid page data size"; return PQ_ERR_INVALID; }
   int64_t avail = *off >= flen ? 0 : flen - *off;
   int64_t take = std::min<int64_t>(csize, avail);
@@ -434,6 +469,15 @@ static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *
     *msg = "compressed data must be " + std::to_string(csize) + " byte but its " + std::to_string(take) + " byte";
     return PQ_ERR_INVALID;
   }
+  if (defer && codec == 1) {
+    int64_t dlen;
+    if (SnappyDecodedLen(blk, take, &dlen) && dlen == usize && (int64_t)out->size() + dlen < (1ll << 31)) {
+      defer->blk = blk;
+      defer->len = take;
+      defer->dlen = dlen;
+      return PQ_OK;
+    }
+  }
   size_t before = out->size();
   Status st = Decompress(codec, blk, take, out);
   if (!st.ok()) { *msg = st.msg; return st.code; }
@@ -446,12 +490,16 @@ static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *
 }
 
 // Values decoder init() (reference: valuesDecoder.init called from page read()).
+// `ensure(k)`: page bytes [0, k) are readable (a device-decompressed page holds only its head
+// on the host); false if the block is corrupt there.
 static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_t vk, PageDesc *pd, BaDelta *bd,
-                       std::string *msg) {
+                       std::string *msg, const std::function<bool(int64_t)> &ensure) {
   GoReader r{page + vstart, plen - vstart};
+  auto corrupt = [&] { *msg = "decompression failed: snappy: corrupt input"; return PQ_ERR_DECOMPRESS; };
   pd->val_off = (uint32_t)vstart;
   pd->val_len = (uint32_t)(plen - vstart);
   if (vk == VK_DICT) {  // dictDecoder.init type_dict.go:22-38
+    if (!ensure(vstart + 1)) return corrupt();
     if (r.i >= r.n) { *msg = "EOF"; return PQ_ERR_EOF; }
     uint8_t w = r.p[0];
     if (w > 32) { *msg = "invalid bitwidth " + std::to_string(w); return PQ_ERR_INVALID; }
@@ -461,6 +509,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     return PQ_OK;
   }
   if (vk == VK_RLE_BOOL) {  // booleanRLEDecoder.init type_boolean.go:104-107 (hybrid initSize)
+    if (!ensure(vstart + 4)) return corrupt();
     int e = r.readfull(4);
     if (e) { *msg = "boolean rle size"; return e; }
     uint32_t size;
@@ -472,6 +521,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     return PQ_OK;
   }
   if (vk == VK_DLBA || vk == VK_DBA) {  // byteArrayDeltaLengthDecoder / byteArrayDeltaDecoder init
+    if (!ensure(plen)) return corrupt();
     *bd = BaDelta{};
     int e;
     auto stream = [&](BaDeltaStream *st, DeltaWalk *dw) {
@@ -505,6 +555,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
     bool is64 = vk == VK_DELTA64;
     int32_t bs, mbc, vc;
     int e;
+    if (!ensure(vstart + 64)) return corrupt();  // five varints at most 50 bytes
     if ((e = r.uvariant32(&bs))) { *msg = "failed to read block size"; return e; }
     if ((e = r.uvariant32(&mbc))) { *msg = "failed to read number of mini blocks"; return e; }
     if (mbc <= 0 || bs % mbc != 0) { *msg = "int/delta: invalid number of mini blocks"; return PQ_ERR_INVALID; }
@@ -528,6 +579,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
       if ((e = r.variant32(&m32))) { *msg = "failed to read min delta"; return e; }
     }
     int64_t wstart = r.i;
+    if (!ensure(vstart + wstart + std::max(mbc, 0))) return corrupt();
     if ((e = r.readfull(mbc))) { *msg = "not enough data to read all miniblock bit widths"; return e; }
     for (int32_t k = 0; k < mbc; k++)
       if (r.p[wstart + k] > (is64 ? 64 : 32)) { *msg = "invalid miniblock bit width"; return PQ_ERR_INVALID; }
@@ -631,6 +683,48 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
     pd.page_in_chunk = (uint32_t)pi;
     block.clear();
     uint8_t vk = 0;
+    // SNAPPY data pages go to k_snappy unless their values decoder reads the whole page at
+    // init (DELTA_LENGTH / DELTA_BYTE_ARRAY walk every length on the host)
+    SnappyDefer sd;
+    SnappyPrefix sp;
+    bool can_defer = false;
+    if (b->dev_snappy && meta->codec == 1 && (ph.type == 0 ? ph.has_dph : ph.has_dph2)) {
+      uint8_t vk_peek = 0;
+      std::string ignored;
+      can_defer = pick_vkind(ph.type == 0 ? ph.dph.encoding : ph.dph2.encoding, col->physical_type, col->type_length,
+                             &vk_peek, &ignored) == PQ_OK &&
+                  vk_peek != VK_DLBA && vk_peek != VK_DBA;
+    }
+    // the page bytes the planner reads: the host-decoded block, or (deferred) the raw prefix
+    // plus the decoded head in pagebuf, extended on demand
+    const uint8_t *pg = nullptr;
+    int64_t plen = 0, raw_len = 0;
+    auto bind_page = [&]() {
+      if (!sd.blk) { pg = block.data(); plen = (int64_t)block.size(); return; }
+      raw_len = (int64_t)block.size();
+      plen = raw_len + sd.dlen;
+      if ((int64_t)b->pagebuf.size() < plen + 64) b->pagebuf.resize((size_t)plen + 64);
+      if (raw_len) memcpy(b->pagebuf.data(), block.data(), (size_t)raw_len);
+      sp.Init(sd.blk, sd.len, b->pagebuf.data() + raw_len, sd.dlen);
+      pg = b->pagebuf.data();
+    };
+    auto ensure = [&](int64_t upto) -> bool { return !sd.blk || upto <= raw_len || sp.Extend(upto - raw_len); };
+    // stage the raw prefix and the block now: a later failure in this chunk checks the block
+    auto stage_snappy = [&]() {
+      pqgpu_batch::DevSnappy j;
+      j.raw_off = stage_append(b, block.data(), (int64_t)block.size());
+      j.raw_len = (uint32_t)block.size();
+      j.comp_off = stage_append(b, sd.blk, sd.len);
+      j.comp_len = (uint32_t)sd.len;
+      j.vlen = (uint32_t)(sp.src - sd.blk);
+      j.dlen = (uint32_t)sd.dlen;
+      j.page = (uint32_t)b->pages.size();
+      b->stage.resize(b->stage.size() + 128, 0);  // k_snappy reads up to 70 bytes past the block
+      b->snappy.push_back(j);
+    };
+    auto corrupt_fail = [&]() {
+      return chunk_fail(b, hc, id, PQ_ERR_DECOMPRESS, pi, "decompression failed: snappy: corrupt input", err);
+    };
     if (ph.type == 0) {
       // dataPageReaderV1.init page_v1.go:65-85 then read :87-122
       if (!ph.has_dph) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "page header is missing data page header", err);
@@ -640,17 +734,21 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "encoding is not supported for definition and repetition level", err);
       if (ph.dph.num_values < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "negative NumValues in DATA_PAGE", err);
       auto d0 = std::chrono::steady_clock::now();
-      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg);
+      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg,
+                         can_defer ? &sd : nullptr);
+      if (!e) bind_page();
       decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
       if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
+      if (sd.blk) stage_snappy();
       if ((e = pick_vkind(ph.dph.encoding, col->physical_type, col->type_length, &vk, &msg)))
         return chunk_fail(b, hc, id, e, pi, msg, err);
       pd.num_slots = (uint32_t)ph.dph.num_values;
-      GoReader r{block.data(), (int64_t)block.size()};
+      GoReader r{pg, plen};
       if (max_rep > 0) {  // hybridDecoder.initSize: u32 length, LimitReader, ReadAll (buffered)
+        if (!ensure(r.i + 4)) return corrupt_fail();
         if ((e = r.readfull(4))) return chunk_fail(b, hc, id, e, pi, "read repetition level size", err);
         uint32_t sz;
-        memcpy(&sz, block.data() + r.i - 4, 4);
+        memcpy(&sz, pg + r.i - 4, 4);
         int64_t take = std::min<int64_t>(sz, r.n - r.i);
         pd.rep_off = (uint32_t)r.i;
         pd.rep_len = (uint32_t)take;
@@ -658,17 +756,17 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         r.i += take;
       }
       if (max_def > 0) {
+        if (!ensure(r.i + 4)) return corrupt_fail();
         if ((e = r.readfull(4))) return chunk_fail(b, hc, id, e, pi, "read definition level size", err);
         uint32_t sz;
-        memcpy(&sz, block.data() + r.i - 4, 4);
+        memcpy(&sz, pg + r.i - 4, 4);
         int64_t take = std::min<int64_t>(sz, r.n - r.i);
         pd.def_off = (uint32_t)r.i;
         pd.def_len = (uint32_t)take;
         pd.flags |= PF_DEF;
         r.i += take;
       }
-      if ((e = init_values(block.data(), (int64_t)block.size(), r.i, vk, &pd, &bd, &msg)))
-        return chunk_fail(b, hc, id, e, pi, msg, err);
+      if ((e = init_values(pg, plen, r.i, vk, &pd, &bd, &msg, ensure))) return chunk_fail(b, hc, id, e, pi, msg, err);
     } else {
       // dataPageReaderV2.read page_v2.go:79-131
       if (!ph.has_dph2) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "null DataPageHeaderV2", err);
@@ -680,9 +778,12 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         return chunk_fail(b, hc, id, e, pi, msg, err);
       int64_t levels = (int64_t)ph.dph2.rep_len + ph.dph2.def_len;
       auto d0 = std::chrono::steady_clock::now();
-      e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, levels, &msg);
+      e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, levels, &msg,
+                     can_defer ? &sd : nullptr);
+      if (!e) bind_page();
       decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
       if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
+      if (sd.blk) stage_snappy();
       pd.num_slots = (uint32_t)ph.dph2.num_values;
       pd.flags |= PF_V2;
       if (ph.dph2.num_nulls >= 0 && ph.dph2.num_nulls <= ph.dph2.num_values) {
@@ -697,8 +798,7 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
         pd.def_len = (uint32_t)ph.dph2.def_len;
         pd.flags |= PF_DEF;
       }
-      if ((e = init_values(block.data(), (int64_t)block.size(), levels, vk, &pd, &bd, &msg)))
-        return chunk_fail(b, hc, id, e, pi, msg, err);
+      if ((e = init_values(pg, plen, levels, vk, &pd, &bd, &msg, ensure))) return chunk_fail(b, hc, id, e, pi, msg, err);
     }
     if (hc.num_slots + pd.num_slots > 0x7fffffffULL)
       return chunk_fail(b, hc, id, PQ_ERR_UNSUPPORTED, pi, "more than 2^31-1 level slots in one chunk", err);
@@ -708,7 +808,12 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       pd.ba_delta = (uint32_t)b->ba_delta.size();
       b->ba_delta.push_back(bd);
     }
-    pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
+    if (sd.blk) {  // staged by stage_snappy(); k_snappy writes the page
+      pd.flags |= PF_DEV_SNAPPY;
+      pd.data = b->snappy.size() - 1;  // job index until upload
+    } else {
+      pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
+    }
     pd.slot_base = hc.num_slots;
     hc.num_slots += pd.num_slots;
     b->pages.push_back(pd);
@@ -894,6 +999,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_totals = take(b->ba_chunks.size() * 8);
   b->o_dbg = take(64 * 8);
   b->o_ba_delta = take(b->ba_delta.size() * sizeof(BaDelta));
+  b->o_snappy = take(b->snappy.size() * sizeof(SnappyJob));
   b->o_dblk = take(b->dblk_total * sizeof(DeltaBlk));
   b->o_dblk_sum = take(b->dblk_total * 8);
   b->o_dblk_base = take((uint64_t)np * 8);
@@ -914,14 +1020,23 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMalloc(&b->d_arena, a), err);
     b->d_arena_cap = a;
   }
-  // stage: pinned host copy + device buffer (64 B zero pad)
+  // stage: pinned host copy + device buffer (64 B zero pad); after it, the pages k_snappy
+  // writes (each 256-B aligned, followed by 64 zero bytes like every staged section)
   size_t ssz = align_up(b->stage.size(), 16) + 64;
-  if (ssz > b->d_stage_cap) {
+  const uint64_t dec_base = align_up(ssz, 256);
+  std::vector<uint64_t> dec_off(b->snappy.size());
+  uint64_t dec = 0;
+  for (size_t k = 0; k < b->snappy.size(); k++) {
+    dec_off[k] = dec;
+    dec = align_up(dec + align_up((uint64_t)b->snappy[k].raw_len + b->snappy[k].dlen, 16) + 64, 256);
+  }
+  const size_t dsz = (size_t)(dec_base + dec);
+  if (dsz > b->d_stage_cap) {
     if (b->d_stage) (void)hipFree(b->d_stage);
     b->d_stage = nullptr;
     b->d_stage_cap = 0;
-    HIPCHECK(hipMalloc(&b->d_stage, ssz), err);
-    b->d_stage_cap = ssz;
+    HIPCHECK(hipMalloc(&b->d_stage, dsz), err);
+    b->d_stage_cap = dsz;
   }
   if (ssz > b->h_pinned_cap) {
     if (b->h_pinned) (void)hipHostFree(b->h_pinned);
@@ -970,8 +1085,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.offsets = hc.o_offsets ? dp(hc.o_offsets) : 0;
     cd.ba_index = hc.o_ba_index ? dp(hc.o_ba_index) : 0;
   }
+  std::vector<SnappyJob> jobs(b->snappy.size());
+  for (size_t k = 0; k < jobs.size(); k++) {
+    const pqgpu_batch::DevSnappy &j = b->snappy[k];
+    const PageDesc &pd = b->pages[j.page];
+    jobs[k] = SnappyJob{(uint64_t)(b->d_stage + j.comp_off + j.vlen), (uint64_t)(b->d_stage + j.raw_off),
+                        (uint64_t)(b->d_stage + dec_base + dec_off[k]), j.comp_len - j.vlen, j.raw_len, j.dlen,
+                        pd.chunk, pd.page_in_chunk, 0};
+  }
   std::vector<PageDesc> pages = b->pages;
-  for (auto &pd : pages) pd.data = (uint64_t)(b->d_stage + pd.data);
+  for (auto &pd : pages) pd.data = (pd.flags & PF_DEV_SNAPPY) ? jobs[pd.data].dst : (uint64_t)(b->d_stage + pd.data);
+  HIPCHECK(hipMemcpyAsync(A + b->o_snappy, jobs.data(), jobs.size() * sizeof(SnappyJob), hipMemcpyHostToDevice, s), err);
   auto up = [&](uint64_t o, const void *src, size_t n) -> hipError_t {
     if (!n) return hipSuccess;
     return hipMemcpyAsync(A + o, src, n, hipMemcpyHostToDevice, s);
@@ -1006,6 +1130,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->stats.num_pages = np;
   b->stats.input_bytes = in_bytes;
   b->stats.staged_bytes = (int64_t)b->stage.size();
+  b->stats.snappy_pages = (int64_t)b->snappy.size();
+  b->stats.snappy_kernel_bytes = 0;
+  for (const auto &j : b->snappy) b->stats.snappy_kernel_bytes += (int64_t)j.comp_len + 2 * (int64_t)j.raw_len + j.dlen;
   b->uploaded = true;
   return PQ_OK;
 }
@@ -1097,6 +1224,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(hipMemsetAsync(A + b->f_begin, 0xff, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
+  // SNAPPY pages first: every later kernel reads page data
+  HIPCHECK(timed(b, 11, s, [&] {
+             return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy), (uint32_t)b->snappy.size(), s);
+           }),
+           err);
   // DELTA work items and the other value work items go out as two launches (separately profiled).
   LaunchLists l1 = l, l2 = l;
   l1.n_items = b->n_delta_items;
@@ -1201,7 +1333,9 @@ static void decode_key(uint64_t key, int chunk, pqgpu_error *e) {
   uint32_t code = (uint32_t)(key & 15);
   static const char *stages[] = {"dictionary", "repetition levels", "definition levels", "values"};
   char msg[200];
-  if (phase == 0) {
+  if (phase == 0 && stage == ST_DECOMP) {  // k_snappy: the page's readPages failure
+    set_err(e, (int)code, chunk, (int)page, "decompression failed: snappy: corrupt input");
+  } else if (phase == 0) {
     snprintf(msg, sizeof(msg), "%s decode failed at entry %u: %s", stages[stage & 3], pos, pqgpu_status_string((int)code));
     set_err(e, (int)code, chunk, -1, msg);
   } else {
@@ -1451,6 +1585,7 @@ int pqgpu_batch_reset(pqgpu_batch *b) {
   b->chunks.clear();
   b->pages.clear();
   b->ba_delta.clear();
+  b->snappy.clear();
   b->stage.clear();
   b->uploaded = b->decoded = false;
   b->force_serial = spec_disabled();

@@ -65,6 +65,7 @@ hipError_t launch_ba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
+hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // walk + sums + prefix
 
 // Names of the kernels, for the timing hook.

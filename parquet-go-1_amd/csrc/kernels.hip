@@ -2689,8 +2689,161 @@ __global__ void __launch_bounds__(256) k_records(BatchDev b_in, const uint32_t *
 }
 
 // ---------------------------------------------------------------------------
+// k_snappy: a SNAPPY data page's raw block -> the page data, one wave per page
+// (golang/snappy v0.0.1 decode_other.go / decode_amd64.s: any inconsistency is ErrCorrupt,
+// which the reference reports as the page's readPages failure, compress.go:102-123).
+//
+// The element chain is walked 64 stream bytes at a time: every lane decodes the element that
+// would start at its byte, the chain is followed lane to lane with readlane, then the chain's
+// elements execute in order. Output goes through an LDS ring holding the most recent
+// kSnappyRing page bytes (copy sources: both encoders keep offsets below 64 KiB, most below
+// the ring) and is flushed to HBM in 16-B aligned pieces; copies reaching past the ring read
+// the flushed output with L1-bypassing loads.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRingMask = kSnappyRing - 1;
+
+struct SnappyOut {
+  uint8_t *ring;      // LDS, 16-B aligned
+  uint8_t *dst;       // page data (global, 16-B aligned)
+  uint32_t flushed;   // page bytes [0, flushed) are in dst; a multiple of 16
+};
+
+DEV void snappy_flush(SnappyOut &o, uint32_t upto) {  // ring[flushed, upto) -> dst, upto % 16 == 0
+  for (uint32_t x = o.flushed + lane_id() * 16; x < upto; x += 64 * 16)
+    *(uint4 *)(o.dst + x) = *(const uint4 *)(o.ring + (x & kRingMask));
+  o.flushed = upto;
+}
+// make room for page bytes [P, P + k) in the ring (k <= kSnappyRing - 16)
+DEV void snappy_room(SnappyOut &o, uint32_t P, uint32_t k) {
+  if (P + k - o.flushed > kSnappyRing) snappy_flush(o, P & ~15u);
+}
+
+// Global bytes S[0, len) -> page bytes [P, P + len), len <= kSnappyRing / 2. Whole ring words
+// are assembled from two aligned dword loads (S's 4-B aligned floor is readable and the
+// source is followed by zero padding); the partial words at either end go byte by byte.
+DEV void snappy_put(SnappyOut &o, const uint8_t *S, uint32_t P, uint32_t len) {
+  snappy_room(o, P, len);
+  const uint32_t w1 = (P + len + 3) >> 2;
+#pragma unroll 4
+  for (uint32_t w = (P >> 2) + lane_id(); w < w1; w += 64) {
+    const uint32_t lo = max(w * 4, P), hi = min(w * 4 + 4, P + len);
+    if (hi - lo == 4) {
+      const uint8_t *a = S + (lo - P);
+      const uint32_t sh = (uint32_t)(uintptr_t)a & 3;
+      const uint32_t *al = (const uint32_t *)(a - sh);
+      *(uint32_t *)(o.ring + ((w * 4) & kRingMask)) = __builtin_amdgcn_alignbyte(al[1], al[0], sh);
+    } else {
+      for (uint32_t x = lo; x < hi; x++) o.ring[x & kRingMask] = S[x - P];
+    }
+  }
+}
+
+// Page bytes [P - off, ...) -> [P, P + len), len <= 64, 1 <= off <= P (overlap repeats the
+// pattern: byte i comes from P - off + i % off).
+DEV void snappy_copy(SnappyOut &o, uint32_t P, uint32_t off, uint32_t len) {
+  snappy_room(o, P, 64);
+  const uint32_t i = lane_id();
+  uint32_t m = i;
+  if (off < len) m = i - off * (uint32_t)(((float)i + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+  const uint32_t q = P - off + m;
+  uint32_t v = 0;
+  if (off <= kSnappyRing) {
+    if (i < len) v = o.ring[q & kRingMask];
+  } else {  // flushed long ago (flushed >= P + 64 - kSnappyRing > q): read HBM, bypassing L1
+    __builtin_amdgcn_s_waitcnt(0);
+    if (i < len) {
+      const uint32_t *wp = (const uint32_t *)(o.dst + (q & ~3u));
+      v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (q & 3));
+    }
+  }
+  if (i < len) o.ring[(P + i) & kRingMask] = (uint8_t)v;
+}
+
+__global__ void __launch_bounds__(64) k_snappy(BatchDev b_in, const SnappyJob *jobs) {
+  const BatchDev b = global_view(b_in);
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
+  const SnappyJob &jb = gp(jobs)[blockIdx.x];
+  const uint8_t *src = gp_u64<const uint8_t>(jb.src);
+  const uint32_t n = sgpr(jb.src_len), raw = sgpr(jb.raw_len), dlen = sgpr(jb.dlen);
+  const uint32_t lane = lane_id();
+  SnappyOut o{ring, gp_u64<uint8_t>(jb.dst), 0};
+  for (uint32_t k = 0; k < raw; k += kSnappyRing / 2)  // V2: the uncompressed level sections first
+    snappy_put(o, gp_u64<const uint8_t>(jb.raw) + k, k, min(raw - k, kSnappyRing / 2));
+  uint32_t pos = 0, op = 0;  // stream position, decoded bytes
+  bool bad = false;
+  while (pos < n) {
+    // the element that would start at pos + lane: tag, header bytes, literal length - 1 or
+    // copy offset, copy length (decode_other.go:20-96)
+    const uint8_t *a = src + pos + lane;
+    const uint32_t sh = (uint32_t)(uintptr_t)a & 3;
+    const uint32_t *al = (const uint32_t *)(a - sh);
+    const uint32_t d0 = al[0], d1 = al[1];
+    const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, sh), b4 = (d1 >> (8 * sh)) & 0xff;
+    const uint32_t tag = w & 0xff, x = tag >> 2, t = tag & 3;
+    uint32_t hdr, val, clen = 0;
+    if (t == 0) {
+      hdr = x < 60 ? 1 : x - 58;
+      val = x < 60 ? x : x == 60 ? (w >> 8) & 0xff : x == 61 ? (w >> 8) & 0xffff : x == 62 ? (w >> 8) & 0xffffff
+                                                                                          : (w >> 8) | (b4 << 24);
+    } else if (t == 1) {
+      hdr = 2; clen = 4 + (x & 7); val = ((tag & 0xe0) << 3) | ((w >> 8) & 0xff);
+    } else if (t == 2) {
+      hdr = 3; clen = 1 + x; val = (w >> 8) & 0xffff;
+    } else {
+      hdr = 5; clen = 1 + x; val = (w >> 8) | (b4 << 24);
+    }
+    // stream bytes of the element (saturated: a literal that long fails its bounds check)
+    const uint32_t esz = t == 0 ? (uint32_t)min<uint64_t>((uint64_t)hdr + val + 1, 0x7fffffffu) : hdr;
+    uint64_t chain = 0;
+    uint32_t cur = 0;
+    while (cur < 64 && pos + cur < n) {
+      chain |= 1ull << cur;
+      cur += (uint32_t)__builtin_amdgcn_readlane((int)esz, (int)cur);
+    }
+    while (chain) {
+      const uint32_t e = (uint32_t)__builtin_ctzll(chain);
+      chain &= chain - 1;
+      const uint32_t et = (uint32_t)__builtin_amdgcn_readlane((int)t, (int)e);
+      const uint32_t eh = (uint32_t)__builtin_amdgcn_readlane((int)hdr, (int)e);
+      const uint32_t ev = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)e);
+      const uint32_t s = pos + e + eh;  // first byte after the header
+      if (s > n) { bad = true; break; }
+      if (et == 0) {
+        const uint64_t len = (uint64_t)ev + 1;
+        if (len > dlen - op || len > n - s) { bad = true; break; }
+        for (uint32_t k = 0; k < (uint32_t)len; k += kSnappyRing / 2)
+          snappy_put(o, src + s + k, raw + op + k, min((uint32_t)len - k, kSnappyRing / 2));
+        op += (uint32_t)len;
+      } else {
+        const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)clen, (int)e);
+        if (ev == 0 || op < ev || el > dlen - op) { bad = true; break; }
+        snappy_copy(o, raw + op, ev, el);
+        op += el;
+      }
+    }
+    if (bad) break;
+    pos += cur;
+  }
+  if (bad || op != dlen) {
+    if (lane == 0) report(b, jb.chunk, 0, jb.page_in_chunk, ST_DECOMP, 0, PQ_ERR_DECOMPRESS);
+    return;
+  }
+  // last piece: zeros past the page end, then the 64 B zero pad every page section carries
+  const uint32_t end = raw + dlen, end16 = (end + 15) & ~15u;
+  snappy_room(o, end, 16);
+  if (end + lane < end16) o.ring[(end + lane) & kRingMask] = 0;
+  snappy_flush(o, end16);
+  if (lane < 4) *(uint4 *)(o.dst + end16 + lane * 16) = uint4{0, 0, 0, 0};
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s) {
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(k_snappy, dim3(njobs), dim3(64), 0, s, b, jobs);
+  return hipGetLastError();
+}
 hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_dict_ba) return hipSuccess;
   hipLaunchKernelGGL(k_dict_ba, dim3(l.n_dict_ba), dim3(64), 0, s, b, l.dict_ba_chunks);

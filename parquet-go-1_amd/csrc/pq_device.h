@@ -45,6 +45,7 @@ enum : uint16_t {
   PF_BASE_KNOWN = 8, // value_base computed on host (required column or V2 num_nulls)
   PF_DELTA_SLOW = 16,// DELTA page outside the tiled pipeline's shapes (miniblock not a multiple of 8
                      // values, block size not dividing kDeltaTileVals, > 8 miniblocks): exact scalar path
+  PF_DEV_SNAPPY = 32,// host only: `data` is an offset into the device decompression region (k_snappy)
 };
 
 // Error staging key (64 bit, smaller = reported first):
@@ -58,7 +59,7 @@ __host__ __device__ inline uint64_t err_key(uint32_t phase, uint32_t page, uint3
   return ((uint64_t)(phase & 3) << 62) | ((uint64_t)(page & 0x3fffff) << 40) | ((uint64_t)(stage & 15) << 36) |
          ((uint64_t)pos << 4) | (uint64_t)(code & 15);
 }
-enum : uint32_t { ST_DICT = 0, ST_REP = 1, ST_DEF = 2, ST_VALUES = 3 };
+enum : uint32_t { ST_DICT = 0, ST_REP = 1, ST_DEF = 2, ST_VALUES = 3 };  // ST_DECOMP = 4 below
 
 struct PageDesc {        // 96 B
   uint64_t data;         // device address of the page payload (decompressed)
@@ -154,6 +155,25 @@ struct BaDelta {
   uint32_t pay_off, pay_len;  // payload (suffix bytes), relative to the page data
   uint32_t page;         // global page index
 };
+// SNAPPY data page decompressed on the device (compress.go:42-48,
+// :102-123, golang/snappy decode.go). The stage holds the raw block after its length preamble
+// (followed by >= 128 zero bytes); k_snappy writes the page — `raw` bytes (V2 level sections,
+// which are not compressed, page_v2.go:112-127), then the decompressed bytes, then 64 zero
+// bytes — at `dst`, the page data address every later kernel reads.
+struct SnappyJob {       // 48 B
+  uint64_t src;          // device address of the first element tag
+  uint64_t raw;          // device address of the raw prefix (16-B aligned)
+  uint64_t dst;          // device address of the page data (16-B aligned)
+  uint32_t src_len;      // element bytes
+  uint32_t raw_len;
+  uint32_t dlen;         // decoded length from the preamble (== the page's decompressed size)
+  uint32_t chunk;
+  uint32_t page_in_chunk;
+  uint32_t pad;
+};
+constexpr uint32_t kSnappyRing = 32768;  // LDS window of the most recent output bytes per page
+enum : uint32_t { ST_DECOMP = 4 };       // err_key stage of a device decompression error
+
 struct WorkItem {        // 16 B
   uint32_t page;         // global page index
   uint32_t v0;           // first value (within page) of this tile

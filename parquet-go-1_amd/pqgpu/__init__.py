@@ -71,10 +71,12 @@ class BatchStats(ctypes.Structure):
                 ("num_values", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
                 ("staged_bytes", ctypes.c_int64), ("host_plan_ms", ctypes.c_double),
                 ("host_decompress_ms", ctypes.c_double), ("levels_kernel_bytes", ctypes.c_int64),
-                ("values_kernel_bytes", ctypes.c_int64), ("delta_kernel_bytes", ctypes.c_int64)]
+                ("values_kernel_bytes", ctypes.c_int64), ("delta_kernel_bytes", ctypes.c_int64),
+                ("snappy_pages", ctypes.c_int64), ("snappy_kernel_bytes", ctypes.c_int64)]
 
 
 _LIB = None
+ABI_VERSION = 2  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -135,6 +137,8 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.pqgpu_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {L.pqgpu_abi_version()}, these bindings need {ABI_VERSION}: rebuild it")
     _LIB = L
     return L
 

@@ -161,9 +161,10 @@ def page_v2(values_bytes, num_values, num_nulls, num_rows, encoding, def_bytes=b
     return hdr + body
 
 
-def write_file(columns, row_groups):
+def write_file(columns, row_groups, codec=0):
     """columns: [(name, type, optional)]; row_groups: [(num_rows, [[page bytes, ...] per column],
-    [num_values per column])]. Returns the file bytes."""
+    [num_values per column])]; codec: 0 UNCOMPRESSED, 1 SNAPPY (pages already compressed).
+    Returns the file bytes."""
     out = bytearray(b"PAR1")
     rgs = []
     for num_rows, col_pages, col_nv in row_groups:
@@ -175,7 +176,7 @@ def write_file(columns, row_groups):
                 out += p
             size = len(out) - off
             total += size
-            md = [(1, I32, TYPES[typ]), (2, LIST, (I32, [0, 3, 5])), (3, LIST, (BIN, [name])), (4, I32, 0),
+            md = [(1, I32, TYPES[typ]), (2, LIST, (I32, [0, 3, 5])), (3, LIST, (BIN, [name])), (4, I32, codec),
                   (5, I64, nv), (6, I64, size), (7, I64, size), (9, I64, off)]
             ccs.append([(2, I64, off), (3, STRUCT, md)])
         rgs.append([(1, LIST, (STRUCT, ccs)), (2, I64, total), (3, I64, num_rows)])
@@ -241,3 +242,109 @@ def ba_column_file(pages, encoding, v2=False):
     ps = [page_v2(st, n, 0, n, encoding) if v2 else page_v1(st, n, encoding) for st, n in pages]
     n = sum(k for _, k in pages)
     return write_file([("s", "BYTE_ARRAY", False)], [(n, [ps], [n])])
+
+
+# ---------------------------------------------------------------- raw snappy blocks
+# Element encoders follow the snappy block format (format_description.txt: tag & 3 = literal /
+# copy with 1-, 2- or 4-byte offset; literal lengths above 60 in 1-4 extra bytes), so streams
+# with chosen element kinds, far offsets and deliberate corruption can be built.
+
+
+def sn_literal(data, extra=None):
+    """A literal element; `extra` forces 1-4 length bytes (else the shortest form)."""
+    n = len(data) - 1
+    if extra is None:
+        extra = 0 if n < 60 else 1 if n < 1 << 8 else 2 if n < 1 << 16 else 3 if n < 1 << 24 else 4
+    if extra == 0:
+        return bytes([n << 2]) + bytes(data)
+    return bytes([(59 + extra) << 2]) + n.to_bytes(extra, "little") + bytes(data)
+
+
+def sn_copy(off, length, kind):
+    """A copy element: kind 1 (length 4-11, offset < 2048), 2 (offset < 65536) or 4."""
+    if kind == 1:
+        assert 4 <= length <= 11 and off < 2048
+        return bytes([1 | ((length - 4) << 2) | ((off >> 8) << 5), off & 0xFF])
+    assert 1 <= length <= 64
+    if kind == 2:
+        return bytes([2 | ((length - 1) << 2)]) + off.to_bytes(2, "little")
+    return bytes([3 | ((length - 1) << 2)]) + off.to_bytes(4, "little")
+
+
+def snappy_block(dlen, elements):
+    return uvar(dlen) + b"".join(elements)
+
+
+def snappy_compress(data, rng=None, min_match=4, max_lit=None):
+    """Greedy LZ77 into snappy elements with no window limit (offsets up to the whole input,
+    copy-4 past 64 KiB). With `rng` the copy kind, copy length split and literal length
+    form vary at random so every element encoding occurs."""
+    data = bytes(data)
+    n = len(data)
+    last = {}
+    out, lit = [], bytearray()
+
+    def flush_lit():
+        k = 0
+        while k < len(lit):
+            m = len(lit) - k if max_lit is None else min(max_lit, len(lit) - k)
+            extra = None
+            if rng is not None and m - 1 >= 60 and rng.random() < 0.3:
+                extra = int(rng.integers(1, 5))
+                if m - 1 >= 1 << (8 * extra):
+                    extra = None
+            out.append(sn_literal(lit[k:k + m], extra))
+            k += m
+        lit.clear()
+
+    i = 0
+    while i < n:
+        key = data[i:i + min_match]
+        j = last.get(key) if len(key) == min_match else None
+        if len(key) == min_match:
+            last[key] = i
+        if j is None:
+            lit.append(data[i])
+            i += 1
+            continue
+        off = i - j
+        L = min_match
+        while i + L < n and data[i + L] == data[j + L]:
+            L += 1
+        flush_lit()
+        k = 0
+        while k < L:
+            cap = 64 if rng is None else int(rng.integers(4, 65))
+            m = min(cap, L - k)  # a tail shorter than 4 is still a valid copy (kinds 2 and 4)
+            kinds = [4]
+            if off < 65536:
+                kinds.append(2)
+            if 4 <= m <= 11 and off < 2048:
+                kinds.append(1)
+            kind = kinds[-1] if rng is None else kinds[int(rng.integers(0, len(kinds)))]
+            out.append(sn_copy(off, m, kind))
+            k += m
+        for t in range(i + 1, min(i + L, n - min_match + 1)):
+            last[data[t:t + min_match]] = t
+        i += L
+    flush_lit()
+    return snappy_block(n, out)
+
+
+def page_v1c(values_bytes, num_values, encoding, def_bytes=b"", compress=None):
+    """DATA_PAGE (V1) whose whole body goes through `compress` (bytes -> bytes)."""
+    body = (struct.pack("<I", len(def_bytes)) + def_bytes if def_bytes else b"") + values_bytes
+    cbody = compress(body) if compress else body
+    dph = [(1, I32, num_values), (2, I32, ENC[encoding]), (3, I32, ENC["RLE"]), (4, I32, ENC["RLE"])]
+    hdr = tstruct([(1, I32, 0), (2, I32, len(body)), (3, I32, len(cbody)), (5, STRUCT, dph)])
+    return hdr + cbody
+
+
+def page_v2c(values_bytes, num_values, num_nulls, num_rows, encoding, def_bytes=b"", compress=None):
+    """DATA_PAGE_V2: level bytes raw, values through `compress` (page_v2.go:112-127)."""
+    cvals = compress(values_bytes) if compress else values_bytes
+    dph = [(1, I32, num_values), (2, I32, num_nulls), (3, I32, num_rows), (4, I32, ENC[encoding]),
+           (5, I32, len(def_bytes)), (6, I32, 0), (7, BOOL, True)]
+    hdr = tstruct([(1, I32, 3), (2, I32, len(def_bytes) + len(values_bytes)),
+                   (3, I32, len(def_bytes) + len(cvals)), (8, STRUCT, dph)])
+    return hdr + def_bytes + cvals
