@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md
 
 
-def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2, first_rg=0):
+def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2, first_rg=0, codec="NONE"):
     """cfg2 file bytes: row groups [first_rg, first_rg + rows / rg_rows) of one
     logical file whose row group g is drawn from default_rng([seed, g]) (column a) and
     default_rng([seed + 1, g]) (column b), so rank shards are a row-group partition of one file.
@@ -63,7 +63,10 @@ def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2, first
         pages[p, k] = False  # one more non-null value
     t = pa.table({"a": pa.array(a, mask=m), "b": pa.array(b, mask=m2)})
     bio = io.BytesIO()
-    pq.write_table(t, bio, use_dictionary=False, data_page_version="2.0", compression="NONE",
+    # SNAPPY pages are V1 (cfg5's page version): pyarrow stores an incompressible V2 values
+    # section uncompressed with is_compressed=false, which the reference ignores (page_v2.go:125)
+    pq.write_table(t, bio, use_dictionary=False, data_page_version="2.0" if codec == "NONE" else "1.0",
+                   compression=codec,
                    column_encoding={"a": "DELTA_BINARY_PACKED", "b": "PLAIN"}, max_rows_per_page=page_rows,
                    row_group_size=rg_rows, write_statistics=False)
     return bio.getvalue(), (a, m, b, m2)
@@ -119,6 +122,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=67_108_864)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--codec", choices=["NONE", "SNAPPY"], default="NONE",
+                    help="SNAPPY: the same cfg2 file with SNAPPY pages, decompressed on the device "
+                         "(k_snappy) inside every step (cfg5's codec; not the headline line)")
     ap.add_argument("--verify", action="store_true", help="check every decoded value against the generator")
     args = ap.parse_args()
 
@@ -139,7 +145,7 @@ def main():
     rg_rows = 4_194_304
     per_rank_rg = max(1, -(-args.rows // rg_rows))
     g0, g1 = shard.row_group_range(per_rank_rg * world, rank, world)
-    data, truth = gen_cfg2(min(args.rows, (g1 - g0) * rg_rows), rg_rows=rg_rows, first_rg=g0)
+    data, truth = gen_cfg2(min(args.rows, (g1 - g0) * rg_rows), rg_rows=rg_rows, first_rg=g0, codec=args.codec)
     ctx = pqgpu.Context(local_rank if world > 1 else 0)
     f = pqgpu.File(data)
     b = pqgpu.Batch(ctx)
@@ -194,7 +200,7 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes moved by that kernel per launch / its avg time
     kb = kernel_bytes(b, kern_name, st) or 0
     achieved = kb / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(kern_name, args.rows)
+    traffic, traffic_src = pmc_traffic(kern_name, args.rows) if args.codec == "NONE" else (None, None)
     line = {
         "metric": "decoded GB/s + rows/s per GPU and whole node (1/2/4/8); % HBM peak",
         "value": round(value, 2),
@@ -208,8 +214,9 @@ def main():
         "vs_baseline": None,
         "dtype": "int64+f64 (bit copies), u8 levels",
         "data": "synthetic (numpy default_rng([2|3, row group]); pyarrow 25 writer)",
-        "config": {"workload": "cfg2: INT64 DELTA_BINARY_PACKED + DOUBLE PLAIN, OPTIONAL 10% nulls, V2, "
-                               "UNCOMPRESSED", "rows_per_gpu": args.rows, "row_groups_per_gpu": f.num_row_groups,
+        "config": {"workload": "cfg2: INT64 DELTA_BINARY_PACKED + DOUBLE PLAIN, OPTIONAL 10% nulls, "
+                               + ("V2, UNCOMPRESSED" if args.codec == "NONE" else
+                                  "V1, SNAPPY (pages resident compressed, decompressed on the device every step)"), "rows_per_gpu": args.rows, "row_groups_per_gpu": f.num_row_groups,
                    "page_rows": 65536, "parallelism": f"row-group shards x{world}"},
         "rows_per_s": round(rows_per_s, 1),
         "algorithmic_GBps": round(algo_bytes * world / 1e9 / (ms_per_step / 1e3), 2),

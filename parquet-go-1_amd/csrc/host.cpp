@@ -1225,10 +1225,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
   // SNAPPY pages first: every later kernel reads page data
-  HIPCHECK(timed(b, 11, s, [&] {
-             return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy), (uint32_t)b->snappy.size(), s);
-           }),
-           err);
+  if (!b->snappy.empty())
+    HIPCHECK(timed(b, 11, s, [&] {
+               return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy), (uint32_t)b->snappy.size(), s);
+             }),
+             err);
   // DELTA work items and the other value work items go out as two launches (separately profiled).
   LaunchLists l1 = l, l2 = l;
   l1.n_items = b->n_delta_items;

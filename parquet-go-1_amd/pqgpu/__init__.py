@@ -20,8 +20,10 @@ readValues' "read values from page failed" wrapping (page_v1.go:57).
 There is no CPU fallback: every decode runs on the GPU; without a GPU (or
 without libpqgpu.so) the constructors raise.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -154,6 +156,21 @@ class DecodeError(Exception):
         super().__init__(f"[{ERROR_NAMES.get(self.code, self.code)}] chunk {self.chunk} page {self.page}: {self.msg}")
 
 
+# Live handles, released in order (batches, then contexts) before the interpreter tears down
+# modules: a batch left alive by an exception traceback would otherwise be destroyed by GC
+# after its context or after the HIP runtime has shut down.
+_live_batches = weakref.WeakSet()
+_live_contexts = weakref.WeakSet()
+
+
+@atexit.register
+def _release_all():
+    for b in list(_live_batches):
+        b.close()
+    for c in list(_live_contexts):
+        c.close()
+
+
 def _check(rc, err):
     if rc:
         raise DecodeError(err)
@@ -167,6 +184,7 @@ class Context:
         err = Error()
         _check(lib().pqgpu_ctx_create(device, ctypes.byref(self._h), ctypes.byref(err)), err)
         self.device = device
+        _live_contexts.add(self)
 
     def close(self):
         if self._h:
@@ -271,6 +289,7 @@ class Batch:
                                         ctypes.byref(err)), err)
         self._files = []
         self._infos = []
+        _live_batches.add(self)
 
     def close(self):
         if self._h:
@@ -338,7 +357,7 @@ class Batch:
     def kernel_times(self):
         """{kernel name: (average ms per launch, launches)} for every timed launch slot."""
         out = {}
-        for k in range(11):
+        for k in range(12):  # PQGPU_TIMER_SLOTS
             ms, n = ctypes.c_double(), ctypes.c_int64()
             name = ctypes.create_string_buffer(64)
             lib().pqgpu_batch_kernel_slot(self._h, k, ctypes.byref(ms), ctypes.byref(n), name, 64)
