@@ -2738,6 +2738,71 @@ DEV void snappy_put(SnappyOut &o, const uint8_t *S, uint32_t P, uint32_t len) {
   }
 }
 
+// A literal of `len` bytes (any length): the head goes through the ring up to a 16-B page
+// boundary, the aligned body is copied global -> global by all kSnappyWaves waves of the
+// workgroup (funnel16, 4 pieces of 16 B in flight per lane; pieces in the body's last
+// kSnappyRing bytes also land in the ring, which must hold the most recent output for later
+// copies), the tail goes through the ring again. Long literals dominate incompressible pages
+// (one literal per 64 KiB encoder fragment).
+constexpr uint32_t kSnappyWaves = 4;
+constexpr uint32_t kSnappyDirect = 2048;  // bytes: shorter literals stay on the ring path
+struct SnappyCmd {                         // LDS: wave 0 -> helper waves
+  uint64_t src;                            // literal body source (global address)
+  uint32_t P, pieces, ring_from, stop;
+};
+
+// Share of one long-literal body for wave `w` (all waves call it between two barriers).
+DEV void snappy_body(const SnappyCmd &c, uint8_t *ring, uint8_t *dst, uint32_t w) {
+  const uint8_t *S = gp_u64<const uint8_t>(c.src);
+  const uint32_t P = c.P, pieces = c.pieces, ring_from = c.ring_from;
+  const uint32_t sa = (uint32_t)((uintptr_t)S & 15);
+  const uint4 *sb = (const uint4 *)(S - sa);
+  uint4 *d = (uint4 *)(dst + P);
+  constexpr uint32_t NT = 64 * kSnappyWaves, U = 4;
+  uint32_t i = w * 64 + lane_id();
+  for (; i + (U - 1) * NT < pieces; i += U * NT) {
+    uint4 a[U], e[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) { a[u] = sb[i + u * NT]; e[u] = sb[i + u * NT + 1]; }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint4 v = funnel16(a[u], e[u], sa);
+      d[i + u * NT] = v;
+      if (i + u * NT >= ring_from) *(uint4 *)(ring + ((P + (i + u * NT) * 16) & kRingMask)) = v;
+    }
+  }
+  for (; i < pieces; i += NT) {
+    const uint4 v = funnel16(sb[i], sb[i + 1], sa);
+    d[i] = v;
+    if (i >= ring_from) *(uint4 *)(ring + ((P + i * 16) & kRingMask)) = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // stores done before the barrier: wave 0 may read them back
+}
+
+DEV void snappy_literal(SnappyOut &o, SnappyCmd &cmd, const uint8_t *S, uint32_t P, uint32_t len) {
+  if (len >= kSnappyDirect) {
+    const uint32_t h = (16 - (P & 15)) & 15;
+    if (h) snappy_put(o, S, P, h);
+    S += h; P += h; len -= h;
+    snappy_flush(o, P);  // ring [flushed, P) -> page, so the page is complete below P
+    const uint32_t body = len & ~15u;
+    if (lane_id() == 0) {
+      cmd.src = (uint64_t)(uintptr_t)S;
+      cmd.P = P;
+      cmd.pieces = body >> 4;
+      cmd.ring_from = body > kSnappyRing ? (body - kSnappyRing) >> 4 : 0;  // first piece kept
+      cmd.stop = 0;
+    }
+    wg_barrier();
+    snappy_body(cmd, o.ring, o.dst, 0);
+    wg_barrier();
+    o.flushed = P + body;
+    S += body; P += body; len -= body;
+  }
+  for (uint32_t k = 0; k < len; k += kSnappyRing / 2)
+    snappy_put(o, S + k, P + k, min(len - k, kSnappyRing / 2));
+}
+
 // Page bytes [P - off, ...) -> [P, P + len), len <= 64, 1 <= off <= P (overlap repeats the
 // pattern: byte i comes from P - off + i % off).
 DEV void snappy_copy(SnappyOut &o, uint32_t P, uint32_t off, uint32_t len) {
@@ -2759,10 +2824,9 @@ DEV void snappy_copy(SnappyOut &o, uint32_t P, uint32_t off, uint32_t len) {
   if (i < len) o.ring[(P + i) & kRingMask] = (uint8_t)v;
 }
 
-__global__ void __launch_bounds__(64) k_snappy(BatchDev b_in, const SnappyJob *jobs) {
-  const BatchDev b = global_view(b_in);
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
-  const SnappyJob &jb = gp(jobs)[blockIdx.x];
+// Wave 0 walks and executes the element chain; waves 1.. wait at barriers and join in the
+// body copies of long literals (snappy_literal) until wave 0 raises `stop`.
+DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, SnappyCmd &cmd) {
   const uint8_t *src = gp_u64<const uint8_t>(jb.src);
   const uint32_t n = sgpr(jb.src_len), raw = sgpr(jb.raw_len), dlen = sgpr(jb.dlen);
   const uint32_t lane = lane_id();
@@ -2811,8 +2875,15 @@ __global__ void __launch_bounds__(64) k_snappy(BatchDev b_in, const SnappyJob *j
       if (et == 0) {
         const uint64_t len = (uint64_t)ev + 1;
         if (len > dlen - op || len > n - s) { bad = true; break; }
-        for (uint32_t k = 0; k < (uint32_t)len; k += kSnappyRing / 2)
-          snappy_put(o, src + s + k, raw + op + k, min((uint32_t)len - k, kSnappyRing / 2));
+        const uint32_t rel = s - pos;  // literal start inside this window's 64 lanes
+        if (rel + len <= 64) {
+          // short literal: its bytes are byte 0 of lanes rel.. of this window (no memory load)
+          snappy_room(o, raw + op, 64);
+          const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rel + lane) * 4), (int)w);
+          if (lane < (uint32_t)len) o.ring[(raw + op + lane) & kRingMask] = (uint8_t)v;
+        } else {
+          snappy_literal(o, cmd, src + s, raw + op, (uint32_t)len);
+        }
         op += (uint32_t)len;
       } else {
         const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)clen, (int)e);
@@ -2836,12 +2907,32 @@ __global__ void __launch_bounds__(64) k_snappy(BatchDev b_in, const SnappyJob *j
   if (lane < 4) *(uint4 *)(o.dst + end16 + lane * 16) = uint4{0, 0, 0, 0};
 }
 
+__global__ void __launch_bounds__(64 * kSnappyWaves) k_snappy(BatchDev b_in, const SnappyJob *jobs) {
+  const BatchDev b = global_view(b_in);
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
+  __shared__ SnappyCmd cmd;
+  const SnappyJob &jb = gp(jobs)[blockIdx.x];
+  const uint32_t w = threadIdx.x / 64;
+  if (w == 0) {
+    snappy_page(b, jb, ring, cmd);
+    if (lane_id() == 0) cmd.stop = 1;
+    wg_barrier();
+  } else {
+    for (;;) {  // one round per long literal; exits when wave 0 is done (every path sets stop)
+      wg_barrier();
+      if (cmd.stop) break;
+      snappy_body(cmd, ring, gp_u64<uint8_t>(jb.dst), w);
+      wg_barrier();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s) {
   if (!njobs) return hipSuccess;
-  hipLaunchKernelGGL(k_snappy, dim3(njobs), dim3(64), 0, s, b, jobs);
+  hipLaunchKernelGGL(k_snappy, dim3(njobs), dim3(64 * kSnappyWaves), 0, s, b, jobs);
   return hipGetLastError();
 }
 hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
