@@ -171,7 +171,7 @@ struct SnappyJob {       // 48 B
   uint32_t page_in_chunk;
   uint32_t pad;
 };
-constexpr uint32_t kSnappyRing = 32768;  // LDS window of the most recent output bytes per page
+constexpr uint32_t kSnappyRing = 16384;  // LDS window of the most recent output bytes per page
 enum : uint32_t { ST_DECOMP = 4 };       // err_key stage of a device decompression error
 
 struct WorkItem {        // 16 B

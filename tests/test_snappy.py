@@ -5,7 +5,7 @@ and pyarrow's codec).
 Blocks are written by tools/rawpq.py's greedy encoder (checked here against pyarrow's snappy
 codec) so that every element encoding occurs: literals with 0-4 length bytes, copies with 1-,
 2- and 4-byte offsets, overlapping copies (offset < length), and offsets past the kernel's
-LDS ring (32 KiB) and past 64 KiB. Corrupt blocks cover every ErrCorrupt condition of the
+LDS ring (16 KiB) and past 64 KiB. Corrupt blocks cover every ErrCorrupt condition of the
 decoder, in the part of a page the host planner reads and in the part only the GPU reads, and
 the reference's error order across pages (readPages decompresses page by page before any value
 is decoded). The GPU must equal the oracle: values bit for bit, errors as (class, page)."""
@@ -28,7 +28,7 @@ def _data(kind, nbytes, rng):
         return bytes(rng.integers(0, 256, nbytes, dtype=np.uint8))
     if kind == "smallint":  # int64 values < 16: short copies everywhere, overlapping runs
         return rng.integers(0, 16, nbytes // 8, dtype=np.int64).tobytes()
-    if kind == "far":  # a 40 000-byte random period: copies reach past the ring (32 KiB)
+    if kind == "far":  # a 40 000-byte random period: copies reach past the ring (16 KiB)
         base = bytes(rng.integers(0, 256, 40_000, dtype=np.uint8))
         return (base * (nbytes // 40_000 + 1))[:nbytes]
     if kind == "far64k":  # 70 000-byte period: copy-4 offsets past 64 KiB
