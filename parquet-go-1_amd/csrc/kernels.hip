@@ -2835,13 +2835,37 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     snappy_put(o, gp_u64<const uint8_t>(jb.raw) + k, k, min(raw - k, kSnappyRing / 2));
   uint32_t pos = 0, op = 0;  // stream position, decoded bytes
   bool bad = false;
+  // The element stream is held in registers, 512 bytes at a time: lane k of W0 / W1 holds the
+  // dword at aligned-stream offset wb + 4k / wb + 256 + 4k (aligned stream = src rounded down
+  // to 4 B). W1 is loaded one window ahead, so the walk does not wait on HBM every 64 bytes.
+  const uint32_t sa0 = (uint32_t)((uintptr_t)src & 3);
+  const uint32_t *srcw = (const uint32_t *)(src - sa0);
+  const uint32_t wlim = n + sa0 + 64;  // dwords below this are inside the block's zero padding
+  auto ldw = [&](uint32_t at) -> uint32_t {  // the dword at aligned offset at + 4 * lane
+    const uint32_t k = at + 4 * lane;
+    return k < wlim ? srcw[k >> 2] : 0u;
+  };
+  uint32_t wb = 0, W0 = ldw(0), W1 = ldw(256);
   while (pos < n) {
     // the element that would start at pos + lane: tag, header bytes, literal length - 1 or
     // copy offset, copy length (decode_other.go:20-96)
-    const uint8_t *a = src + pos + lane;
-    const uint32_t sh = (uint32_t)(uintptr_t)a & 3;
-    const uint32_t *al = (const uint32_t *)(a - sh);
-    const uint32_t d0 = al[0], d1 = al[1];
+    const uint32_t ap = pos + sa0;
+    if (ap - wb >= 256) {
+      if (ap - wb < 512) {
+        W0 = W1; wb += 256; W1 = ldw(wb + 256);
+      } else {  // jumped past a long literal
+        wb = ap & ~3u; W0 = ldw(wb); W1 = ldw(wb + 256);
+      }
+    }
+    const uint32_t off = ap - wb, r = off + lane, q = r >> 2, sh = r & 3;
+    uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4), (int)W0);
+    uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4 + 4), (int)W0);
+    if (off >= 256 - 68) {  // some lane reads W1 (uniform)
+      const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4), (int)W1);
+      const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(q * 4 + 4), (int)W1);
+      if (q >= 64) d0 = e0;
+      if (q + 1 >= 64) d1 = e1;
+    }
     const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, sh), b4 = (d1 >> (8 * sh)) & 0xff;
     const uint32_t tag = w & 0xff, x = tag >> 2, t = tag & 3;
     uint32_t hdr, val, clen = 0;
