@@ -200,7 +200,8 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes moved by that kernel per launch / its avg time
     kb = kernel_bytes(b, kern_name, st) or 0
     achieved = kb / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(kern_name, args.rows) if args.codec == "NONE" else (None, None)
+    traffic, traffic_src = pmc_traffic(kern_name, args.rows, os.path.join(
+        ROOT, "profiles", "r01_pmc_traffic.json" if args.codec == "NONE" else "r01_s7_pmc_snappy.json"))
     line = {
         "metric": "decoded GB/s + rows/s per GPU and whole node (1/2/4/8); % HBM peak",
         "value": round(value, 2),
