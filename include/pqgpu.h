@@ -167,8 +167,12 @@ int pqgpu_batch_reset(pqgpu_batch *b);
 
 /* readChunk + readPages (chunk_reader.go:182-362): walk the chunk's page
  * headers on the host, validate them exactly as the reference does, and
- * stage the page sections (decompressed on host threads when the codec is
- * SNAPPY/GZIP) for upload. `file_bytes` is the whole file (offsets in `meta`
+ * stage the page sections for upload. GZIP pages (and dictionary pages) are
+ * decompressed on the host; SNAPPY data pages are staged compressed and
+ * decompressed by k_snappy at the start of every decode (the host decodes
+ * only the page head it validates; PQ_HOST_SNAPPY=1 forces host decoding).
+ * A corrupt SNAPPY block is reported at sync as that page's PQ_ERR_DECOMPRESS,
+ * in the reference's order (compress.go:102-123). `file_bytes` is the whole file (offsets in `meta`
  * are absolute); `col` carries maxD/maxR (schema.go:893-924).
  * A chunk-level error is recorded and returned here; the chunk id is still
  * assigned so its error can be queried later. */

@@ -363,3 +363,36 @@ def test_preamble_mismatch_host():
     cid, e = b.add_file_chunk(pqgpu.File(data), 0, 0)
     assert e is not None and (e.code, e.page) == (7, 0)
     b.close()
+
+
+def _pyarrow_snappy_file(kind, rows=3 * 65536 + 777):
+    """pyarrow (Arrow C++ snappy) V1 SNAPPY pages of 65,536 rows: the bench's page shape."""
+    pa = pytest.importorskip("pyarrow")
+    import io
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(11)
+    if kind == "double_opt":  # def-level bitmap (short elements) + 64 KiB literals (direct path)
+        col = pa.array(rng.random(rows), mask=rng.random(rows) < 0.1)
+    elif kind == "int64_small":  # copies every few bytes, ring wrap-around, HBM flushes
+        col = pa.array(rng.integers(0, 16, rows).astype(np.int64))
+    else:  # "int64_small_opt"
+        col = pa.array(rng.integers(0, 16, rows).astype(np.int64), mask=rng.random(rows) < 0.3)
+    bio = io.BytesIO()
+    pq.write_table(pa.table({"c": col}), bio, use_dictionary=False, data_page_version="1.0",
+                   compression="SNAPPY", column_encoding={"c": "PLAIN"}, max_rows_per_page=65536,
+                   write_statistics=False)
+    return bio.getvalue()
+
+
+@pytest.mark.parametrize("kind", ["double_opt", "int64_small", "int64_small_opt"])
+def test_oracle_pyarrow_pages(kind):
+    data = _pyarrow_snappy_file(kind)
+    got = O.File(data).read_chunk(0, 0)
+    assert got.num_values > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["double_opt", "int64_small", "int64_small_opt"])
+def test_gpu_pyarrow_pages(gpu_ctx, kind):
+    data = _pyarrow_snappy_file(kind)
+    _compare(_gpu(gpu_ctx, data)[0], data, kind)
