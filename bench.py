@@ -126,6 +126,9 @@ def main():
                     help="SNAPPY: the same cfg2 file with SNAPPY pages, decompressed on the device "
                          "(k_snappy) inside every step (cfg5's codec; not the headline line)")
     ap.add_argument("--verify", action="store_true", help="check every decoded value against the generator")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: after the timed decode, all-gather column a over RCCL into one contiguous "
+                         "column on every rank and time it separately (SURVEY §8(e), optional)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -232,6 +235,19 @@ def main():
                         if kernel_bytes(b, k, st) is not None and ms > 0 else None}
                     for k, (ms, n) in ktimes.items()},
     }
+    if args.gather and dist is not None:
+        import torch
+        col_a = shard.device_values(b, ids[0::2], f"cuda:{local_rank}")
+        shard.gather_column(col_a, dist)  # warm-up (communicator setup)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        whole = shard.gather_column(col_a, dist)
+        torch.cuda.synchronize()
+        gdt = shard.max_over_ranks(time.perf_counter() - t0, dist, device="cuda")
+        line["allgather"] = {"column": "a", "bytes_per_rank": col_a.numel() * 8,
+                             "bytes_out": whole.numel() * 8, "ms": round(gdt * 1e3, 3),
+                             "GBps_out": round(whole.numel() * 8 / gdt / 1e9, 1), "backend": dist.get_backend()}
     if rank == 0 and not args.no_cpu_baseline:
         rps, gbs, thr, desc = cpu_baseline(data)
         line["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s (decoded output)", "rows_per_s": round(rps, 1),

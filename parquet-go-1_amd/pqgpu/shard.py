@@ -24,3 +24,55 @@ def max_over_ranks(value, dist=None, device="cpu"):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_column(local, dist=None):
+    """The whole column on every rank from each rank's decoded slice (the
+    optional collective): rank r contributes its row-group range's values, in order, and every
+    rank receives the concatenation in rank order. One all-gather of the slice sizes, then one
+    all_gather_into_tensor of the slices padded to the largest (RCCL over xGMI on GPUs, gloo on
+    CPU). Not on the decode path: the benchmark times it separately (`bench.py --gather`)."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return local
+    world = dist.get_world_size()
+    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+    sizes = torch.empty(world, dtype=torch.int64, device=local.device)
+    dist.all_gather_into_tensor(sizes, n)
+    sizes = [int(s) for s in sizes.cpu()]
+    m = max(sizes)
+    buf = local if local.numel() == m else torch.cat([local, local.new_zeros(m - local.numel())])
+    out = local.new_empty(world * m)
+    dist.all_gather_into_tensor(out, buf.contiguous())
+    if all(s == m for s in sizes):
+        return out
+    return torch.cat([out[r * m: r * m + s] for r, s in enumerate(sizes)])
+
+
+def device_values(batch, chunk_ids, device):
+    """This rank's decoded values of `chunk_ids` (fixed-width columns) concatenated into one
+    torch tensor on `device`, copied device to device from the batch's output arena (no host
+    round trip). The element type is the column's 8-byte lane (int64 view) or int32.
+    torch must initialise HIP before libpqgpu is loaded (bench.py does): torch ships its own
+    libamdhip64 (soname libamdhip64.so.7), which libpqgpu then binds to, so the process has one
+    HIP runtime and the two share device pointers."""
+    import ctypes
+    import torch
+    rs = [batch.result(c, copy=False) for c in chunk_ids]
+    width = {r.value_width for r in rs}
+    if len(width) != 1 or width.pop() not in (4, 8):
+        raise ValueError("device_values: one fixed width of 4 or 8 bytes expected")
+    dt = torch.int64 if rs[0].value_width == 8 else torch.int32
+    out = torch.empty(sum(r.num_values for r in rs), dtype=dt, device=device)
+    hip = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.synchronize(device)
+    at = 0
+    for r in rs:
+        nb = r.num_values * r.value_width
+        if nb:
+            rc = hip.hipMemcpy(ctypes.c_void_p(out.data_ptr() + at), ctypes.c_void_p(r.values), ctypes.c_size_t(nb),
+                               ctypes.c_int(3))  # hipMemcpyDeviceToDevice
+            if rc != 0:
+                raise RuntimeError(f"hipMemcpy device to device failed ({rc})")
+        at += nb
+    return out

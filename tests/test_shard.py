@@ -52,3 +52,68 @@ def test_gloo_world2_shards_and_max():
         assert p.exitcode == 0
     assert [(g0, g1) for _, g0, g1, _ in out] == [(0, 16), (16, 32)]
     assert all(t == 2.0 for *_, t in out)
+
+
+def _gather_worker(rank, world, port, sizes, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    start = sum(sizes[:rank])
+    local = torch.arange(start, start + sizes[rank], dtype=torch.int64)
+    got = shard.gather_column(local, dist)
+    q.put((rank, got.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [(5, 5), (7, 3), (0, 4)])
+def test_gloo_world2_gather_column(sizes):
+    """The optional all-gather of a decoded column: rank slices in rank order,
+    uneven and empty slices included."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, 2, port, list(sizes), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got in out:
+        assert got == list(range(sum(sizes)))
+
+
+_DEVICE_VALUES = r"""
+import sys
+import numpy as np
+import torch
+torch.zeros(1, device="cuda:0")  # torch's HIP runtime first: libpqgpu then binds to the same one
+sys.path[:0] = sys.argv[1:]
+import pqgpu, pqtest
+from pqgpu import shard
+f = pqgpu.File(pqtest.load("cfg2_v2_small"))
+b = pqgpu.Batch(pqgpu.Context(0))
+ids = [b.add_file_chunk(f, rg, 0)[0] for rg in range(f.num_row_groups)]
+b.decode()
+assert b.sync() is None
+got = shard.device_values(b, ids, "cuda:0").cpu().numpy()
+want = np.concatenate([b.result(c).values_raw for c in ids])
+np.testing.assert_array_equal(got, want)
+b.close()
+print("device_values ok", got.size)
+"""
+
+
+@pytest.mark.gpu
+def test_device_values_match_result():
+    """shard.device_values copies a chunk's decoded values device to device, bit for bit, in a
+    process where torch initialises HIP first (as in bench.py's multi-rank path)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, d) for d in ("parquet-go-1_amd", "tests", "oracle")]
+    r = subprocess.run([sys.executable, "-c", _DEVICE_VALUES, *paths], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "device_values ok" in r.stdout, r.stdout + r.stderr
