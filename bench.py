@@ -135,11 +135,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = 0
+    red_dev = "cuda"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # one rank per GPU; PQ_BENCH_BACKEND=gloo (with ranks sharing a card) only rehearses the
+        # multi-rank path on a 1-GPU box: timing then reduces on the CPU
+        backend = os.environ.get("PQ_BENCH_BACKEND", "nccl")
+        device = local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(device)  # torch initialises HIP before libpqgpu loads (one runtime)
+        torch.zeros(1, device=f"cuda:{device}")
+        dist.init_process_group(backend)
+        red_dev = "cuda" if backend == "nccl" else "cpu"
     import pqgpu
     from pqgpu import shard
 
@@ -149,7 +157,7 @@ def main():
     per_rank_rg = max(1, -(-args.rows // rg_rows))
     g0, g1 = shard.row_group_range(per_rank_rg * world, rank, world)
     data, truth = gen_cfg2(min(args.rows, (g1 - g0) * rg_rows), rg_rows=rg_rows, first_rg=g0, codec=args.codec)
-    ctx = pqgpu.Context(local_rank if world > 1 else 0)
+    ctx = pqgpu.Context(device)
     f = pqgpu.File(data)
     b = pqgpu.Batch(ctx)
     ids = []
@@ -192,7 +200,7 @@ def main():
     st = b.stats()
     kern_ms, kern_n, kern_name = b.kernel_time()
     ktimes = b.kernel_times()
-    dt = shard.max_over_ranks(dt, dist, device="cuda")
+    dt = shard.max_over_ranks(dt, dist, device=red_dev)
     ms_per_step = dt / args.steps * 1e3
     rows_total = args.rows * world
     out_gb = st.output_bytes * world / 1e9
@@ -237,14 +245,16 @@ def main():
     }
     if args.gather and dist is not None:
         import torch
-        col_a = shard.device_values(b, ids[0::2], f"cuda:{local_rank}")
+        col_a = shard.device_values(b, ids[0::2], f"cuda:{device}")
+        if red_dev == "cpu":  # gloo rehearsal: gather host copies
+            col_a = col_a.cpu()
         shard.gather_column(col_a, dist)  # warm-up (communicator setup)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         whole = shard.gather_column(col_a, dist)
         torch.cuda.synchronize()
-        gdt = shard.max_over_ranks(time.perf_counter() - t0, dist, device="cuda")
+        gdt = shard.max_over_ranks(time.perf_counter() - t0, dist, device=red_dev)
         line["allgather"] = {"column": "a", "bytes_per_rank": col_a.numel() * 8,
                              "bytes_out": whole.numel() * 8, "ms": round(gdt * 1e3, 3),
                              "GBps_out": round(whole.numel() * 8 / gdt / 1e9, 1), "backend": dist.get_backend()}
