@@ -2882,6 +2882,7 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     }
     // stream bytes of the element (saturated: a literal that long fails its bounds check)
     const uint32_t esz = t == 0 ? (uint32_t)min<uint64_t>((uint64_t)hdr + val + 1, 0x7fffffffu) : hdr;
+    const uint32_t pk = t | (hdr << 2) | (clen << 5);  // one readlane per element for type, header, length
     uint64_t chain = 0;
     uint32_t cur = 0;
     while (cur < 64 && pos + cur < n) {
@@ -2891,8 +2892,8 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     while (chain) {
       const uint32_t e = (uint32_t)__builtin_ctzll(chain);
       chain &= chain - 1;
-      const uint32_t et = (uint32_t)__builtin_amdgcn_readlane((int)t, (int)e);
-      const uint32_t eh = (uint32_t)__builtin_amdgcn_readlane((int)hdr, (int)e);
+      const uint32_t epk = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)e);
+      const uint32_t et = epk & 3, eh = (epk >> 2) & 7;
       const uint32_t ev = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)e);
       const uint32_t s = pos + e + eh;  // first byte after the header
       if (s > n) { bad = true; break; }
@@ -2910,7 +2911,7 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
         }
         op += (uint32_t)len;
       } else {
-        const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)clen, (int)e);
+        const uint32_t el = epk >> 5;
         if (ev == 0 || op < ev || el > dlen - op) { bad = true; break; }
         snappy_copy(o, raw + op, ev, el);
         op += el;
