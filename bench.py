@@ -72,7 +72,7 @@ def gen_cfg2(rows=67_108_864, rg_rows=4_194_304, page_rows=65_536, seed=2, first
     return bio.getvalue(), (a, m, b, m2)
 
 
-def cpu_baseline(data, budget_s=20.0):
+def cpu_baseline(data, budget_s=20.0, codec="NONE"):
     """The oracle (CPU port of the reference decoders) on this host: one thread per chunk,
     threads = min(16, cores). Returns (rows/s, GB/s decoded output, threads, sample description)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -111,7 +111,8 @@ def cpu_baseline(data, budget_s=20.0):
     for t in ts:
         t.join()
     dt = time.perf_counter() - t0
-    desc = f"{n} of {len(chunks)} column chunks ({n * 4194304 // 2 / 1e6:.0f}M rows x col) of cfg2, oracle liboracle.so"
+    desc = (f"{n} of {len(chunks)} column chunks ({n * 4194304 // 2 / 1e6:.0f}M rows x col) of cfg2"
+            + ("" if codec == "NONE" else f" ({codec} pages, decompressed by the oracle)") + ", oracle liboracle.so")
     return rows[0] / dt, out_bytes[0] / dt / 1e9, threads, desc
 
 
@@ -259,7 +260,7 @@ def main():
                              "bytes_out": whole.numel() * 8, "ms": round(gdt * 1e3, 3),
                              "GBps_out": round(whole.numel() * 8 / gdt / 1e9, 1), "backend": dist.get_backend()}
     if rank == 0 and not args.no_cpu_baseline:
-        rps, gbs, thr, desc = cpu_baseline(data)
+        rps, gbs, thr, desc = cpu_baseline(data, codec=args.codec)
         line["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s (decoded output)", "rows_per_s": round(rps, 1),
                                 "cores": thr, "kind": "port", "sample": desc,
                                 "host_cpus": os.cpu_count()}
