@@ -450,6 +450,7 @@ static int tc_list_begin(tc *t, int *etype, int32_t *size) {
   if (sz == 15) sz = (int32_t)tc_uvar(t);
   if (t->err) return t->err;
   if (sz < 0) return t->err = OR_ERR_THRIFT;
+  if ((b & 0x0f) > CT_STRUCT) return t->err = OR_ERR_THRIFT; /* getTType: unknown compact type */
   *etype = b & 0x0f;
   *size = sz;
   return OR_OK;
@@ -703,8 +704,9 @@ static void rd_row_group(tc *t, row_group *g) {
   while (tc_field(t, &st, &id, &ty)) {
     if (id == 1 && ty == CT_LIST) {
       int et; int32_t n;
+      /* parquet.go RowGroup.ReadField1: the list's element type is not checked, every element is
+         read as a ColumnChunk struct */
       if (tc_list_begin(t, &et, &n)) return;
-      if (et != CT_STRUCT) { for (int32_t i = 0; i < n && !t->err; i++) tc_skip(t, et, 1); continue; }
       if ((int64_t)n > br_rem(t->r)) { t->err = OR_ERR_THRIFT; return; }
       g->cols = (col_chunk *)calloc((size_t)(n ? n : 1), sizeof(col_chunk));
       if (!g->cols) { t->err = OR_ERR_NOMEM; return; }
@@ -726,8 +728,8 @@ static int rd_file_meta(breader *r, or_file *f) {
     if (id == 1 && ty == CT_I32) { tc_int(&t, ty); set_ver = 1; }
     else if (id == 2 && ty == CT_LIST) {
       int et; int32_t n;
+      /* FileMetaData.ReadField2: elements read as SchemaElement whatever the element type */
       if (tc_list_begin(&t, &et, &n)) break;
-      if (et != CT_STRUCT) { for (int32_t i = 0; i < n && !t.err; i++) tc_skip(&t, et, 1); continue; }
       if ((int64_t)n > br_rem(r)) { t.err = OR_ERR_THRIFT; break; }
       f->schema = (schema_el *)calloc((size_t)(n ? n : 1), sizeof(schema_el));
       if (!f->schema) return OR_ERR_NOMEM;
@@ -737,8 +739,8 @@ static int rd_file_meta(breader *r, or_file *f) {
     } else if (id == 3 && ty == CT_I64) { tc_int(&t, ty); set_nr = 1; }
     else if (id == 4 && ty == CT_LIST) {
       int et; int32_t n;
+      /* FileMetaData.ReadField4: elements read as RowGroup whatever the element type */
       if (tc_list_begin(&t, &et, &n)) break;
-      if (et != CT_STRUCT) { for (int32_t i = 0; i < n && !t.err; i++) tc_skip(&t, et, 1); continue; }
       if ((int64_t)n > br_rem(r)) { t.err = OR_ERR_THRIFT; break; }
       f->rgs = (row_group *)calloc((size_t)(n ? n : 1), sizeof(row_group));
       if (!f->rgs) return OR_ERR_NOMEM;

@@ -48,7 +48,7 @@ bool ThriftReader::list_begin(int *etype, int32_t *size) {
   if (!byte(&b)) return false;
   int32_t sz = (b >> 4) & 0x0f;
   if (sz == 15) sz = (int32_t)uvarint();
-  if (err_ || sz < 0) { err_ = true; return false; }
+  if (err_ || sz < 0 || (b & 0x0f) > CT_STRUCT) { err_ = true; return false; }  // getTType: unknown type
   *etype = b & 0x0f;
   *size = sz;
   return true;
@@ -227,11 +227,9 @@ template <class T, class F>
 static bool read_struct_list(ThriftReader &t, std::vector<T> *v, F fn, int64_t remaining) {
   int et;
   int32_t n;
+  // parquet.go's generated ReadFieldN discards ReadListBegin's element type and reads every
+  // element as the field's struct type
   if (!t.list_begin(&et, &n)) return false;
-  if (et != CT_STRUCT) {
-    for (int32_t k = 0; k < n && !t.failed(); k++) t.skip(et, 1);
-    return !t.failed();
-  }
   if ((int64_t)n > remaining) { t.fail(); return false; }
   v->resize((size_t)n);
   for (int32_t k = 0; k < n && !t.failed(); k++) fn(t, &(*v)[(size_t)k]);

@@ -140,19 +140,18 @@ int delta32_walk(GoReader &r, DeltaWalk *w, std::string *msg) {
   if (mbvc == 0) { *msg = "invalid mini block value count, it can't be zero"; return PQ_ERR_INVALID; }
   if ((e = r.uvariant32(&vc))) { *msg = "failed to read total value count"; return e; }
   if ((e = r.variant32(&f32))) { *msg = "failed to read first value"; return e; }
-  if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
+  if (mbc > 65535) { *msg = "more than 65535 miniblocks per block"; return PQ_ERR_UNSUPPORTED; }
   w->hdr = r.i; w->first = f32; w->count = vc; w->mbc = mbc; w->mbvc = mbvc; w->bs = bs;
-  uint8_t widths[256];
+  const uint8_t *widths = nullptr;  // the current block's width bytes, in place
   auto mb_header = [&]() -> int {
     int32_t m32;
     int er;
     if ((er = r.variant32(&m32))) { *msg = "failed to read min delta"; return er; }
     const int64_t ws = r.i;
     if ((er = r.readfull(mbc))) { *msg = "not enough data to read all miniblock bit widths"; return er; }
-    for (int32_t k = 0; k < mbc; k++) {
-      widths[k] = r.p[ws + k];
+    widths = r.p + ws;
+    for (int32_t k = 0; k < mbc; k++)
       if (widths[k] > 32) { *msg = "invalid miniblock bit width"; return PQ_ERR_INVALID; }
-    }
     return PQ_OK;
   };
   if ((e = mb_header())) return e;
@@ -223,10 +222,6 @@ int pick_vkind(int32_t enc, int32_t type, int32_t type_length, uint8_t *vk, std:
     *msg = std::string("unsupported encoding ") + std::to_string(enc) + " for " + what;
     return PQ_ERR_UNSUPPORTED;
   };
-  auto gpu_gap = [&]() {
-    *msg = "DELTA_BYTE_ARRAY for FIXED_LEN_BYTE_ARRAY is not implemented by the GPU decoder yet";
-    return PQ_ERR_UNSUPPORTED;
-  };
   switch (type) {
     case T_BOOLEAN:
       if (enc == ENC_PLAIN) { *vk = VK_PLAIN_BOOL; return PQ_OK; }
@@ -240,7 +235,9 @@ int pick_vkind(int32_t enc, int32_t type, int32_t type_length, uint8_t *vk, std:
       return unsup("binary");
     case T_FLBA:
       if (enc == ENC_PLAIN) { *vk = type_length == 0 ? VK_PLAIN_BA : VK_PLAIN_FIXED; return PQ_OK; }
-      if (enc == ENC_DELTA_BYTE_ARRAY) return gpu_gap();
+      // byteArrayDeltaDecoder (chunk_reader.go:71-72): values of any length, so a chunk with
+      // such a page is laid out as byte arrays (add_chunk_impl)
+      if (enc == ENC_DELTA_BYTE_ARRAY) { *vk = VK_DBA; return PQ_OK; }
       if (enc == ENC_RLE_DICTIONARY) { *vk = VK_DICT; return PQ_OK; }
       return unsup("fixed_len_byte_array");
     case T_FLOAT: case T_DOUBLE:
@@ -387,7 +384,7 @@ struct pqgpu_batch {
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
   uint64_t l_level_bw1 = 0;
-  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_rec = 0;
+  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_ba_gather = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   uint32_t n_delta_items = 0;
   uint64_t o_dbg = 0;
@@ -585,7 +582,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
       if (r.p[wstart + k] > (is64 ? 64 : 32)) { *msg = "invalid miniblock bit width"; return PQ_ERR_INVALID; }
     pd->delta_first = first;
     pd->delta_count = vc;
-    pd->delta_mbc = (uint16_t)std::min<int32_t>(mbc, 65535);
+    pd->delta_mbc = (uint16_t)mbc;  // <= 65535, checked below
     pd->delta_mbvc = (uint32_t)mbvc;
     pd->delta_first_mb = (uint32_t)(vstart + mb_start);
     // shapes of the parallel paths (kernels.hip): whole groups per miniblock, widths packed in
@@ -596,7 +593,7 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
                           (delta_tiled() ? (bs >= 128 && (int32_t)kDeltaTileVals % bs == 0)
                                          : max_blk + 48 <= kDeltaWinLoad);
     if (!shape_ok) pd->flags |= PF_DELTA_SLOW;
-    if (mbc > 256) { *msg = "too many miniblocks for the GPU decoder"; return PQ_ERR_UNSUPPORTED; }
+    if (mbc > 65535) { *msg = "more than 65535 miniblocks per block"; return PQ_ERR_UNSUPPORTED; }
     return PQ_OK;
   }
   return PQ_OK;
@@ -819,6 +816,18 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
     b->pages.push_back(pd);
     hc.num_pages++;
   }
+  if (col->physical_type == T_FLBA && hc.value_width > 0) {
+    // FIXED_LEN_BYTE_ARRAY with a DELTA_BYTE_ARRAY page: the reference's byteArrayDeltaDecoder
+    // returns []byte values of any length (type_bytearray.go:216-240), so the whole chunk uses
+    // the byte-array layout (offsets + payload); its PLAIN pages walk type_length-byte values
+    bool any_dba = false;
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) any_dba |= b->pages[p].vkind == VK_DBA;
+    if (any_dba) {
+      hc.value_width = 0;
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
+        if (b->pages[p].vkind == VK_PLAIN_FIXED) b->pages[p].vkind = VK_PLAIN_BA;
+    }
+  }
   b->stats.host_decompress_ms += decomp_ms;
   b->stats.host_plan_ms +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - decomp_ms;
@@ -1011,6 +1020,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_base = take(b->base_chunks.size() * 4);
   b->l_dict_ba = take(b->dict_ba_chunks.size() * 4);
   b->l_ba = take(b->ba_chunks.size() * 4);
+  b->l_ba_gather = take(b->ba_chunks.size() * 4);  // per decode: the BYTE_ARRAY chunks without an error
   b->l_rec = take(b->rec_pages.size() * 4);
   b->arena_size = a;
   if (a > b->d_arena_cap) {
@@ -1310,10 +1320,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     for (uint32_t c : gather) maxnn = std::max<uint64_t>(maxnn, b->chunks[c].num_slots);
     uint32_t gx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((maxnn + 255) / 256, 1), 4096);
     if (!gather.empty()) {
-      // the offsets kernels are done with the BYTE_ARRAY list: reuse its slot for the gather list
-      HIPCHECK(hipMemcpyAsync(A + b->l_ba, gather.data(), gather.size() * 4, hipMemcpyHostToDevice, s), err);
+      // its own slot: the BYTE_ARRAY list (l_ba) must stay intact for the next decode of the batch
+      HIPCHECK(hipMemcpyAsync(A + b->l_ba_gather, gather.data(), gather.size() * 4, hipMemcpyHostToDevice, s), err);
       HIPCHECK(timed(b, 6, s, [&] {
-                 return launch_ba_gather_impl(d, (const uint32_t *)(A + b->l_ba), (uint32_t)gather.size(), gx, s);
+                 return launch_ba_gather_impl(d, (const uint32_t *)(A + b->l_ba_gather), (uint32_t)gather.size(), gx, s);
                }),
                err);
       HIPCHECK(launch_dba_gather(d, l, s), err);

@@ -1302,7 +1302,7 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
   for (uint32_t i = 0; i < mbc; i++) {
     uint32_t wi = s[p + i];
     if (wi > (is64 ? 64u : 32u)) { *err = PQ_ERR_INVALID; return false; }
-    w[i] = (uint8_t)wi;
+    if (w) w[i] = (uint8_t)wi;
   }
   *hdr_len = k + 1 + mbc;
   return true;
@@ -1880,7 +1880,7 @@ union ValuesLDS {
   DictLDS dict;
   DeltaTileLDS dtile;        // WI_DELTA_TILE
   DeltaPageLDS dpage;        // WI_DELTA_PAGE
-  uint8_t slow_widths[256];
+
 };
 
 // Length of the block at stream position pos (scalar registers): header varint of at most
@@ -2197,7 +2197,7 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
 
 // Exact scalar restatement of deltaBitPackDecoder.next for pages whose miniblock
 // value count is not a multiple of 8 (deltabp_decoder.go:113-174).
-DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn, uint8_t *widths) {
+DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn) {
   if (threadIdx.x != 0 || nn == 0) return;
   const uint8_t *s = ds.s;
   const uint32_t n = ds.n;
@@ -2206,12 +2206,14 @@ DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn, ui
   uint32_t rpos = ds.hdr;
   int64_t md = 0;
   uint32_t hl, e = 0;
-  if (mbc > 256) { report(b, ds.chunk, 1, ds.page, ST_VALUES, 0, PQ_ERR_UNSUPPORTED); return; }
+  // the miniblock widths are read in place from the stream (any miniblock count the reference
+  // accepts): wpos = the current block's first width byte
   // init(): the first miniblock header was validated on the host; re-read it here
-  if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
+  if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, nullptr, &hl, &e)) {
     report(b, ds.chunk, 0, 0, ST_VALUES, 0, e);
     return;
   }
+  uint32_t wpos = rpos + hl - mbc;
   rpos += hl;
   uint32_t cur_mb = 0, cur_w = 0, mb_pos = 0;  // mb_pos: miniBlockPosition (bytes read in the miniblock)
   int64_t mbv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2222,14 +2224,15 @@ DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn, ui
     if (pos % 8 == 0) {
       if (pos % mbvc == 0) {
         if (cur_mb >= mbc) {
-          if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, widths, &hl, &e)) {
+          if (!delta_hdr(s, s, n, rpos, is64, mbc, &md, nullptr, &hl, &e)) {
             report(b, ds.chunk, 1, ds.page, ST_VALUES, pos, e);
             return;
           }
+          wpos = rpos + hl - mbc;
           rpos += hl;
           cur_mb = 0;
         }
-        cur_w = widths[cur_mb];
+        cur_w = s[wpos + cur_mb];
         mb_pos = 0;
         cur_mb++;
       }
@@ -2293,7 +2296,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
     case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
-    case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn, lds.slow_widths); break;
+    case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
     case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
@@ -2312,7 +2315,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
       ds.out = (uint8_t *)(gp_u64<int32_t>(bd.scratch) + (wi.v0 ? bd.cap : 0u));
       ds.chunk = pd.chunk;
       ds.page = pd.page_in_chunk;
-      if (st.slow) do_delta_slow(b, ds, wi.v1, lds.slow_widths);
+      if (st.slow) do_delta_slow(b, ds, wi.v1);
       else do_delta_page(b, ds, wi.v1, lds.dpage);
       break;
     }

@@ -12,7 +12,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # Fixtures whose every chunk must decode without error (values compared with pyarrow too).
 VALID = ["cfg1", "cfg2_v2_small", "cfg3_small", "cfg4_small", "cfg5_small", "types_v1", "types_v2", "types_dict",
          "edge_nulls_v1", "edge_nulls_v2", "edge_tiny_pages", "edge_delta32", "edge_delta64_wide",
-         "cfg2_snappy_v1", "cfg4_v2", "edge_empty", "dlba_v1", "dba_v2", "dba_v1_snappy"]
+         "cfg2_snappy_v1", "cfg4_v2", "edge_empty", "dlba_v1", "dba_v2", "dba_v1_snappy", "cfg1_full",
+         "cfg3_dict64k", "crc_v1", "crc_v1_flipped"]
 # Fixtures with a known reference error: name -> (error class, data page index or -1 for chunk level).
 EXPECTED_ERRORS = {
     "bad_dict_index": (5, 1),      # dict: invalid index (type_dict.go:52-54) on the 2nd data page

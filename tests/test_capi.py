@@ -85,13 +85,24 @@ def test_host_plan_errors_match_oracle(name):
 
 
 def test_must_not_crash_host():
+    """The reference's fuzz regression images through the host planner: footer errors and
+    readPages errors match the oracle's class (and page)."""
     d = os.path.join(pqtest.GOLDEN, "must_not_crash")
     for fn in sorted(os.listdir(d)):
         data = open(os.path.join(d, fn), "rb").read()
         try:
-            _plan_errors(data)
-        except pqgpu.DecodeError:
-            pass
+            orc = pqtest.oracle_decode(data)
+        except O.OracleError as oe:
+            with pytest.raises(pqgpu.DecodeError) as ei:
+                pqgpu.File(data)
+            assert ei.value.code == oe.code, (fn, ei.value, oe)
+            continue
+        plan = _plan_errors(data)
+        for rg, col, r in orc:
+            e = plan[(rg, col)]
+            if e is not None:
+                assert isinstance(r, O.OracleError), (fn, rg, col, e)
+                assert (e.code, e.page) == (r.code, r.page), (fn, rg, col, e, r)
 
 
 def test_ctx_without_gpu_fails_loudly():

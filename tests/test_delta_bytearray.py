@@ -33,7 +33,7 @@ def _words(rng, n, shared=0.0):
     return out
 
 
-SHAPES = [(128, 4), (256, 8), (128, 1), (128, 32)]  # (block size, miniblocks); 128/32: 4-value miniblocks
+SHAPES = [(128, 4), (256, 8), (128, 1), (128, 32), (4096, 512)]  # (block size, miniblocks); 128/32: 4-value miniblocks
 COUNTS = [2, 7, 8, 100, 128, 130, 1000, 4000]  # 1: no block at all, see dlba_single
 
 
@@ -169,3 +169,62 @@ def test_gpu_valid(gpu_ctx, k, enc, v2):
 def test_gpu_errors(gpu_ctx, name):
     data, _ = BAD[name]
     _compare(_gpu(gpu_ctx, data), data, name)
+
+
+# ---------------------------------------------------------------- FIXED_LEN_BYTE_ARRAY x DELTA_BYTE_ARRAY
+# getFixedLenByteArrayValuesDecoder (chunk_reader.go:64-75) returns byteArrayDeltaDecoder for
+# DELTA_BYTE_ARRAY pages: values of any length (the type length is not checked), so the GPU lays
+# such a chunk out as byte arrays; its PLAIN pages (byteArrayPlainDecoder{length}) and dictionary
+# entries are type_length bytes each.
+
+def _flba_file(v2=False, with_dict=False):
+    rng = np.random.default_rng(91)
+    tl = 12
+    fixed = [bytes(rng.integers(0, 256, tl, dtype=np.uint8)) for _ in range(500)]
+    fixed.sort()
+    ragged = _words(rng, 300, shared=0.6)  # the reference accepts other lengths on DBA pages
+    pages, expect = [], []
+    if with_dict:
+        dvals = fixed[:40]
+        pages.append(rawpq.dict_page_ref("FIXED_LEN_BYTE_ARRAY", dvals, tl))
+        idx = rng.integers(0, 40, 700)
+        body = rawpq.dict_values_section(idx, 40)
+        pages.append(rawpq.data_page_v2_ref(700, 0, 700, "RLE_DICTIONARY", body) if v2
+                     else rawpq.data_page_v1_ref(700, "RLE_DICTIONARY", body))
+        expect += [dvals[i] for i in idx]
+    for vals, enc in ((fixed[:250], "DELTA_BYTE_ARRAY"), (fixed[250:], "PLAIN"), (ragged, "DELTA_BYTE_ARRAY")):
+        body = rawpq.dba_stream(*rawpq.dba_encode(vals)) if enc == "DELTA_BYTE_ARRAY" else \
+            rawpq.plain_encode("FIXED_LEN_BYTE_ARRAY", vals, tl)
+        n = len(vals)
+        pages.append(rawpq.data_page_v2_ref(n, 0, n, enc, body) if v2 else rawpq.data_page_v1_ref(n, enc, body))
+        expect += vals
+    schema = [[(4, rawpq.BIN, "schema"), (5, rawpq.I32, 1)], rawpq.schema_leaf("f", "FIXED_LEN_BYTE_ARRAY", "REQUIRED", tl)]
+    n = len(expect)
+    return rawpq.write_file_schema(schema, [("f", "FIXED_LEN_BYTE_ARRAY")], [(n, [(pages, n, with_dict)])]), expect
+
+
+FLBA_CASES = [(v2, d) for v2 in (False, True) for d in (False, True)]
+
+
+@pytest.mark.parametrize("v2,with_dict", FLBA_CASES)
+def test_oracle_flba_dba(v2, with_dict):
+    data, expect = _flba_file(v2, with_dict)
+    assert _oracle_values(data) == expect
+
+
+def test_host_plans_flba_dba():
+    import pqgpu
+    data, _ = _flba_file()
+    b = pqgpu.Batch(None)
+    cid, e = b.add_file_chunk(pqgpu.File(data), 0, 0)
+    assert e is None, e
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v2,with_dict", FLBA_CASES)
+def test_gpu_flba_dba(gpu_ctx, v2, with_dict):
+    data, expect = _flba_file(v2, with_dict)
+    g = _gpu(gpu_ctx, data)
+    _compare(g, data, f"flba dba v2={v2} dict={with_dict}")
+    assert g.values == expect

@@ -21,6 +21,9 @@ SHAPES = [  # (block size, miniblocks, step bits, typ)
     (1024, 8, 20, "INT64"), (2048, 8, 12, "INT64"), (2048, 1, 63, "INT64"), (128, 1, 9, "INT64"),
     (384, 4, 10, "INT64"), (128, 16, 5, "INT64"), (128, 32, 5, "INT64"),
     (256, 4, 31, "INT32"), (128, 4, 32, "INT32"), (512, 2, 1, "INT32"), (256, 16, 4, "INT32"),
+    # more than 256 miniblocks per block: valid streams the reference decodes (widths are read
+    # in place by the exact scalar path, no per-block width buffer)
+    (4096, 512, 9, "INT64"), (8192, 1024, 5, "INT32"),
 ]
 COUNTS = [2, 8, 9, 100, 129, 255, 256, 258, 1000, 2047, 2049, 5000, 20000]
 

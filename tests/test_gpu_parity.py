@@ -59,14 +59,32 @@ def test_expected_errors(gpu_ctx, name, expected):
 
 
 def test_must_not_crash_gpu(gpu_ctx):
+    """The reference's fuzz regression images: the GPU path must return the oracle's result for
+    every chunk — the same error class on the same page, or the same decoded bytes."""
     import os
     d = os.path.join(pqtest.GOLDEN, "must_not_crash")
+    checked = 0
     for fn in sorted(os.listdir(d)):
         data = open(os.path.join(d, fn), "rb").read()
         try:
-            _gpu_decode(gpu_ctx, data)
-        except pqgpu.DecodeError:
-            pass
+            orc = pqtest.oracle_decode(data)
+        except O.OracleError as oe:
+            with pytest.raises(pqgpu.DecodeError) as ei:
+                pqgpu.File(data)
+            assert ei.value.code == oe.code, (fn, ei.value, oe)
+            continue
+        gpu = _gpu_decode(gpu_ctx, data)
+        for rg, col, r in orc:
+            g = gpu[(rg, col)]
+            where = f"{fn} rg{rg} col{col}"
+            if isinstance(r, O.OracleError):
+                assert isinstance(g, pqgpu.DecodeError), f"{where}: oracle error {r} but GPU decoded"
+                assert (g.code, g.page) == (r.code, r.page), f"{where}: {g} vs {r}"
+            else:
+                assert not isinstance(g, pqgpu.DecodeError), f"{where}: GPU error {g}"
+                pqtest.assert_chunk_equal(g, r, where)
+            checked += 1
+    assert checked > 0
 
 
 def test_file_reader_mirror(gpu_ctx):
@@ -115,3 +133,38 @@ def test_chunk_page_split(gpu_ctx):
                 want = int((dl[s0:s0 + sn] == r.max_def).sum()) if r.max_def > 0 else sn
                 assert vn == want, (name, rg, c)
         b.close()
+
+
+def test_repeated_decode_with_failed_byte_array_chunk(gpu_ctx):
+    """A batch decoded twice (the benchmark's pattern) whose first BYTE_ARRAY chunk fails on the
+    device (dictionary index out of range, type_dict.go:52-54) and whose second decodes: the good
+    chunk must be identical after both decodes, and the bad one must keep its error."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
+    import rawpq
+    rng = np.random.default_rng(5)
+    vocab = sorted({bytes(rng.integers(97, 123, int(rng.integers(1, 30)), dtype=np.uint8)) for _ in range(200)})
+    n = 5000
+    cols = []
+    for bad in (True, False):
+        idx = rng.integers(0, len(vocab), n)
+        if bad:
+            idx[3000] = len(vocab) + 3  # fits the 8-bit width, past the dictionary
+        pages = [rawpq.dict_page_ref("BYTE_ARRAY", vocab),
+                 rawpq.data_page_v1_ref(n, "RLE_DICTIONARY", rawpq.dict_values_section(idx, len(vocab)))]
+        cols.append((pages, n, True))
+    schema = [[(4, rawpq.BIN, "schema"), (5, rawpq.I32, 2)], rawpq.schema_leaf("bad", "BYTE_ARRAY", "REQUIRED"),
+              rawpq.schema_leaf("good", "BYTE_ARRAY", "REQUIRED")]
+    data = rawpq.write_file_schema(schema, [("bad", "BYTE_ARRAY"), ("good", "BYTE_ARRAY")], [(n, cols)])
+    orc = pqtest.oracle_decode(data)
+    assert isinstance(orc[0][2], O.OracleError) and orc[0][2].code == pqgpu.PQ_ERR_DICT_INDEX
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = [b.add_file_chunk(f, 0, c)[0] for c in range(2)]
+    for _ in range(3):
+        b.decode()
+        e = b.sync()
+        assert e is not None and (e.code, e.page) == (orc[0][2].code, orc[0][2].page)
+        pqtest.assert_chunk_equal(b.result(ids[1]), orc[1][2], "good chunk")
+    b.close()

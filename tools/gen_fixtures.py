@@ -89,6 +89,42 @@ def cfg3(n=120_000, k=4096, page_rows=None):
     return write(t, **kw)
 
 
+def cfg1_full():
+    # cfg1 exactly as BASELINE.json configs[0] / SURVEY §8(d): 1,048,576 rows, 8 pages of 131,072
+    return cfg1(1_048_576, 131_072)
+
+
+def cfg3_dict64k(n=262_144, k=65_536, page_rows=65_536):
+    # cfg3's defining shape: a 65,536-entry BYTE_ARRAY dictionary (lengths 4-28, mean 16) with
+    # 16-bit indices. The first k rows are a permutation of the vocabulary, so every entry is
+    # used and pyarrow's index width is bit_width(k - 1) = 16 (seed 4).
+    rng = np.random.default_rng(4)
+    vocab = np.array(words(rng, k), dtype=object)
+    idx = np.concatenate([rng.permutation(k), rng.integers(0, k, n - k)])
+    t = pa.table({"s": pa.array(list(vocab[idx]), pa.string())},
+                 schema=pa.schema([pa.field("s", pa.string(), nullable=False)]))
+    return write(t, use_dictionary=True, data_page_version="1.0", compression="NONE",
+                 dictionary_pagesize_limit=8 << 20, max_rows_per_page=page_rows)
+
+
+def crc_files():
+    """Page checksums (pyarrow write_page_checksum; checked with WithCRC32Validation,
+    file_reader.go:134-139, chunk_reader.go:173-177): a valid file, and the same file with one
+    value byte of the second data page of column `a` flipped (still decodable without the
+    check; CRC32 check failed on that page with it)."""
+    rng = np.random.default_rng(31)
+    n = 20_000
+    t = pa.table({"a": pa.array(rng.integers(0, 1 << 40, n, dtype=np.int64), mask=rng.random(n) < 0.1),
+                  "s": pa.array(["v%d" % (i % 37) for i in range(n)])})
+    good = write(t, data_page_version="1.0", compression="NONE", use_dictionary=["s"], max_rows_per_page=4096,
+                 write_page_checksum=True)
+    buf = bytearray(good)
+    ph, j = [(ph, j) for ph, j in pqinspect.pages(good) if ph[1] == 0][1]
+    csize = ph[3]
+    buf[j + csize - 5] ^= 0x5A  # a PLAIN value byte near the end of the page
+    return {"crc_v1": good, "crc_v1_flipped": bytes(buf)}
+
+
 def cfg4(n=20_000, version="1.0", seed=5):
     # LIST<INT32> + MAP<BYTE_ARRAY, INT64> (seed 5)
     rng = np.random.default_rng(seed)
@@ -330,6 +366,9 @@ def main():
         "types_v2": types_v("2.0"),
         "types_dict": types_dict(),
     }
+    files["cfg1_full"] = cfg1_full()
+    files["cfg3_dict64k"] = cfg3_dict64k()
+    files.update(crc_files())
     files.update(edge_cases())
     files.update(delta_ba())
     files.update(corrupt(files))

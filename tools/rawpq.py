@@ -93,8 +93,12 @@ def hybrid_bitpacked(levels, bw):
     return uvar((g << 1) | 1) + bitpack(padded, bw)
 
 
-def delta_encode(vals, bs=128, mbc=4, bits=64, trailing_width=0, min_delta_override=None):
+def delta_encode(vals, bs=128, mbc=4, bits=64, trailing_width=0, min_delta_override=None, ref_single=False):
     """DELTA_BINARY_PACKED stream of `vals` (python ints, wrapped to `bits`).
+
+    ref_single: a single value gets one empty block (minDelta MaxInt32, all widths 0), as the
+    reference writer flushes it (deltaBitPackEncoder.write deltabp_encoder.go:139-144); the
+    reader's look-ahead needs that header (App. A Q1).
 
     trailing_width: width byte written for miniblocks of the last block that hold no
     delta (the spec lets writers put anything there). min_delta_override: force every
@@ -111,6 +115,8 @@ def delta_encode(vals, bs=128, mbc=4, bits=64, trailing_width=0, min_delta_overr
     if not vals:
         return bytes(out + uvar(0))
     out += uvar(zz64(s(vals[0])))
+    if ref_single and len(vals) == 1:
+        return bytes(out + uvar(zz64((1 << 31) - 1)) + bytes(mbc))
     deltas = [s(vals[i] - vals[i - 1]) for i in range(1, len(vals))]
     for b0 in range(0, len(deltas), bs):
         blk = deltas[b0:b0 + bs]
@@ -348,3 +354,135 @@ def page_v2c(values_bytes, num_values, num_nulls, num_rows, encoding, def_bytes=
     hdr = tstruct([(1, I32, 3), (2, I32, len(def_bytes) + len(values_bytes)),
                    (3, I32, len(def_bytes) + len(cvals)), (8, STRUCT, dph)])
     return hdr + def_bytes + cvals
+
+
+# ---------------------------------------------------------------- reference-writer-style files
+# The reference writer (fraugster/parquet-go) emits every hybrid stream as ONE bit-packed run
+# (hybridEncoder.bpEncode hybrid_encoder.go:55-70), level bit width bits.Len16(max)
+# (helpers.go:262-290), dictionary index width bits.Len(len(dict)) (page_v1.go:185,
+# page_v2.go:200) and DELTA blocks of 128 values in 4 miniblocks. The helpers below build pages
+# in that shape (and nested schemas, dictionary pages, page CRCs) so the GPU's dictionary and
+# level paths see the reference's own stream layout.
+
+TYPES.update({"BOOLEAN": 0, "INT96": 3, "FLOAT": 4, "FIXED_LEN_BYTE_ARRAY": 7})
+ENC.update({"PLAIN_DICTIONARY": 2, "RLE_DICTIONARY": 8})
+REP = {"REQUIRED": 0, "OPTIONAL": 1, "REPEATED": 2}
+
+
+def hybrid_ref(vals, bw):
+    """hybridEncoder: one bit-packed run of all values (nothing at bit width 0)."""
+    return b"" if bw == 0 else hybrid_bitpacked(list(vals), bw)
+
+
+def levels_v1_ref(levels, max_level):
+    """encodeLevelsV1: u32 byte length + hybrid_ref at bits.Len16(max)."""
+    st = hybrid_ref(levels, int(max_level).bit_length())
+    return struct.pack("<I", len(st)) + st
+
+
+def plain_encode(typ, vals, type_length=0):
+    """PLAIN values section (type_*.go encoders): LE fixed width, BOOLEAN LSB-first bits,
+    BYTE_ARRAY u32 length + bytes, FIXED_LEN_BYTE_ARRAY raw bytes."""
+    if typ == "INT32":
+        return np.asarray(vals, "<i4").tobytes()
+    if typ == "INT64":
+        return np.asarray(vals, "<i8").tobytes()
+    if typ == "FLOAT":
+        return np.asarray(vals, "<f4").tobytes()
+    if typ == "DOUBLE":
+        return np.asarray(vals, "<f8").tobytes()
+    if typ == "BOOLEAN":
+        bits = np.zeros(-(-len(vals) // 8) * 8, np.uint8)
+        bits[:len(vals)] = np.asarray(vals, bool)
+        return np.packbits(bits, bitorder="little").tobytes()
+    if typ == "BYTE_ARRAY":
+        return b"".join(struct.pack("<I", len(v)) + bytes(v) for v in vals)
+    if typ == "FIXED_LEN_BYTE_ARRAY":
+        assert all(len(v) == type_length for v in vals)
+        return b"".join(bytes(v) for v in vals)
+    raise ValueError(typ)
+
+
+def _page(ptype, body, hdr_field, hdr_struct, crc=False, usize=None):
+    import zlib
+    f = [(1, I32, ptype), (2, I32, len(body) if usize is None else usize), (3, I32, len(body))]
+    if crc:
+        c = zlib.crc32(body) & 0xFFFFFFFF
+        f.append((4, I32, c - (1 << 32) if c >= 1 << 31 else c))
+    f.append((hdr_field, STRUCT, hdr_struct))
+    return tstruct(f) + body
+
+
+def dict_page_ref(typ, entries, type_length=0, crc=False):
+    """DICTIONARY_PAGE with PLAIN entries (page_dict.go:74-136)."""
+    return _page(2, plain_encode(typ, entries, type_length), 7, [(1, I32, len(entries)), (2, I32, ENC["PLAIN"])], crc)
+
+
+def data_page_v1_ref(num_values, encoding, values_section, def_levels=None, max_def=0, rep_levels=None, max_rep=0,
+                     crc=False):
+    """DATA_PAGE: [rep: u32 + hybrid] [def: u32 + hybrid] values (page_v1.go:124-231)."""
+    body = b""
+    if max_rep > 0:
+        body += levels_v1_ref(rep_levels, max_rep)
+    if max_def > 0:
+        body += levels_v1_ref(def_levels, max_def)
+    body += values_section
+    dph = [(1, I32, num_values), (2, I32, ENC[encoding]), (3, I32, ENC["RLE"]), (4, I32, ENC["RLE"])]
+    return _page(0, body, 5, dph, crc)
+
+
+def data_page_v2_ref(num_values, num_nulls, num_rows, encoding, values_section, def_levels=None, max_def=0,
+                     rep_levels=None, max_rep=0, crc=False):
+    """DATA_PAGE_V2: rep and def hybrid streams without length prefix, then values (page_v2.go:133-255)."""
+    rep = hybrid_ref(rep_levels, int(max_rep).bit_length()) if max_rep > 0 else b""
+    dfn = hybrid_ref(def_levels, int(max_def).bit_length()) if max_def > 0 else b""
+    body = rep + dfn + values_section
+    dph = [(1, I32, num_values), (2, I32, num_nulls), (3, I32, num_rows), (4, I32, ENC[encoding]),
+           (5, I32, len(dfn)), (6, I32, len(rep)), (7, BOOL, False)]
+    return _page(3, body, 8, dph, crc)
+
+
+def dict_values_section(indices, dict_len):
+    """RLE_DICTIONARY values section as the reference writes it: 1 byte bit width
+    bits.Len(len(dict)), then one bit-packed run (dictEncoder, type_dict.go)."""
+    bw = int(dict_len).bit_length()
+    return bytes([bw]) + hybrid_ref(indices, bw)
+
+
+def schema_group(name, rep, num_children):
+    return [(3, I32, REP[rep]), (4, BIN, name), (5, I32, num_children)]
+
+
+def schema_leaf(name, typ, rep, type_length=None):
+    return [(1, I32, TYPES[typ]), (2, I32, type_length), (3, I32, REP[rep]), (4, BIN, name)]
+
+
+def write_file_schema(schema, leaves, row_groups, codec=0):
+    """schema: SchemaElement field lists in depth-first order (root first, with num_children);
+    leaves: [(dotted path, type)] in column order; row_groups: [(num_rows, [(pages, num_values,
+    has_dict) per leaf])] where pages are whole page byte strings (a dictionary page first when
+    has_dict). Returns the file bytes."""
+    out = bytearray(b"PAR1")
+    rgs = []
+    for num_rows, chunks in row_groups:
+        ccs, total = [], 0
+        for (path, typ), (pages, nv, has_dict) in zip(leaves, chunks):
+            off = len(out)
+            data_off = off
+            for k, p in enumerate(pages):
+                if k == 1 and has_dict:
+                    data_off = len(out)
+                out += p
+            size = len(out) - off
+            total += size
+            md = [(1, I32, TYPES[typ]), (2, LIST, (I32, [0, 3, 8] if has_dict else [0, 3])),
+                  (3, LIST, (BIN, path.split("."))), (4, I32, codec), (5, I64, nv), (6, I64, size), (7, I64, size),
+                  (9, I64, data_off)]
+            if has_dict:
+                md.append((11, I64, off))
+            ccs.append([(2, I64, off), (3, STRUCT, md)])
+        rgs.append([(1, LIST, (STRUCT, ccs)), (2, I64, total), (3, I64, num_rows)])
+    fmd = tstruct([(1, I32, 1), (2, LIST, (STRUCT, schema)), (3, I64, sum(r[0] for r in row_groups)),
+                   (4, LIST, (STRUCT, rgs)), (6, BIN, "rawpq reference-style writer")])
+    out += fmd + struct.pack("<I", len(fmd)) + b"PAR1"
+    return bytes(out)
