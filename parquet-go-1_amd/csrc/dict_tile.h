@@ -1,0 +1,142 @@
+// dict_tile.h — the values of one tile of a hybrid-encoded VALUE stream (dictionary indices,
+// type_dict.go:40-60; boolean RLE, type_boolean.go:109-120), for the kernels that consume
+// them (k_values WI_DICT, k_ba_sums, k_ba_emit).
+//
+// k_scan_runs has already walked the page's run-header chain (hybrid_decoder.go:142-165) into
+// a run table (HybRun: first value, payload position, RLE value / bit-packed flag) with the run
+// covering the first value of every kDictTile-value tile. A tile load copies the tile's runs to
+// LDS and stages the stream bytes the tile's bit-packed values occupy (one coalesced sweep of
+// 16-B loads; bytes at or past the stream end read as zero, the short-final-group zero fill of
+// hybrid_decoder.go:132-140). Values are then read by lanes in any order: a per-lane run cursor
+// advances monotonically, and each bit-packed value is one LDS funnel read.
+#pragma once
+#include "dev_util.h"
+
+namespace pq {
+
+constexpr uint32_t kTileRuns = 1024;      // runs held in LDS (a tile with more reads the run table)
+constexpr uint32_t kTileStageB = 16896;   // staged stream bytes (a wider tile reads global memory)
+
+struct DictTileLDS {
+  HybRun runs[kTileRuns];
+  uint32_t stage[kTileStageB / 4 + 8];
+};
+
+struct DictTile {
+  const uint8_t *s;      // value stream (after the bit-width byte)
+  uint32_t n, bw;        // stream bytes, index bit width
+  const HybRun *runs;    // the tile's runs: LDS copy, or the run table in global memory
+  uint32_t nr;           // number of runs
+  uint64_t sbit;         // stream bit of stage[0] (staged)
+  uint32_t v0, v1;       // tile values [v0, v1) after clipping to the runs the scan validated
+  bool staged;
+};
+
+// Open tile [v0, v1) of page `page` (values within the page) without staging: the tile's runs
+// are read from the run table in global memory. Returns false when no value of the tile is
+// decodable (the scan failed before it: the error is already reported at the right value
+// position). Any lane may call it.
+DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
+                        DictTile &t, uint32_t &r0, uint32_t &r1) {
+  t.s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
+  t.n = pd.val_len;
+  t.bw = pd.dict_bw;
+  t.nr = 0;
+  t.staged = false;
+  t.runs = nullptr;
+  t.sbit = 0;
+  t.v0 = v0;
+  t.v1 = v1;
+  if (t.bw == 0) return v0 < v1;  // bit width 0: every index is 0 and no stream is read
+  const uint32_t nruns = b.run_count[page];
+  if (nruns == 0) return false;
+  const HybRun *rg = b.runs + b.run_base[page];
+  const uint32_t *tf = b.tile_first + b.tile_base[page];
+  const uint32_t tile = v0 / kDictTile;
+  r0 = tf[tile];
+  if (r0 >= nruns) return false;
+  r1 = ((uint64_t)(tile + 1) * kDictTile < nn) ? tf[tile + 1] : nruns - 1;
+  if (r1 >= nruns) r1 = nruns - 1;
+  t.v1 = min(v1, rg[nruns].value_start);  // sentinel: values covered by valid runs
+  if (t.v0 >= t.v1) return false;
+  t.nr = r1 - r0 + 1;
+  t.runs = rg + r0;
+  return true;
+}
+
+// Load tile [v0, v1) of page `page`: dict_tile_open, then the runs (up to kTileRuns) and the
+// stream bytes of the tile's bit-packed values are staged in LDS. Every thread of the workgroup
+// calls it; it ends with a barrier unless it returns false or the bit width is 0 (both
+// workgroup-uniform).
+DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
+                        DictTileLDS &L, DictTile &t) {
+  uint32_t r0 = 0, r1 = 0;
+  if (!dict_tile_open(b, pd, page, v0, v1, nn, t, r0, r1)) return false;
+  if (t.bw == 0) return true;
+  const HybRun *rg = b.runs + b.run_base[page];
+  if (t.nr <= kTileRuns) {
+    for (uint32_t k = threadIdx.x; k < t.nr; k += blockDim.x) L.runs[k] = rg[r0 + k];
+    t.runs = L.runs;
+  }
+  // stream bytes of the tile's bit-packed values: from the first value's byte to the last's
+  const HybRun f = rg[r0], l = rg[r1];
+  const uint32_t bw = t.bw;
+  uint64_t lo = (f.info & 0x80000000u) ? (uint64_t)f.payload_off + (((uint64_t)(t.v0 - f.value_start) * bw) >> 3)
+                                       : (uint64_t)f.payload_off;
+  uint64_t hi = (l.info & 0x80000000u) && t.v1 > l.value_start
+                    ? (uint64_t)l.payload_off + (((uint64_t)(t.v1 - l.value_start) * bw + 7) >> 3)
+                    : (uint64_t)l.payload_off + 8;
+  hi = min(hi, (uint64_t)t.n);
+  const uintptr_t ga = ((uintptr_t)(t.s + lo)) & ~(uintptr_t)15;  // 16-B aligned global start
+  const uint64_t sb = (uint64_t)(ga - (uintptr_t)t.s);             // its stream offset (may be "negative")
+  const uint64_t span = hi > lo ? (hi + 8) - (lo & ~(uint64_t)15) + 16 : 0;
+  if (span <= kTileStageB) {
+    t.staged = true;
+    t.sbit = sb * 8;
+    const uint4 *src = (const uint4 *)gp_u64<const uint8_t>((uint64_t)ga);
+    const uint32_t nv = (uint32_t)((span + 15) / 16);
+    for (uint32_t k = threadIdx.x; k < nv; k += blockDim.x) {
+      uint4 x = src[k];
+      // zero the bytes at or past the stream end (stream offset sb + 16k + j >= n)
+      const int64_t rel = (int64_t)t.n - (int64_t)(sb + 16ull * k);  // stream bytes left at this block
+      if (rel < 16) {
+        uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int64_t r = rel - 4 * q;
+          w[q] = r >= 4 ? w[q] : (r <= 0 ? 0u : (w[q] & ((1u << (8 * r)) - 1u)));
+        }
+        x = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *(uint4 *)&L.stage[4 * k] = x;
+    }
+    if (threadIdx.x < 8) L.stage[4 * nv + threadIdx.x] = 0;  // funnel reads past the last block
+  }
+  wg_barrier();
+  return true;
+}
+
+// The run of value v: binary search over the tile's runs (first value of a lane).
+DEV uint32_t dict_tile_seek(const DictTile &t, uint32_t v) {
+  if (t.bw == 0) return 0;
+  uint32_t lo = 0, hi = t.nr;
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (t.runs[m].value_start <= v) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+// Index of value v (v inside [t.v0, t.v1)); `ri` is the lane's run cursor (values visited by a
+// lane must not decrease).
+DEV uint32_t dict_tile_value(const DictTile &t, const DictTileLDS &L, uint32_t &ri, uint32_t v) {
+  if (t.bw == 0) return 0;
+  while (ri + 1 < t.nr && t.runs[ri + 1].value_start <= v) ri++;
+  const HybRun r = t.runs[ri];
+  if (!(r.info & 0x80000000u)) return r.info;
+  const uint64_t bo = (uint64_t)r.payload_off * 8 + (uint64_t)(v - r.value_start) * t.bw;
+  if (t.staged) return (uint32_t)lds_bits64(L.stage, (uint32_t)(bo - t.sbit), t.bw);
+  return bits32c(t.s, t.n, bo, t.bw);
+}
+
+}  // namespace pq

@@ -195,6 +195,43 @@ int delta32_walk(GoReader &r, DeltaWalk *w, std::string *msg) {
   return PQ_OK;
 }
 
+// dictPageReader.read (page_dict.go:35-72) -> byteArrayPlainDecoder.decodeValues of `count`
+// entries (type_bytearray.go:24-55): a u32 length read with io.ReadFull (EOF when no byte is
+// left, else ErrUnexpectedEOF), a negative length is "len is negative", then io.ReadFull of the
+// bytes (a zero-length entry reads nothing). Records (position, length) of every entry; the
+// whole dictionary is read when the chunk is (readPages), so a failure is the chunk's error.
+int walk_ba_dict(const uint8_t *p, int64_t n, uint32_t count, int32_t fixed, std::vector<uint32_t> *ent,
+                 uint32_t *max_len, std::string *msg) {
+  ent->assign(2 * (size_t)count, 0);
+  int64_t i = 0;
+  uint32_t mx = 0;
+  auto fail = [&](uint32_t v, int code) {
+    *msg = "expected " + std::to_string(count) + " values, read " + std::to_string(v) + " values: " +
+           (code == PQ_ERR_EOF ? "EOF" : code == PQ_ERR_UNEXPECTED_EOF ? "unexpected EOF" : "bytearray/plain: len is negative");
+    return code;
+  };
+  for (uint32_t v = 0; v < count; v++) {
+    int64_t l = fixed;
+    if (fixed == 0) {
+      if (i >= n) return fail(v, PQ_ERR_EOF);
+      if (i + 4 > n) return fail(v, PQ_ERR_UNEXPECTED_EOF);
+      int32_t x;
+      memcpy(&x, p + i, 4);
+      i += 4;
+      if (x < 0) return fail(v, PQ_ERR_INVALID);
+      l = x;
+    }
+    if (l > 0 && i >= n) return fail(v, PQ_ERR_EOF);
+    if (i + l > n) return fail(v, PQ_ERR_UNEXPECTED_EOF);
+    (*ent)[2 * (size_t)v] = (uint32_t)i;
+    (*ent)[2 * (size_t)v + 1] = (uint32_t)l;
+    mx = std::max<uint32_t>(mx, (uint32_t)l);
+    i += l;
+  }
+  *max_len = mx;
+  return PQ_OK;
+}
+
 struct HostChunk {
   pqgpu_column_info col{};
   pqgpu_chunk_meta meta{};
@@ -206,10 +243,21 @@ struct HostChunk {
   uint64_t dict_off = 0;  // stage offset
   uint32_t dict_len = 0, dict_count = 0;
   // device outputs (offsets into the arena)
-  uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0,
-           o_dict_offsets = 0;
+  uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0;
+  // byte-array dictionaries: (position, length) of every entry, from the host's walk of the
+  // dictionary page (page_dict.go:35-72 + byteArrayPlainDecoder type_bytearray.go:24-55)
+  std::vector<uint32_t> dict_ent;
+  uint64_t dict_ent_off = 0;  // stage offset of dict_ent
+  uint32_t dict_max_len = 0;
+  bool ba_sync = false;       // no upload-time payload bound: size it after the scan (host sync)
+  uint64_t payload_off = 0;   // offset in the batch payload arena (bounded chunks)
+  uint64_t payload_bound = 0; // its size (k_ba_emit writes nothing past it)
   uint64_t payload_cap = 0;
-  uint8_t *payload = nullptr;  // separately allocated (size known after the offsets scan)
+  uint8_t *payload = nullptr;  // the chunk's payload (arena slice, or own allocation when ba_sync)
+  bool payload_own = false;
+  bool sync_err = false;      // ba_sync chunk whose payload exceeded 2 GiB at the last decode
+  uint32_t slot_shift = 0;    // dictionary slot table (k_dict_slots): log2 slot bytes, 0 = none
+  uint64_t o_slots = 0;
   // results after sync
   int64_t nn = 0, records = 0, payload_bytes = 0;
   pqgpu_error dev_err{};
@@ -323,8 +371,9 @@ struct KernelTimer {
   }
 };
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
-    "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_dict_ba", "k_ba_offsets",
-    "k_ba_gather", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy"};
+    "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
+    "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
+    "(unused)", "(unused)", "(unused)"};
 
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
@@ -353,7 +402,7 @@ struct pqgpu_batch {
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
   uint32_t n_delta_tiles = 0;
-  std::vector<uint32_t> level_pages, scan_pages, base_chunks, dict_ba_chunks, ba_chunks, rec_pages;
+  std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages;
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
   std::vector<uint32_t> page_nn_init;
@@ -367,9 +416,15 @@ struct pqgpu_batch {
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  std::vector<uint64_t> ba_tile_off;
-  uint64_t ba_tiles_total = 0;
-  uint32_t ba_max_tiles = 0;
+  std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
+  std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
+  uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
+  uint32_t n_ba_class[3] = {0, 0, 0};  // tiles per k_ba_emit class
+  std::vector<uint32_t> slot_chunks;   // byte-array dictionaries materialised in slots
+  uint32_t slot_grid_x = 0;
+  bool any_ba_sync = false;
+  uint8_t *d_payload = nullptr;         // payload arena of the bounded byte-array chunks
+  size_t d_payload_cap = 0;
   // device
   uint8_t *d_stage = nullptr;
   size_t d_stage_cap = 0;
@@ -382,9 +437,10 @@ struct pqgpu_batch {
   uint64_t o_nnv = 0, o_spec_flag = 0, o_dblk = 0, o_dblk_base = 0, o_dblk_n = 0, o_dblk_sum = 0, l_delta = 0;
   uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
-           o_ba_tile_sum = 0, o_ba_tile_off = 0, o_ba_totals = 0;
+           o_ba_tile_sum = 0, o_ba_tile_page = 0, o_ba_tile_order = 0, o_ba_totals = 0, l_slot = 0,
+           o_ba_state = 0;
   uint64_t l_level_bw1 = 0;
-  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_dict_ba = 0, l_ba = 0, l_ba_gather = 0, l_rec = 0;
+  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   uint32_t n_delta_items = 0;
   uint64_t o_dbg = 0;
@@ -393,7 +449,7 @@ struct pqgpu_batch {
   bool uploaded = false, decoded = false;
   pqgpu_batch_stats stats{};
   KernelTimer timer;
-  std::vector<uint8_t *> payload_allocs;
+  int64_t slot_bytes[PQGPU_TIMER_SLOTS] = {0};  // algorithmic bytes per launch of each timer slot
 };
 
 // ---------------------------------------------------------------------------
@@ -652,6 +708,11 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       hc.dict_len = (uint32_t)block.size();
       hc.dict_off = stage_append(b, block.data(), (int64_t)block.size());
       int w = hc.value_width;
+      if (w == 0) {  // BYTE_ARRAY: byteArrayPlainDecoder.next per entry (type_bytearray.go:24-45)
+        std::string dm;
+        int de = walk_ba_dict(block.data(), (int64_t)block.size(), hc.dict_count, 0, &hc.dict_ent, &hc.dict_max_len, &dm);
+        if (de) return chunk_fail(b, hc, id, de, -1, dm, err);
+      }
       if (w > 0) {  // fixed width PLAIN dictionary: binary.Read per entry
         uint64_t need = (uint64_t)w * hc.dict_count;
         if (need > block.size()) {
@@ -826,8 +887,18 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       hc.value_width = 0;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
         if (b->pages[p].vkind == VK_PLAIN_FIXED) b->pages[p].vkind = VK_PLAIN_BA;
+      if (hc.has_dict) {  // entries of type_length bytes (validated above as a fixed-width dictionary)
+        hc.dict_ent.resize(2 * (size_t)hc.dict_count);
+        for (uint32_t k = 0; k < hc.dict_count; k++) {
+          hc.dict_ent[2 * k] = k * (uint32_t)col->type_length;
+          hc.dict_ent[2 * k + 1] = (uint32_t)col->type_length;
+        }
+        hc.dict_max_len = (uint32_t)col->type_length;
+      }
     }
   }
+  if (!hc.dict_ent.empty())
+    hc.dict_ent_off = stage_append(b, (const uint8_t *)hc.dict_ent.data(), (int64_t)hc.dict_ent.size() * 4);
   b->stats.host_decompress_ms += decomp_ms;
   b->stats.host_plan_ms +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - decomp_ms;
@@ -848,16 +919,18 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->dblk_total = 0;
   b->scan_pages.clear();
   b->base_chunks.clear();
-  b->dict_ba_chunks.clear();
   b->ba_chunks.clear();
   b->rec_pages.clear();
   b->run_base.assign(np, 0);
   b->tile_base.assign(np, 0);
   b->page_nn_init.assign(np, 0);
-  b->ba_tile_off.clear();
+  b->ba_tile_page.clear();
+  b->ba_tile_order.clear();
+  b->slot_chunks.clear();
+  b->slot_grid_x = 0;
+  b->any_ba_sync = false;
   b->run_total = b->tile_total = 0;
-  b->ba_tiles_total = 0;
-  b->ba_max_tiles = 0;
+  uint64_t payload_arena = 0;  // bytes of the bounded byte-array chunks' payload arena
   uint64_t a = 256;  // offset 0 is reserved: a zero offset means "not allocated"
   auto take = [&](uint64_t bytes) {
     uint64_t o = align_up(a, 256);
@@ -874,6 +947,14 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
   b->o_spec_flag = take(4);
+  uint64_t n_ba_tiles = 0;  // byte-array tiles (for the look-back state, zeroed per decode)
+  for (uint32_t c = 0; c < nc; c++) {
+    const HostChunk &hc = b->chunks[c];
+    if (hc.err.code || hc.value_width != 0) continue;
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
+      n_ba_tiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
+  }
+  b->o_ba_state = take(n_ba_tiles * 128);  // one 128-B line per tile (bytearray.hip kStStride)
   b->z_end = a;
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -886,19 +967,41 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     hc.o_rep = hc.col.max_rep > 0 ? take(ns) : 0;
     hc.o_lists = hc.col.max_rep > 0 ? take((ns + 1) * 4) : 0;
     hc.o_offsets = is_ba ? take((ns + 1) * 4) : 0;
-    hc.o_ba_index = is_ba ? take(ns * 8) : 0;
-    hc.o_dict_offsets = (hc.has_dict && is_ba) ? take((uint64_t)hc.dict_count * 8) : 0;
+    hc.o_ba_index = 0;
     b->base_chunks.push_back(c);
-    if (hc.has_dict) {
-      in_bytes += hc.dict_len;
-      if (is_ba) b->dict_ba_chunks.push_back(c);
-    }
+    if (hc.has_dict) in_bytes += hc.dict_len;
+    uint64_t bound = 0;  // byte-array payload upper bound (k_ba_emit writes no more)
+    hc.ba_sync = false;
     if (is_ba) {
       b->ba_chunks.push_back(c);
-      uint64_t nt = (ns + kBaTile - 1) / kBaTile;
-      b->ba_tile_off.push_back(b->ba_tiles_total);
-      b->ba_tiles_total += std::max<uint64_t>(nt, 1);
-      b->ba_max_tiles = std::max<uint32_t>(b->ba_max_tiles, (uint32_t)std::max<uint64_t>(nt, 1));
+      bool srcs = false;  // pages whose value kernels record a source address per value
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+        PageDesc &pd = b->pages[p];
+        pd.ba_tile = (uint32_t)b->ba_tile_page.size();
+        for (uint32_t k = 0; k < (pd.num_slots + kBaTile - 1) / kBaTile; k++) b->ba_tile_page.push_back(p);
+        switch (pd.vkind) {
+          case VK_DICT: bound += (uint64_t)pd.num_slots * hc.dict_max_len; break;
+          case VK_PLAIN_BA: bound += pd.val_len; srcs = true; break;
+          case VK_DLBA: bound += b->ba_delta[pd.ba_delta].pay_len; srcs = true; break;
+          default: hc.ba_sync = true; srcs = true; break;  // DELTA_BYTE_ARRAY: prefixes repeat bytes
+        }
+      }
+      if (bound > 0x7fffffffULL - 64) hc.ba_sync = true;
+      hc.o_ba_index = srcs ? take(ns * 8) : 0;
+      hc.slot_shift = 0;
+      hc.o_slots = 0;
+      if (hc.has_dict && hc.dict_count && hc.dict_max_len <= 60) {  // slot table (k_dict_slots)
+        hc.slot_shift = hc.dict_max_len <= 12 ? 4 : hc.dict_max_len <= 28 ? 5 : 6;  // [u32 len | bytes]
+        hc.o_slots = take((uint64_t)hc.dict_count << hc.slot_shift);
+        b->slot_chunks.push_back(c);
+        b->slot_grid_x = std::max<uint32_t>(b->slot_grid_x, std::min<uint32_t>((hc.dict_count + 255) / 256, 1024));
+      }
+      if (!hc.ba_sync) {
+        hc.payload_off = payload_arena;
+        hc.payload_bound = bound;
+        payload_arena = align_up(payload_arena + bound + 64, 256);
+      }
+      b->any_ba_sync |= hc.ba_sync;
     }
     for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
       PageDesc &pd = b->pages[p];
@@ -923,7 +1026,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
             b->tile_base[p] = b->tile_total;
             b->tile_total += (ns_p + kDictTile - 1) / kDictTile;
           }
-          tiles(WI_DICT, kDictTile);
+          if (!is_ba) tiles(WI_DICT, kDictTile);  // byte-array dictionaries: k_ba_sums / k_ba_emit
           break;
         }
         case VK_DELTA32: case VK_DELTA64:
@@ -954,6 +1057,35 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           break;
         }
       }
+    }
+  }
+  // k_ba_emit block order: class 0 / 1 = chunks whose pages are all dictionary pages with a
+  // slot table of 16/32-byte / 64-byte slots, class 2 = the rest. Within a class, chunk c's
+  // tiles (in order) go to queue c mod 8 and block b takes tile b / 8 of queue b mod 8: blocks
+  // are dispatched round-robin over the 8 XCDs, so the chunk's dictionary, slot table and index
+  // streams stay in one XCD's L2, and a tile's predecessors have lower block indices.
+  b->n_ba_class[0] = b->n_ba_class[1] = b->n_ba_class[2] = 0;
+  if (!b->ba_tile_page.empty()) {
+    std::vector<std::vector<uint32_t>> q(24);
+    std::vector<int8_t> cls(nc, -1);
+    for (uint32_t c : b->ba_chunks) {
+      const HostChunk &hc = b->chunks[c];
+      bool slot_only = hc.slot_shift != 0 && !hc.ba_sync;
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) slot_only &= b->pages[p].vkind == VK_DICT;
+      cls[c] = slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
+    }
+    for (uint32_t t = 0; t < (uint32_t)b->ba_tile_page.size(); t++) {
+      const uint32_t c = b->pages[b->ba_tile_page[t]].chunk;
+      q[8 * cls[c] + c % 8].push_back(t);
+    }
+    for (uint32_t k = 0; k < 3; k++) {
+      size_t m = 0;
+      for (uint32_t x = 0; x < 8; x++) m = std::max(m, q[8 * k + x].size());
+      b->ba_class_off[k] = (uint32_t)b->ba_tile_order.size();
+      b->n_ba_class[k] = (uint32_t)(8 * m);
+      b->ba_tile_order.resize(b->ba_tile_order.size() + 8 * m, ~0u);
+      for (uint32_t x = 0; x < 8; x++)
+        for (size_t i = 0; i < q[8 * k + x].size(); i++) b->ba_tile_order[b->ba_class_off[k] + 8 * i + x] = q[8 * k + x][i];
     }
   }
   // Speculative mode: every page's non-null count is known from its header (or it has no
@@ -1003,9 +1135,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_run_base = take((uint64_t)np * 8);
   b->o_tile_base = take((uint64_t)np * 8);
   b->o_items = take(b->items.size() * sizeof(WorkItem));
-  b->o_ba_tile_sum = take(b->ba_tiles_total * 4);
-  b->o_ba_tile_off = take(b->ba_tile_off.size() * 8);
-  b->o_ba_totals = take(b->ba_chunks.size() * 8);
+  b->o_ba_tile_sum = take(b->ba_tile_page.size() * 8);
+  b->o_ba_tile_page = take(b->ba_tile_page.size() * 4);
+  b->o_ba_tile_order = take(b->ba_tile_order.size() * 4);
+  b->l_slot = take(b->slot_chunks.size() * 4);
+  b->o_ba_totals = take((uint64_t)nc * 8);
   b->o_dbg = take(64 * 8);
   b->o_ba_delta = take(b->ba_delta.size() * sizeof(BaDelta));
   b->o_snappy = take(b->snappy.size() * sizeof(SnappyJob));
@@ -1018,9 +1152,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
   b->l_base = take(b->base_chunks.size() * 4);
-  b->l_dict_ba = take(b->dict_ba_chunks.size() * 4);
   b->l_ba = take(b->ba_chunks.size() * 4);
-  b->l_ba_gather = take(b->ba_chunks.size() * 4);  // per decode: the BYTE_ARRAY chunks without an error
   b->l_rec = take(b->rec_pages.size() * 4);
   b->arena_size = a;
   if (a > b->d_arena_cap) {
@@ -1029,6 +1161,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->d_arena_cap = 0;
     HIPCHECK(hipMalloc(&b->d_arena, a), err);
     b->d_arena_cap = a;
+  }
+  if (payload_arena > b->d_payload_cap) {
+    if (b->d_payload) (void)hipFree(b->d_payload);
+    b->d_payload = nullptr;
+    b->d_payload_cap = 0;
+    HIPCHECK(hipMalloc(&b->d_payload, payload_arena), err);
+    b->d_payload_cap = payload_arena;
   }
   // stage: pinned host copy + device buffer (64 B zero pad); after it, the pages k_snappy
   // writes (each 256-B aligned, followed by 64 zero bytes like every staged section)
@@ -1085,7 +1224,27 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       cd.dict_raw_len = hc.dict_len;
       cd.dict_count = hc.dict_count;
       cd.dict_values = cd.dict_raw;
-      cd.dict_offsets = hc.o_dict_offsets ? dp(hc.o_dict_offsets) : 0;
+      cd.dict_offsets = hc.dict_ent.empty() ? 0 : (uint64_t)(b->d_stage + hc.dict_ent_off);
+      cd.dict_max_len = hc.dict_max_len;
+      cd.slot_shift = hc.slot_shift;
+      cd.dict_slots = hc.o_slots ? dp(hc.o_slots) : 0;
+    }
+    if (hc.value_width == 0) {
+      const PageDesc *fp = hc.num_pages ? &b->pages[hc.first_page] : nullptr;
+      cd.ba_tile0 = fp ? fp->ba_tile : 0;
+      cd.ba_ntiles = 0;
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
+        cd.ba_ntiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
+      if (hc.ba_sync) {
+        cd.flags |= CF_BA_SYNC;
+        cd.payload = hc.payload ? (uint64_t)hc.payload : 0;  // (re)sized after the scan of each decode
+      } else {
+        if (hc.payload_own && hc.payload) (void)hipFree(hc.payload);
+        hc.payload_own = false;
+        hc.payload = b->d_payload + hc.payload_off;
+        cd.payload = (uint64_t)hc.payload;
+        cd.payload_capacity = hc.payload_bound;
+      }
     }
     cd.values = hc.o_values ? dp(hc.o_values) : 0;
     cd.def_levels = hc.o_def ? dp(hc.o_def) : 0;
@@ -1124,12 +1283,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(hipMemsetAsync(A + b->o_dbg, 0, 64 * 8, s), err);
   HIPCHECK(up(b->o_tile_base, b->tile_base.data(), np * 8), err);
   HIPCHECK(up(b->o_items, b->items.data(), b->items.size() * sizeof(WorkItem)), err);
-  HIPCHECK(up(b->o_ba_tile_off, b->ba_tile_off.data(), b->ba_tile_off.size() * 8), err);
+  HIPCHECK(up(b->o_ba_tile_page, b->ba_tile_page.data(), b->ba_tile_page.size() * 4), err);
+  HIPCHECK(up(b->o_ba_tile_order, b->ba_tile_order.data(), b->ba_tile_order.size() * 4), err);
+  HIPCHECK(up(b->l_slot, b->slot_chunks.data(), b->slot_chunks.size() * 4), err);
   HIPCHECK(up(b->l_level, b->level_pages.data(), b->level_pages.size() * 4), err);
   HIPCHECK(up(b->l_level_bw1, b->level_pages_bw1.data(), b->level_pages_bw1.size() * 4), err);
   HIPCHECK(up(b->l_scan, b->scan_pages.data(), b->scan_pages.size() * 4), err);
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
-  HIPCHECK(up(b->l_dict_ba, b->dict_ba_chunks.data(), b->dict_ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
@@ -1171,7 +1331,12 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.run_count = (uint32_t *)(A + b->o_run_count);
   d.tile_first = (uint32_t *)(A + b->o_tile_first);
   d.tile_base = (const uint64_t *)(A + b->o_tile_base);
-  d.ba_tile_sum = (uint32_t *)(A + b->o_ba_tile_sum);
+  d.ba_tile_sum = (uint64_t *)(A + b->o_ba_tile_sum);
+  d.ba_tile_page = (const uint32_t *)(A + b->o_ba_tile_page);
+  d.ba_tile_order = (const uint32_t *)(A + b->o_ba_tile_order);
+  for (int k = 0; k < 4; k++) d.ba_class_off[k] = b->ba_class_off[k];
+  d.ba_state = (uint64_t *)(A + b->o_ba_state);
+  d.ba_totals = (uint64_t *)(A + b->o_ba_totals);
   d.dbg = b->debug_stamps ? (unsigned long long *)(A + b->o_dbg) : nullptr;
   d.npages = (uint32_t)b->pages.size();
   d.nchunks = (uint32_t)b->chunks.size();
@@ -1192,10 +1357,13 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_base_chunks = (uint32_t)b->base_chunks.size();
   l.items = (const WorkItem *)(A + b->o_items);
   l.n_items = (uint32_t)b->items.size();
-  l.dict_ba_chunks = (const uint32_t *)(A + b->l_dict_ba);
-  l.n_dict_ba = (uint32_t)b->dict_ba_chunks.size();
   l.ba_chunks = (const uint32_t *)(A + b->l_ba);
   l.n_ba_chunks = (uint32_t)b->ba_chunks.size();
+  l.n_ba_tiles = (uint32_t)b->ba_tile_page.size();
+  for (int k = 0; k < 3; k++) l.n_ba_class[k] = b->n_ba_class[k];
+  l.slot_chunks = (const uint32_t *)(A + b->l_slot);
+  l.n_slot_chunks = (uint32_t)b->slot_chunks.size();
+  l.slot_grid_x = b->slot_grid_x;
   l.rec_pages = (const uint32_t *)(A + b->l_rec);
   l.n_rec_pages = (uint32_t)b->rec_pages.size();
   l.delta_pages = (const uint32_t *)(A + b->l_delta);
@@ -1205,9 +1373,11 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
 }
 
 // Launch with optional event timing on the launch stream.
+// `n` = the launch's work units: nothing is launched (or timed) for an empty list.
 template <class F>
-static hipError_t timed(pqgpu_batch *b, int slot, hipStream_t s, F f) {
+static hipError_t timed(pqgpu_batch *b, int slot, hipStream_t s, uint64_t n, F f) {
   KernelTimer &t = b->timer;
+  if (!n) return hipSuccess;
   if (!t.enabled) return f();
   hipEvent_t ea = t.get(), eb = t.get();
   if (!ea || !eb) return hipErrorOutOfMemory;
@@ -1236,7 +1406,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   LaunchLists l = launch_lists(b);
   // SNAPPY pages first: every later kernel reads page data
   if (!b->snappy.empty())
-    HIPCHECK(timed(b, 11, s, [&] {
+    HIPCHECK(timed(b, 11, s, b->snappy.size(), [&] {
                return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy), (uint32_t)b->snappy.size(), s);
              }),
              err);
@@ -1254,83 +1424,68 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
-    HIPCHECK(timed(b, 4, v, [&] { return launch_dict_ba(d, l, v); }), err);
-    HIPCHECK(timed(b, 2, v, [&] { return launch_scan_runs(d, l, v); }), err);
-    HIPCHECK(timed(b, 10, v, [&] { return launch_delta_prep(d, l, v); }), err);
-    HIPCHECK(timed(b, 9, v, [&] { return launch_values(d, l, v); }), err);
+    HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
+    HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
+    HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
     HIPCHECK(launch_ba_delta(d, l, v), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
-    HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
-    HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
   } else {
-    HIPCHECK(timed(b, 4, s, [&] { return launch_dict_ba(d, l, s); }), err);
-    HIPCHECK(timed(b, 0, s, [&] { return launch_levels(d, l, s); }), err);
-    HIPCHECK(timed(b, 3, s, [&] { return launch_bases(d, l, s); }), err);
-    HIPCHECK(timed(b, 2, s, [&] { return launch_scan_runs(d, l, s); }), err);
-    HIPCHECK(timed(b, 10, s, [&] { return launch_delta_prep(d, l, s); }), err);
+    HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
+    HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
     if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items as two launches (profiling)
-      HIPCHECK(timed(b, 1, s, [&] { return launch_values(d, l1, s); }), err);
-      HIPCHECK(timed(b, 8, s, [&] { return launch_values(d, l2, s); }), err);
+      HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values(d, l1, s); }), err);
+      HIPCHECK(timed(b, 8, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     } else {
       // one grid: the DELTA pages (latency-bound: serial header walks and per-batch barriers)
       // are dispatched first and the bandwidth-bound tiles fill the CUs around them
-      HIPCHECK(timed(b, 9, s, [&] { return launch_values(d, l, s); }), err);
+      HIPCHECK(timed(b, 9, s, l.n_items, [&] { return launch_values(d, l, s); }), err);
     }
     HIPCHECK(launch_ba_delta(d, l, s), err);  // DELTA_LENGTH / DELTA_BYTE_ARRAY: lengths -> values
   }
   if (!b->ba_chunks.empty()) {
-    HIPCHECK(timed(b, 5, s, [&] {
-               return launch_ba_offsets_impl(d, l.ba_chunks, l.n_ba_chunks, (const uint64_t *)(A + b->o_ba_tile_off),
-                                             b->ba_max_tiles, (uint64_t *)(A + b->o_ba_totals), s);
-             }),
-             err);
-    std::vector<uint64_t> totals(b->ba_chunks.size()), keys(nc);
-    HIPCHECK(hipMemcpyAsync(totals.data(), A + b->o_ba_totals, totals.size() * 8, hipMemcpyDeviceToHost, s), err);
-    HIPCHECK(hipMemcpyAsync(keys.data(), A + b->o_err, (size_t)nc * 8, hipMemcpyDeviceToHost, s), err);
-    HIPCHECK(hipStreamSynchronize(s), err);
-    bool changed = false;
-    std::vector<uint32_t> gather;  // chunks without a decode error: their lengths and sources are all set
-    for (size_t k = 0; k < b->ba_chunks.size(); k++) {
-      HostChunk &hc = b->chunks[b->ba_chunks[k]];
-      if (keys[b->ba_chunks[k]] != ~0ull) continue;
-      if (totals[k] > 0x7fffffffULL) {
-        set_err(&hc.err, PQ_ERR_UNSUPPORTED, (int)b->ba_chunks[k], -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
-        continue;
-      }
-      hc.payload_bytes = (int64_t)totals[k];
-      if ((uint64_t)hc.payload_bytes + 64 > hc.payload_cap) {
-        if (hc.payload) (void)hipFree(hc.payload);
-        hc.payload = nullptr;
-        hc.payload_cap = 0;
-        HIPCHECK(hipMalloc(&hc.payload, (size_t)hc.payload_bytes + 64), err);
-        hc.payload_cap = (uint64_t)hc.payload_bytes + 64;
-      }
-      b->chunk_desc[b->ba_chunks[k]].payload = (uint64_t)hc.payload;
-      changed = true;
-      gather.push_back(b->ba_chunks[k]);
-    }
-    if (changed) {
-      for (uint32_t c : b->ba_chunks)
-        HIPCHECK(hipMemcpyAsync(A + b->o_chunks + (uint64_t)c * sizeof(ChunkDesc), &b->chunk_desc[c], sizeof(ChunkDesc),
+    // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
+    HIPCHECK(timed(b, 12, s, l.n_slot_chunks, [&] { return launch_dict_slots(d, l, s); }), err);
+    if (b->any_ba_sync) {
+      HIPCHECK(timed(b, 4, s, l.n_ba_tiles, [&] { return launch_ba_sums(d, l, s); }), err);
+      HIPCHECK(timed(b, 5, s, l.n_ba_chunks, [&] { return launch_ba_scan(d, l, s); }), err);
+      // chunks without an upload-time payload bound (DELTA_BYTE_ARRAY pages): size them now
+      std::vector<uint64_t> totals(nc);
+      HIPCHECK(hipMemcpyAsync(totals.data(), A + b->o_ba_totals, (size_t)nc * 8, hipMemcpyDeviceToHost, s), err);
+      HIPCHECK(hipStreamSynchronize(s), err);
+      for (uint32_t c : b->ba_chunks) {
+        HostChunk &hc = b->chunks[c];
+        if (!hc.ba_sync) continue;
+        ChunkDesc &cd = b->chunk_desc[c];
+        hc.sync_err = totals[c] > 0x7fffffffULL - 64;
+        if (hc.sync_err) {
+          cd.payload = 0;  // k_ba_emit / k_dba_gather skip the chunk; sync reports it
+        } else {
+          if (totals[c] + 64 > hc.payload_cap) {
+            if (hc.payload_own && hc.payload) (void)hipFree(hc.payload);
+            hc.payload = nullptr;
+            hc.payload_cap = 0;
+            HIPCHECK(hipMalloc(&hc.payload, (size_t)totals[c] + 64), err);
+            hc.payload_own = true;
+            hc.payload_cap = totals[c] + 64;
+          }
+          cd.payload = (uint64_t)hc.payload;
+          cd.payload_capacity = totals[c];
+        }
+        HIPCHECK(hipMemcpyAsync(A + b->o_chunks + (uint64_t)c * sizeof(ChunkDesc), &cd, sizeof(ChunkDesc),
                                 hipMemcpyHostToDevice, s),
                  err);
+      }
     }
-    uint64_t maxnn = 0;
-    for (uint32_t c : gather) maxnn = std::max<uint64_t>(maxnn, b->chunks[c].num_slots);
-    uint32_t gx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((maxnn + 255) / 256, 1), 4096);
-    if (!gather.empty()) {
-      // its own slot: the BYTE_ARRAY list (l_ba) must stay intact for the next decode of the batch
-      HIPCHECK(hipMemcpyAsync(A + b->l_ba_gather, gather.data(), gather.size() * 4, hipMemcpyHostToDevice, s), err);
-      HIPCHECK(timed(b, 6, s, [&] {
-                 return launch_ba_gather_impl(d, (const uint32_t *)(A + b->l_ba_gather), (uint32_t)gather.size(), gx, s);
-               }),
-               err);
-      HIPCHECK(launch_dba_gather(d, l, s), err);
-    }
-    HIPCHECK(hipStreamSynchronize(s), err);  // host vectors above stay valid until here
+    HIPCHECK(timed(b, 6, s, l.n_ba_tiles, [&] { return launch_ba_emit(d, l, s); }), err);
+    HIPCHECK(launch_dba_gather(d, l, s), err);
+    if (b->any_ba_sync) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc copies above read host memory
   }
-  HIPCHECK(timed(b, 7, s, [&] { return launch_records(d, l, s); }), err);
+  HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   b->decoded = true;
   return PQ_OK;
 }
@@ -1382,15 +1537,24 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMemcpy(rbase.data(), A + b->o_rbase, np * 8, hipMemcpyDeviceToHost), err);
     HIPCHECK(hipMemcpy(rec.data(), A + b->o_rec, np * 4, hipMemcpyDeviceToHost), err);
   }
+  std::vector<uint64_t> ba_tot;
+  if (!b->ba_chunks.empty()) {
+    ba_tot.resize(nc);
+    HIPCHECK(hipMemcpy(ba_tot.data(), A + b->o_ba_totals, (size_t)nc * 8, hipMemcpyDeviceToHost), err);
+  }
   b->page_vbase_out = vbase;
   b->page_nn_out = nn;
   int first = PQ_OK;
   int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0;
+  int64_t kb[PQGPU_TIMER_SLOTS] = {0};  // algorithmic bytes per launch slot
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
     clear_err(&hc.dev_err);
     hc.dev_err.chunk = (int)c;
     if (!hc.err.code && keys[c] != ~0ull) decode_key(keys[c], (int)c, &hc.dev_err);
+    if (!hc.err.code && hc.sync_err && !hc.dev_err.code)
+      set_err(&hc.dev_err, PQ_ERR_UNSUPPORTED, (int)c, -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
+    if (!ba_tot.empty() && hc.value_width == 0) hc.payload_bytes = (int64_t)ba_tot[c];
     if (hc.num_pages) {
       uint32_t lp = hc.first_page + hc.num_pages - 1;
       hc.nn = (int64_t)(vbase[lp] + nn[lp]);
@@ -1413,18 +1577,44 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.o_rep) out_bytes += (int64_t)hc.num_slots;
       if (hc.o_valid) out_bytes += (int64_t)(hc.num_slots + 7) / 8;
       if (hc.o_lists) out_bytes += (hc.records + 1) * 4;
+      int64_t ba_dict_nn = 0, ba_other_nn = 0;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
         const PageDesc &pd = b->pages[p];
         lvl_bytes += pd.rep_len + pd.def_len;
-        val_bytes += pd.val_len;
         if (pd.vkind == VK_DELTA32 || pd.vkind == VK_DELTA64) dl_bytes += pd.val_len + (int64_t)nn[p] * w;
+        if (pd.vkind == VK_DICT || pd.vkind == VK_RLE_BOOL) kb[2] += pd.val_len;  // k_scan_runs: index streams
+        if (w == 0 && pd.vkind == VK_DICT) {
+          if (hc.ba_sync) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices (CF_BA_SYNC chunks)
+          kb[6] += pd.val_len;
+          ba_dict_nn += nn[p];
+        } else {
+          val_bytes += pd.val_len;  // k_values reads the page's value section
+          if (w == 0) ba_other_nn += nn[p];
+        }
       }
       if (hc.o_def) lvl_bytes += (int64_t)hc.num_slots;
       if (hc.o_rep) lvl_bytes += (int64_t)hc.num_slots;
       if (hc.o_valid) lvl_bytes += (int64_t)(hc.num_slots + 7) / 8;
-      val_bytes += w ? hc.nn * w : (hc.nn + 1) * 4;
+      if (w) {
+        val_bytes += hc.nn * w;
+      } else {
+        // lengths of the non-dictionary pages: read by k_ba_sums; read with their sources and
+        // bytes by k_ba_emit, which writes every offset and the payload
+        if (hc.ba_sync) kb[4] += 4 * ba_other_nn;
+        kb[6] += 4 * (hc.nn + 1) + hc.payload_bytes + 12 * ba_other_nn;
+        kb[5] += 16 * (int64_t)b->chunk_desc[c].ba_ntiles;
+        if (hc.slot_shift) kb[12] += (int64_t)hc.dict_len + 8 * (int64_t)hc.dict_count + ((int64_t)hc.dict_count << hc.slot_shift);
+        (void)ba_dict_nn;
+      }
+      if (hc.o_lists) kb[7] += (int64_t)hc.num_slots + 4 * (hc.records + 1);
     }
   }
+  kb[0] = lvl_bytes;
+  kb[1] = dl_bytes;
+  kb[9] = val_bytes;
+  kb[8] = val_bytes - dl_bytes;
+  kb[11] = b->stats.snappy_kernel_bytes;
+  memcpy(b->slot_bytes, kb, sizeof(kb));
   b->stats.levels_kernel_bytes = lvl_bytes;
   b->stats.values_kernel_bytes = val_bytes;
   b->stats.delta_kernel_bytes = dl_bytes;
@@ -1568,8 +1758,12 @@ int pqgpu_batch_create(pqgpu_ctx *ctx, pqgpu_batch **out, pqgpu_error *err) {
 }
 
 static void free_payloads(pqgpu_batch *b) {
-  for (auto &hc : b->chunks)
-    if (hc.payload) { (void)hipFree(hc.payload); hc.payload = nullptr; hc.payload_cap = 0; }
+  for (auto &hc : b->chunks) {
+    if (hc.payload_own && hc.payload) (void)hipFree(hc.payload);
+    hc.payload = nullptr;
+    hc.payload_cap = 0;
+    hc.payload_own = false;
+  }
 }
 
 void pqgpu_batch_destroy(pqgpu_batch *b) {
@@ -1582,6 +1776,7 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
+  if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);
   if (b->h_pinned) (void)hipHostFree(b->h_pinned);
   b->timer.destroy();
@@ -1795,6 +1990,12 @@ int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, c
   if (avg_ms) *avg_ms = t.total_ms[best] / (double)t.launches[best];
   if (launches) *launches = t.launches[best];
   if (name && name_len) snprintf(name, name_len, "%s", kTimerNames[best]);
+  return PQ_OK;
+}
+
+int pqgpu_batch_kernel_bytes(const pqgpu_batch *b, int slot, int64_t *bytes) {
+  if (!b || slot < 0 || slot >= PQGPU_TIMER_SLOTS || !bytes) return PQ_ERR_ARG;
+  *bytes = b->slot_bytes[slot];
   return PQ_OK;
 }
 

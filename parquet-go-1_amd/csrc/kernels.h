@@ -25,7 +25,13 @@ struct BatchDev {
   uint32_t *run_count;            // [npages]
   uint32_t *tile_first;           // dict tiles: first run index per tile
   const uint64_t *tile_base;      // [npages] first tile-table entry per page
-  uint32_t *ba_tile_sum;          // BYTE_ARRAY: per 4096-value tile payload sum
+  uint64_t *ba_tile_sum;          // byte-array tiles: payload bytes per tile, then (k_ba_scan) its
+                                  // exclusive base within the chunk
+  const uint32_t *ba_tile_page;   // byte-array tile -> global page index
+  const uint32_t *ba_tile_order;  // k_ba_emit block -> byte-array tile, per class (~0u: padding)
+  uint32_t ba_class_off[4];       // class k's blocks: ba_tile_order[ba_class_off[k] ..]
+  uint64_t *ba_state;             // [tiles] look-back state of each tile (zeroed per decode)
+  uint64_t *ba_totals;            // [nchunks] payload bytes of each byte-array chunk (k_ba_scan)
   DeltaBlk *dblk;                 // DELTA block tables of all tiled DELTA pages
   const uint64_t *dblk_base;      // [npages] first DeltaBlk of the page
   uint32_t *dblk_n;               // [npages] blocks the header walk produced
@@ -39,7 +45,8 @@ struct BatchDev {
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
-constexpr uint32_t kBaTile = 4096;     // values per BYTE_ARRAY scan tile
+constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
+                                        // page's BA tiles are its dictionary tiles)
 
 struct LaunchLists {
   const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams (generic)
@@ -48,20 +55,26 @@ struct LaunchLists {
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
   const WorkItem *items; uint32_t n_items;               // values work items
-  const uint32_t *dict_ba_chunks; uint32_t n_dict_ba;    // chunks with a BYTE_ARRAY dictionary page
-  const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with BYTE_ARRAY output
+  const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with byte-array output
+  uint32_t n_ba_tiles;
+  uint32_t n_ba_class[3];  // k_ba_emit tiles per class (bytearray.hip ba_emit)                                   // byte-array tiles (BatchDev::ba_tile_page)
+  const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
+  uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
   const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)
   uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE
 };
 
-hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
-hipError_t launch_ba_offsets(const BatchDev &b, const LaunchLists &l, uint64_t *payload_totals_dev, hipStream_t s);
-hipError_t launch_ba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+// byte-array outputs (bytearray.hip): per-tile payload sums, per-chunk scan of the tile sums,
+// offsets + payload of every tile
+hipError_t launch_dict_slots(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_ba_sums(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_ba_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_ba_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads

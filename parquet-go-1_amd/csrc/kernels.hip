@@ -18,205 +18,19 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/pqgpu.h"
+#include "dev_util.h"
+#include "dict_tile.h"
 #include "kernels.h"
 
 namespace pq {
 
 const char *kValuesKernelName = "k_values";
 
-#define DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------------------
-// Unaligned little-endian loads from the (padded) staging buffer.
-// ---------------------------------------------------------------------------
-DEV uint32_t ld32(const uint8_t *p) {
-  uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(p - (a & 3));  // pointer arithmetic keeps the address space
-  uint32_t lo = q[0], hi = q[1];
-  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
-}
-DEV uint64_t ld64(const uint8_t *p) {
-  uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(p - (a & 3));
-  uint32_t s = (uint32_t)(a & 3);
-  uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
-  uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, s);
-  uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, s);
-  return ((uint64_t)hi << 32) | lo;
-}
-// bw (<= 32) bits at bit offset `bo` of stream p, LSB-first (bitpack_gen.go:19-59).
-DEV uint32_t bits32(const uint8_t *p, uint64_t bo, uint32_t bw) {
-  uint64_t x = ld64(p + (bo >> 3)) >> (bo & 7);
-  return bw >= 32 ? (uint32_t)x : (uint32_t)x & ((1u << bw) - 1u);
-}
-// bw (<= 64) bits at bit offset bo.
-DEV uint64_t bits64(const uint8_t *p, uint64_t bo, uint32_t bw) {
-  if (bw == 0) return 0;
-  const uint8_t *q = p + (bo >> 3);
-  uint32_t sh = (uint32_t)(bo & 7);
-  uint64_t x = ld64(q) >> sh;
-  if (sh && bw > 64 - sh) x |= (uint64_t)q[8] << (64 - sh);
-  return bw >= 64 ? x : x & ((1ull << bw) - 1ull);
-}
-
-// Same, but bytes at or past the stream end `n` read as zero (the reference's
-// bit-packed groups are read with a bare Read into a zeroed buffer: a short final
-// group is zero-filled, hybrid_decoder.go:132-140).
-DEV uint32_t bits32c(const uint8_t *p, uint32_t n, uint64_t bo, uint32_t bw) {
-  uint64_t by = bo >> 3;
-  if (by >= n) return 0;
-  uint64_t x = ld64(p + by);
-  uint64_t avail = n - by;
-  if (avail < 8) x &= (1ull << (8 * avail)) - 1ull;
-  x >>= (bo & 7);
-  return bw >= 32 ? (uint32_t)x : (uint32_t)x & ((1u << bw) - 1u);
-}
-DEV uint64_t bits64c(const uint8_t *p, uint32_t n, uint64_t bo, uint32_t nb) {  // nb <= 57
-  uint64_t by = bo >> 3;
-  if (by >= n) return 0;
-  uint64_t x = ld64(p + by);
-  uint64_t avail = n - by;
-  if (avail < 8) x &= (1ull << (8 * avail)) - 1ull;
-  x >>= (bo & 7);
-  return nb >= 64 ? x : x & ((1ull << nb) - 1ull);
-}
-
-DEV uint32_t lane_id() { return __lane_id(); }
-
-// Global-memory pointers. Device addresses travel in descriptors as integers and in BatchDev
-// as generic pointers, which compile to FLAT instructions; a FLAT access counts in both vmcnt
-// and lgkmcnt, so every LDS wait (lgkmcnt) would also wait for all outstanding loads and
-// stores. Casting each pointer's origin to address space 1 lets the compiler emit global_*
-// instructions along every use.
-#define PQ_GLOBAL __attribute__((address_space(1)))
-template <class T>
-DEV T *gp(T *p) { return (T *)(PQ_GLOBAL T *)p; }
-template <class T>
-DEV T *gp_u64(uint64_t a) { return (T *)(PQ_GLOBAL T *)(uintptr_t)a; }
-DEV BatchDev global_view(BatchDev b) {
-  b.pages = gp(b.pages); b.chunks = gp(b.chunks); b.chunk_err = gp(b.chunk_err);
-  b.page_nn = gp(b.page_nn); b.page_nn_v = gp(b.page_nn_v); b.spec_mismatch = gp(b.spec_mismatch);
-  b.page_rec = gp(b.page_rec); b.page_vbase = gp(b.page_vbase); b.page_rbase = gp(b.page_rbase);
-  b.runs = gp(b.runs); b.run_base = gp(b.run_base); b.run_count = gp(b.run_count);
-  b.tile_first = gp(b.tile_first); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
-  b.dblk = gp(b.dblk); b.dblk_base = gp(b.dblk_base); b.dblk_n = gp(b.dblk_n); b.dblk_sum = gp(b.dblk_sum);
-  b.ba_delta = gp(b.ba_delta);
-  if (b.dbg) b.dbg = gp(b.dbg);
-  return b;
-}
-
-// Workgroup barrier for LDS hand-offs. __syncthreads() is a workgroup-scope release/acquire
-// over every address space, so it waits for all of the wave's outstanding global loads and
-// stores (vmcnt(0)) before s_barrier: prefetched windows and the previous batch's stores
-// would be drained at every barrier. Every barrier in this file orders LDS accesses only
-// (global results are never read back by another thread of the same workgroup), so the
-// fences are restricted to LDS and only lgkmcnt is waited for.
-DEV void wg_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Diagnostic phase stamps: per-wave cycle sums added to b.dbg. Compiled in only for the
-// diagnostic library (make diag -> lib/libpqgpu_diag.so, -DPQ_DIAG_STAMPS) and active there
-// when PQ_DEBUG_STAMPS=1; the production kernels carry no stamp code or registers.
-#ifdef PQ_DIAG_STAMPS
-DEV uint64_t stamp() { return __builtin_amdgcn_s_memtime(); }
-struct Stamps {
-  unsigned long long *dbg;
-  uint64_t t, acc[8];
-  DEV void begin() { if (dbg) t = stamp(); }
-  DEV void lap(int k) {
-    if (dbg) { uint64_t n = stamp(); acc[k] += n - t; t = n; }
-  }
-  DEV void flush(int base) {
-    if (dbg && __lane_id() == 0)
-      for (int k = 0; k < 8; k++) if (acc[k]) atomicAdd(&dbg[base + k], (unsigned long long)acc[k]);
-  }
-  DEV void count(int k) { if (dbg) acc[k]++; }
-  DEV void add(int k, uint64_t v) { if (dbg) acc[k] += v; }
-};
-#define PQ_STAMPS(name, dbgp) Stamps name{dbgp, 0, {0, 0, 0, 0, 0, 0, 0, 0}}
-#define PQ_ABLATE(b, bit) (((b).ablate >> (bit)) & 1u)
-#else
-#define PQ_ABLATE(b, bit) 0u
-struct Stamps {
-  DEV void begin() {}
-  DEV void lap(int) {}
-  DEV void flush(int) {}
-  DEV void count(int) {}
-  DEV void add(int, uint64_t) {}
-};
-#define PQ_STAMPS(name, dbgp) Stamps name
-#endif
-DEV uint32_t rdlane(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
-
-DEV uint32_t wave_excl_scan(uint32_t v) {
-  uint32_t x = v;
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  return x - v;
-}
-DEV uint64_t wave_incl_scan64(uint64_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t y = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += y;
-  }
-  return v;
-}
-// wave64 inclusive prefix sum with DPP row shifts and row broadcasts (GFX9 DPP)
-template <int CTRL, int ROWS = 0xf>
-DEV uint32_t dpp0(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false); }
-DEV uint32_t wave_incl_scan32(uint32_t x) {
-  x += dpp0<0x111>(x);       // row_shr:1
-  x += dpp0<0x112>(x);       // row_shr:2
-  x += dpp0<0x114>(x);       // row_shr:4
-  x += dpp0<0x118>(x);       // row_shr:8
-  x += dpp0<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
-  x += dpp0<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
-  return x;
-}
-// wave64 inclusive scan of 64-bit values (wrapping) with DPP row shifts / broadcasts
-DEV uint64_t wave_incl_scan64_dpp(uint64_t v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#define PQ_SCAN_STEP(CTRL, ROWS)                                                  \
-  {                                                                               \
-    const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROWS, 0xf, false); \
-    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWS, 0xf, false); \
-    const uint64_t s = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2); \
-    lo = (uint32_t)s; hi = (uint32_t)(s >> 32);                                   \
-  }
-  PQ_SCAN_STEP(0x111, 0xf)
-  PQ_SCAN_STEP(0x112, 0xf)
-  PQ_SCAN_STEP(0x114, 0xf)
-  PQ_SCAN_STEP(0x118, 0xf)
-  PQ_SCAN_STEP(0x142, 0xa)
-  PQ_SCAN_STEP(0x143, 0xc)
-#undef PQ_SCAN_STEP
-  return ((uint64_t)hi << 32) | lo;
-}
-
-DEV uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-
-DEV void report(const BatchDev &b, uint32_t chunk, uint32_t phase, uint32_t page, uint32_t stage, uint32_t pos,
-                uint32_t code) {
-  atomicMin(&b.chunk_err[chunk], (unsigned long long)err_key(phase, page, stage, pos, code));
-}
-
-// ---------------------------------------------------------------------------
-// Hybrid RLE / bit-packing walker (hybrid_decoder.go:81-165), one wave.
+// Hybrid RLE / bit-packing walker (hybrid_decoder.go:81-165), wave 0 of a workgroup.
 //
-// The wave keeps a 4 KiB LDS window of the stream. For the header at `pos`
+// The walker keeps an LDS window of the stream (hyb_scan below). For the header at `pos`
 // every lane decodes the header that WOULD start at pos+lane (uvarint,
 // kind, count, payload length, Go error class). The true chain is then
 // followed lane to lane with readlane hops; each visited lane is a run.
@@ -230,41 +44,7 @@ DEV void report(const BatchDev &b, uint32_t chunk, uint32_t phase, uint32_t page
 //   RLE value >= 2^bw                     -> "RLE run value is too large"
 //   bit-packed group starting at EOF      -> io.EOF (a short group zero-fills)
 // ---------------------------------------------------------------------------
-constexpr uint32_t kStage = 4096;
 constexpr uint32_t kSegSlots = 65536;  // bitmap slots staged in LDS per page
-
-struct WalkLDS {
-  uint32_t stage[kStage / 4 + 8];
-};
-
-DEV uint32_t lds_ld32(const uint32_t *stg, uint32_t off) {
-  uint32_t w = off >> 2, s = off & 3;
-  return __builtin_amdgcn_alignbyte(stg[w + 1], stg[w], s);
-}
-DEV uint32_t sgpr(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// Stage stream bytes [sb, sb + kStage + 32) into LDS; bytes at or past n read as 0
-// (the zero fill of a short final bit-packed group, hybrid_decoder.go:132-140).
-DEV void stage_load(uint32_t *stg, const uint8_t *s, uint32_t sb, uint32_t n) {
-  const uint32_t lane = lane_id();
-  const uint8_t *src = s + sb;
-  const uint32_t lim = n > sb ? n - sb : 0;
-#pragma unroll 4
-  for (uint32_t k = lane; k < kStage / 4 + 8; k += 64) {
-    uint32_t o = 4 * k;
-    stg[k] = o + 4 <= lim ? ld32(src + o) : (o < lim ? ld32(src + o) & ((1u << (8 * (lim - o))) - 1u) : 0u);
-  }
-}
-
-// bits at bit offset bo (relative to the stage start) of the LDS stage, width <= 64
-DEV uint64_t lds_bits64(const uint32_t *win, uint32_t bo, uint32_t w) {
-  if (w == 0) return 0;
-  uint32_t wi = bo >> 5, sh = bo & 31;
-  uint64_t lo = (uint64_t)win[wi] | ((uint64_t)win[wi + 1] << 32);
-  uint64_t x = lo >> sh;
-  if (sh && w > 64 - sh) x |= (uint64_t)win[wi + 2] << (64 - sh);
-  return w >= 64 ? x : x & ((1ull << w) - 1ull);
-}
 
 constexpr uint32_t kErrLongVarint = 15;  // internal: varint longer than 12 bytes, resolved lazily
 DEV uint32_t resolve_long_varint(const uint8_t *s, uint32_t c, uint32_t n) {
@@ -354,64 +134,151 @@ DEV Hdr decode_hdr(const uint32_t *stg, uint32_t sb, const uint8_t *s, uint32_t 
 }
 
 
+// The walker over a whole stream, one 256-thread workgroup: the stream goes through an LDS
+// window of kScanWin bytes (+ kScanOver bytes of look-ahead). All four waves load the next
+// window into registers (16-B loads) while wave 0 walks the current one, so a long run of
+// bit-packed values costs one step of the walk, not a load round trip.
+constexpr uint32_t kScanWin = 16384;
+constexpr uint32_t kScanOver = 256;
+constexpr uint32_t kScanVec = (kScanWin + kScanOver) / 16;  // uint4 per window
+constexpr uint32_t kScanPer = (kScanVec + 255) / 256;       // uint4 per thread
+struct ScanLDS {
+  uint32_t win[kScanVec * 4 + 8];
+  uint32_t ctl_pos, ctl_done, ctl_stop;
+};
+
 template <class Sink>
-DEV uint32_t hyb_walk(WalkLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink,
-                      Stamps *st = nullptr) {
-  const uint32_t lane = lane_id();
-  n = sgpr(n);
-  bw = sgpr(bw);
-  need = sgpr(need);
+DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t rs = (bw + 7) >> 3;
-  uint32_t pos = 0, done = 0, sb = 0;
-  stage_load(L.stage, s, 0, n);
+  // window w holds the bytes at 16-B aligned global addresses [s_al + w * kScanWin, + kScanWin + kScanOver)
+  const uintptr_t s_al = (uintptr_t)s & ~(uintptr_t)15;
+  const uint32_t sbase = (uint32_t)((uintptr_t)s - s_al);
+  const uint4 *g = (const uint4 *)gp_u64<const uint8_t>((uint64_t)s_al);
+  uint4 pre[kScanPer];
+  auto fetch = [&](uint32_t w) {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; j++) {
+      const uint32_t k = tid + j * 256;
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      const uint64_t ap = (uint64_t)w * kScanWin + 16ull * k;  // aligned position
+      const int64_t rel = (int64_t)n + sbase - (int64_t)ap;       // stream bytes left at this block
+      if (k < kScanVec && rel > 0) {
+        x = g[ap >> 4];
+        if (rel < 16) {  // bytes at or past the stream end read as zero
+          uint32_t q[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int64_t r = rel - 4 * i;
+            q[i] = r >= 4 ? q[i] : (r <= 0 ? 0u : (q[i] & ((1u << (8 * r)) - 1u)));
+          }
+          x = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+      }
+      pre[j] = x;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; j++) {
+      const uint32_t k = tid + j * 256;
+      if (k < kScanVec) *(uint4 *)&L.win[4 * k] = pre[j];
+    }
+    if (tid < 8) L.win[kScanVec * 4 + tid] = 0;
+  };
+  fetch(0);
+  store();
+  fetch(1);
+  uint32_t w = 0, pos = 0, done = 0;
   wg_barrier();
-  while (done < need) {
-    // keep the candidate headers (pos .. pos+76) and short-run payloads staged
-    if (st) st->lap(7);
-    if (pos + 208 > sb + kStage) {
-      sb = sgpr(pos & ~3u);
-      wg_barrier();
-      stage_load(L.stage, s, sb, n);
-      wg_barrier();
-      if (st) { st->lap(0); st->count(5); }
+  for (;;) {
+    if (wv == 0) {
+      const uint32_t sb = w * kScanWin - sbase;  // stream position of win[0] (mod 2^32)
+      const uint32_t lim = (w + 1) * kScanWin - sbase;
+      uint32_t stop = 0;
+      while (done < need && pos < lim) {
+        // ---- scalar fast path: a well-formed run of >= 64 stream bytes (long bit-packed runs;
+        // one header per step, no speculation)
+        {
+          const uint32_t off = pos - sb;
+          const uint32_t u0 = sgpr(lds_ld32(L.win, off)), u1 = sgpr(lds_ld32(L.win, off + 4));
+          const uint32_t tm = ~u0 & 0x80808080u;
+          if (tm && pos < n) {
+            const uint32_t Lv = (uint32_t)(__builtin_ctz(tm) >> 3) + 1;
+            const uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
+            const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+            const uint32_t cnt = h >> 1, isbp = h & 1u;
+            const uint64_t adv = isbp ? Lv + (uint64_t)cnt * bw : (uint64_t)(Lv + rs);
+            const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
+            const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
+            const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
+            if (ok && adv >= 64) {
+              const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - done;
+              const uint32_t take = min(nv, rem);
+              sink.one(done, take, isbp != 0, val, pos);
+              done += take;
+              if (nv >= rem) break;
+              pos += (uint32_t)adv;
+              continue;
+            }
+          }
+        }
+        // ---- speculative header decode at c = pos + lane
+        const uint32_t c = pos + lane;
+        const Hdr h = decode_hdr(L.win, sb, s, c, n, bw, rs);
+        // ---- follow the true chain lane to lane (scalar registers)
+        uint64_t mask = 0;
+        uint32_t cum = 0, p = 0, next_pos = pos;
+        uint32_t stop_err = 0, stop_pos = 0;
+        for (;;) {
+          uint32_t e = rdlane(h.err, p);
+          if (e == kErrLongVarint) e = sgpr(resolve_long_varint(s, pos + p, n));
+          if (e) { stop = 1; stop_err = e; stop_pos = done + cum; break; }
+          const uint32_t nv = rdlane(h.nvals, p), ok = rdlane(h.okvals, p);
+          mask |= 1ull << p;
+          const uint32_t rem = need - done - cum;
+          if (ok < nv && ok < rem) { cum += ok; stop = 1; stop_err = PQ_ERR_EOF; stop_pos = done + cum; break; }
+          if (nv >= rem) { cum += rem; stop = 1; break; }
+          cum += nv;
+          const uint32_t q = p + rdlane(h.adv, p);
+          if (q >= 64) { next_pos = pos + q; break; }
+          p = q;
+        }
+        // ---- the runs of this step
+        const bool mine = (mask >> lane) & 1ull;
+        const uint32_t first = wave_excl_scan(mine ? h.nvals : 0u);
+        uint32_t cnt = 0;
+        if (mine && first < cum) cnt = min(h.nvals, cum - first);
+        sink.window(mine && cnt > 0, done + first, cnt, h.bp != 0, h.value, c, L.win, sb);
+        done = sgpr(done + cum);
+        if (stop) {
+          if (stop_err) sink.error(stop_pos, stop_err);
+          break;
+        }
+        pos = sgpr(next_pos);
+      }
+      if (lane == 0) {
+        L.ctl_pos = pos;
+        L.ctl_done = done;
+        L.ctl_stop = stop || done >= need;
+      }
     }
-    // ---- speculative header decode at c = pos + lane
-    const uint32_t c = pos + lane;
-    const Hdr h = decode_hdr(L.stage, sb, s, c, n, bw, rs);
-    if (st) { (void)__builtin_amdgcn_readfirstlane(h.err + h.adv + h.nvals); st->lap(1); st->count(6); }
-    // ---- follow the true chain lane to lane (scalar registers)
-    uint64_t mask = 0;
-    uint32_t cum = 0, p = 0, next_pos = pos;
-    uint32_t stop = 0, stop_err = 0, stop_pos = 0;
-    for (;;) {
-      uint32_t e = rdlane(h.err, p);
-      if (e == kErrLongVarint) e = sgpr(resolve_long_varint(s, pos + p, n));
-      if (e) { stop = 1; stop_err = e; stop_pos = done + cum; break; }
-      const uint32_t nv = rdlane(h.nvals, p), ok = rdlane(h.okvals, p);
-      mask |= 1ull << p;
-      const uint32_t rem = need - done - cum;
-      if (ok < nv && ok < rem) { cum += ok; stop = 1; stop_err = PQ_ERR_EOF; stop_pos = done + cum; break; }
-      if (nv >= rem) { cum += rem; stop = 1; break; }
-      cum += nv;
-      const uint32_t q = p + rdlane(h.adv, p);
-      if (q >= 64) { next_pos = pos + q; break; }
-      p = q;
+    wg_barrier();
+    pos = L.ctl_pos;
+    done = L.ctl_done;
+    const uint32_t fin = L.ctl_stop;
+    if (fin) break;
+    const uint32_t nw = (pos + sbase) / kScanWin;
+    if (nw == w + 1) {
+      store();
+      fetch(nw + 1);
+    } else {  // a run longer than a window: that window was not prefetched
+      fetch(nw);
+      store();
+      fetch(nw + 1);
     }
-    if (st) st->lap(2);
-    // ---- expansion
-    const bool mine = (mask >> lane) & 1ull;
-    const uint32_t first = wave_excl_scan(mine ? h.nvals : 0u);
-    uint32_t cnt = 0;
-    if (mine && first < cum) cnt = min(h.nvals, cum - first);
-    if (st) st->lap(3);
-    sink.window(mine && cnt > 0, done + first, cnt, h.bp != 0, h.value, c, L.stage, sb);
-    if (st) st->lap(4);
-    done = sgpr(done + cum);
-    if (stop) {
-      if (stop_err) sink.error(stop_pos, stop_err);
-      break;
-    }
-    pos = sgpr(next_pos);
+    w = nw;
+    wg_barrier();
   }
   return done;
 }
@@ -1035,23 +902,37 @@ struct RunSink {
     }
     nruns += __popcll(m);
   }
+  // One run found by the scalar fast path (every lane calls it with uniform arguments).
+  DEV void one(uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t c) {
+    const uint32_t idx = nruns;
+    if (lane_id() == 0) {
+      HybRun r;
+      r.value_start = first;
+      r.payload_off = bp ? value : c;
+      r.info = bp ? 0x80000000u : value;
+      runs[idx] = r;
+    }
+    const uint32_t t0 = (first + kDictTile - 1) / kDictTile, t1 = (first + cnt - 1) / kDictTile;
+    for (uint32_t t = t0 + lane_id(); t <= t1; t += 64) tile_first[t] = idx;
+    nruns = idx + 1;
+  }
   DEV void error(uint32_t pos, uint32_t code) {
     if (!err_code) { err_code = code; err_pos = pos; }
   }
 };
 
-__global__ void __launch_bounds__(64) k_scan_runs(BatchDev b_in, const uint32_t *pages) {
+__global__ void __launch_bounds__(256) k_scan_runs(BatchDev b_in, const uint32_t *pages) {
   const BatchDev b = global_view(b_in);
-  __shared__ WalkLDS lds;
+  __shared__ ScanLDS lds;
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
   const uint32_t nn = b.page_nn_v[pi];
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
   uint32_t done = 0;
-  if (nn && pd.dict_bw > 0) {
-    done = hyb_walk(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs);
+  if (nn && pd.dict_bw > 0) {  // workgroup-uniform
+    done = hyb_scan(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs);
   }
-  if (lane_id() == 0) {
+  if (threadIdx.x == 0) {  // wave 0 walked: its sink holds the run count and the error
     b.run_count[pi] = rs.nruns;
     HybRun sentinel;
     sentinel.value_start = done;  // values covered by valid runs
@@ -1065,9 +946,6 @@ __global__ void __launch_bounds__(64) k_scan_runs(BatchDev b_in, const uint32_t 
 // ---------------------------------------------------------------------------
 // Values kernel: one workgroup (256 threads) per work item.
 // ---------------------------------------------------------------------------
-struct DictLDS {
-  HybRun runs[1024];
-};
 struct DeltaTileLDS {
   uint64_t scan[260];        // per-group exclusive scan + per-wave totals
   uint32_t stage[(kDeltaTileVals * 8 + 8 * 24 + 64) / 4];  // the tile's payload bytes
@@ -1078,61 +956,6 @@ struct DeltaTileLDS {
 // no byte of it is left, else ErrUnexpectedEOF.
 DEV uint32_t plain_err(uint64_t have, uint32_t w) { return (have % w) == 0 ? PQ_ERR_EOF : PQ_ERR_UNEXPECTED_EOF; }
 
-// Byte-range copy dst[0..n) = src[0..n) with arbitrary alignments. The destination is
-// walked in 16-B aligned pieces, one per lane; each piece is assembled from the two
-// 16-B aligned source blocks that cover it (dwordx4 loads; the second block is the
-// next lane's first, so the pair costs no extra HBM traffic) with v_alignbyte funnel
-// shifts. Four pieces per lane are kept in flight.
-DEV uint4 funnel16(uint4 a, uint4 b, uint32_t s) {  // bytes [s, s+16) of the 32-byte pair (a, b)
-  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t q = s >> 2, r = s & 3;
-  uint4 o;
-  switch (q) {  // wave-uniform (same source alignment for every lane)
-    case 0: o.x = __builtin_amdgcn_alignbyte(w[1], w[0], r); o.y = __builtin_amdgcn_alignbyte(w[2], w[1], r);
-            o.z = __builtin_amdgcn_alignbyte(w[3], w[2], r); o.w = __builtin_amdgcn_alignbyte(w[4], w[3], r); break;
-    case 1: o.x = __builtin_amdgcn_alignbyte(w[2], w[1], r); o.y = __builtin_amdgcn_alignbyte(w[3], w[2], r);
-            o.z = __builtin_amdgcn_alignbyte(w[4], w[3], r); o.w = __builtin_amdgcn_alignbyte(w[5], w[4], r); break;
-    case 2: o.x = __builtin_amdgcn_alignbyte(w[3], w[2], r); o.y = __builtin_amdgcn_alignbyte(w[4], w[3], r);
-            o.z = __builtin_amdgcn_alignbyte(w[5], w[4], r); o.w = __builtin_amdgcn_alignbyte(w[6], w[5], r); break;
-    default: o.x = __builtin_amdgcn_alignbyte(w[4], w[3], r); o.y = __builtin_amdgcn_alignbyte(w[5], w[4], r);
-             o.z = __builtin_amdgcn_alignbyte(w[6], w[5], r); o.w = __builtin_amdgcn_alignbyte(w[7], w[6], r); break;
-  }
-  return o;
-}
-
-DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
-  if (n == 0) return;
-  uintptr_t da = (uintptr_t)dst;
-  uint64_t head = (16 - (da & 15)) & 15;
-  if (head > n) head = n;
-  if (tid < head) dst[tid] = src[tid];
-  const uint64_t body = (n - head) & ~(uint64_t)15;
-  uint4 *d = (uint4 *)(dst + head);
-  const uint8_t *sp = src + head;
-  const uint32_t sa = (uint32_t)((uintptr_t)sp & 15);
-  const uint4 *sb = (const uint4 *)(sp - sa);
-  const uint64_t pieces = body >> 4;
-  uint64_t i = tid;
-  if (sa == 0) {
-    for (; i + 3 * (uint64_t)nt < pieces; i += 4 * (uint64_t)nt) {
-      uint4 v0 = sb[i], v1 = sb[i + nt], v2 = sb[i + 2 * nt], v3 = sb[i + 3 * nt];
-      d[i] = v0; d[i + nt] = v1; d[i + 2 * nt] = v2; d[i + 3 * nt] = v3;
-    }
-    for (; i < pieces; i += nt) d[i] = sb[i];
-  } else {
-    for (; i + 3 * (uint64_t)nt < pieces; i += 4 * (uint64_t)nt) {
-      uint4 a0 = sb[i], b0 = sb[i + 1], a1 = sb[i + nt], b1 = sb[i + nt + 1];
-      uint4 a2 = sb[i + 2 * nt], b2 = sb[i + 2 * nt + 1], a3 = sb[i + 3 * nt], b3 = sb[i + 3 * nt + 1];
-      d[i] = funnel16(a0, b0, sa);
-      d[i + nt] = funnel16(a1, b1, sa);
-      d[i + 2 * nt] = funnel16(a2, b2, sa);
-      d[i + 3 * nt] = funnel16(a3, b3, sa);
-    }
-    for (; i < pieces; i += nt) d[i] = funnel16(sb[i], sb[i + 1], sa);
-  }
-  const uint64_t tail = n - head - body;
-  if (tid < tail) dst[head + body + tid] = sp[body + tid];
-}
 
 // PLAIN fixed width (INT32/INT64/FLOAT/DOUBLE/INT96/FLBA): byte copy.
 DEV void do_plain(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
@@ -1161,94 +984,49 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   for (uint32_t v = wi.v0 + threadIdx.x; v < e1; v += blockDim.x) dst[v] = (src[v >> 3] >> (v & 7)) & 1;
 }
 
-// Dictionary indices (type_dict.go:40-60) / boolean RLE (type_boolean.go:109-120) over
-// the page's run table: 4096 values per tile, 16 consecutive values per thread.
+// Dictionary indices of a fixed-width column (type_dict.go:40-60: dst[i] = dict[idx], an index
+// outside the dictionary fails the page with "dict: invalid index") and boolean RLE
+// (type_boolean.go:109-120: value = index == 1), one kDictTile-value tile per workgroup.
+// The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
+// [w * 1024, (w + 1) * 1024) of the tile in 16 rounds of 64 consecutive values, so every
+// store instruction writes 64 consecutive outputs (256 B for 4-byte values).
 DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
-                 DictLDS &lds) {
-  uint32_t v1 = min(wi.v1, nn);
+                 DictTileLDS &lds) {
+  const uint32_t v1 = min(wi.v1, nn);
   if (wi.v0 >= v1) return;
-  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
-  const uint32_t bw = pd.dict_bw;
-  const uint32_t tile = wi.v0 / kDictTile;
-  const uint32_t nruns = b.run_count[wi.page];
-  const HybRun *runs = b.runs + b.run_base[wi.page];
-  const uint32_t *tf = b.tile_first + b.tile_base[wi.page];
+  DictTile t;
+  if (!dict_tile_load(b, pd, wi.page, wi.v0, v1, nn, lds, t)) return;
   const uint64_t vb = b.page_vbase[wi.page];
   const bool is_bool = pd.vkind == VK_RLE_BOOL;
-  const bool is_ba = !is_bool && cd.value_width == 0;
   const uint32_t w = (uint32_t)cd.value_width;
   const uint32_t dcount = cd.dict_count;
-  uint32_t r0 = 0, r1 = 0;
-  if (bw > 0) {
-    if (nruns == 0) return;  // the scan failed before this tile; error already reported
-    r0 = tf[tile];
-    if (r0 >= nruns) return;   // tile not reached by the scan (stream error)
-    uint32_t tnext = tile + 1;
-    r1 = ((uint64_t)tnext * kDictTile < nn) ? tf[tnext] : nruns - 1;
-    if (r1 >= nruns) r1 = nruns - 1;
-    v1 = min(v1, runs[nruns].value_start);  // sentinel: values covered by valid runs
-    if (wi.v0 >= v1) return;
-  }
-  uint32_t first_err = 0xffffffffu, first_err_code = 0;
-  for (uint32_t rb = r0; rb <= r1; rb += 1024) {
-    uint32_t nr = min(1024u, r1 + 1 - rb);
-    wg_barrier();
-    if (bw > 0)
-      for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) lds.runs[k] = runs[rb + k];
-    wg_barrier();
-    // value range covered by this batch of runs
-    uint32_t lo = bw > 0 ? max(wi.v0, lds.runs[0].value_start) : wi.v0;
-    uint32_t hi = v1;
-    if (bw > 0 && rb + nr <= r1) hi = min(hi, runs[rb + nr].value_start);
-    uint32_t a = wi.v0 + threadIdx.x * 16;
-    uint32_t e = min(a + 16, hi);
-    if (a < lo) a = lo;
-    if (a < e) {
-      // run of the first value: binary search in LDS
-      uint32_t ri = 0;
-      if (bw > 0) {
-        uint32_t l = 0, h = nr;
-        while (h - l > 1) {
-          uint32_t m = (l + h) >> 1;
-          if (lds.runs[m].value_start <= a) l = m; else h = m;
-        }
-        ri = l;
-      }
-      for (uint32_t v = a; v < e; v++) {
-        uint32_t idx = 0;
-        if (bw > 0) {
-          while (ri + 1 < nr && lds.runs[ri + 1].value_start <= v) ri++;
-          HybRun r = lds.runs[ri];
-          if (r.info & 0x80000000u)
-            idx = bits32c(s, pd.val_len, (uint64_t)r.payload_off * 8 + (uint64_t)(v - r.value_start) * bw, bw);
-          else idx = r.info;
-        }
-        if (is_bool) {
-          (gp_u64<uint8_t>(cd.values))[vb + v] = idx == 1;
-          continue;
-        }
-        if ((int32_t)idx < 0 || idx >= dcount) {
-          if (v < first_err) { first_err = v; first_err_code = PQ_ERR_DICT_INDEX; }
-          continue;
-        }
-        if (is_ba) {
-          const int32_t *doff = gp_u64<const int32_t>(cd.dict_offsets);
-          int32_t o0 = doff[2 * idx], o1 = doff[2 * idx + 1];
-          (gp_u64<uint64_t>(cd.ba_index))[vb + v] = cd.dict_values + (uint64_t)o0;
-          (gp_u64<int32_t>(cd.offsets))[vb + v + 1] = o1 - o0;  // length, scanned later
-        } else if (w == 4) {
-          (gp_u64<uint32_t>(cd.values))[vb + v] = (gp_u64<const uint32_t>(cd.dict_values))[idx];
-        } else if (w == 8) {
-          (gp_u64<uint64_t>(cd.values))[vb + v] = (gp_u64<const uint64_t>(cd.dict_values))[idx];
-        } else {
-          const uint8_t *src = gp_u64<const uint8_t>(cd.dict_values) + (uint64_t)idx * w;
-          uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v) * w;
-          for (uint32_t k = 0; k < w; k++) dst[k] = src[k];
-        }
-      }
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values
+  uint32_t first_err = 0xffffffffu;
+  uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
+  for (uint32_t r = 0; r < 16; r++) {
+    const uint32_t v = seg0 + r * 64 + lane;
+    if (v < t.v0 || v >= t.v1) continue;
+    const uint32_t idx = dict_tile_value(t, lds, ri, v);
+    if (is_bool) {
+      (gp_u64<uint8_t>(cd.values))[vb + v] = idx == 1;
+      continue;
+    }
+    if (idx >= dcount) {
+      first_err = min(first_err, v);
+      continue;
+    }
+    if (w == 4) {
+      (gp_u64<uint32_t>(cd.values))[vb + v] = (gp_u64<const uint32_t>(cd.dict_values))[idx];
+    } else if (w == 8) {
+      (gp_u64<uint64_t>(cd.values))[vb + v] = (gp_u64<const uint64_t>(cd.dict_values))[idx];
+    } else {
+      const uint8_t *src = gp_u64<const uint8_t>(cd.dict_values) + (uint64_t)idx * w;
+      uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v) * w;
+      for (uint32_t k = 0; k < w; k++) dst[k] = src[k];
     }
   }
-  if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, first_err_code);
+  if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
 }
 
 // DELTA_BINARY_PACKED (deltabp_decoder.go:113-174 / :272-333), one workgroup per page,
@@ -1877,7 +1655,7 @@ struct DeltaPageLDS {
 };
 
 union ValuesLDS {
-  DictLDS dict;
+  DictTileLDS dict;
   DeltaTileLDS dtile;        // WI_DELTA_TILE
   DeltaPageLDS dpage;        // WI_DELTA_PAGE
 
@@ -2323,160 +2101,6 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
 }
 
 // ---------------------------------------------------------------------------
-// BYTE_ARRAY dictionary page (page_dict.go:35-72 + type_bytearray.go:24-55):
-// walk the length-prefixed entries; dict_offsets[2i], [2i+1] = start and end
-// byte position of entry i inside the dictionary page. One lane per page.
-// ---------------------------------------------------------------------------
-__global__ void k_dict_ba(BatchDev b_in, const uint32_t *chunks) {
-  const BatchDev b = global_view(b_in);
-  if (threadIdx.x != 0) return;
-  const uint32_t ci = chunks[blockIdx.x];
-  const ChunkDesc &cd = b.chunks[ci];
-  const uint8_t *s = gp_u64<const uint8_t>(cd.dict_raw);
-  const uint32_t n = cd.dict_raw_len;
-  int32_t *offs = gp_u64<int32_t>(cd.dict_offsets);  // [2*count]: (start, end) of each entry
-  const int32_t fixed = cd.type == T_FLBA ? cd.type_length : 0;
-  uint32_t p = 0;
-  for (uint32_t v = 0; v < cd.dict_count; v++) {
-    int64_t l = fixed;
-    if (fixed == 0) {
-      if (p >= n) { report(b, ci, 0, 0, ST_DICT, v, PQ_ERR_EOF); return; }
-      if (p + 4 > n) { report(b, ci, 0, 0, ST_DICT, v, PQ_ERR_UNEXPECTED_EOF); return; }
-      l = (int32_t)ld32(s + p);
-      p += 4;
-      if (l < 0) { report(b, ci, 0, 0, ST_DICT, v, PQ_ERR_INVALID); return; }
-    }
-    if (l > 0 && p >= n) { report(b, ci, 0, 0, ST_DICT, v, PQ_ERR_EOF); return; }
-    if ((uint64_t)p + (uint64_t)l > n) { report(b, ci, 0, 0, ST_DICT, v, PQ_ERR_UNEXPECTED_EOF); return; }
-    offs[2 * v] = (int32_t)p;
-    p += (uint32_t)l;
-    offs[2 * v + 1] = (int32_t)p;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// BYTE_ARRAY offsets: lengths (stored at offsets[v+1]) -> exclusive prefix.
-// Pass 1: per-tile sums. Pass 2 (one WG per chunk): scan of tile sums.
-// Pass 3: per-tile scan + write offsets.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ba_tile_sums(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off) {
-  const BatchDev b = global_view(b_in);
-  const uint32_t ci = chunks[blockIdx.y];
-  const ChunkDesc &cd = b.chunks[ci];
-  const uint64_t nn = cd.nn_capacity;  // actual NN is page_vbase of last page + page_nn
-  const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
-  (void)nn;
-  const uint64_t t = blockIdx.x;
-  if (t * kBaTile >= total && !(t == 0)) return;
-  const int32_t *len = gp_u64<const int32_t>(cd.offsets) + 1;
-  uint64_t s = 0;
-  for (uint64_t v = t * kBaTile + threadIdx.x; v < min(total, (t + 1) * kBaTile); v += 256) s += (uint32_t)len[v];
-  __shared__ uint64_t red[256];
-  red[threadIdx.x] = s;
-  wg_barrier();
-  for (uint32_t d = 128; d > 0; d >>= 1) {
-    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-    wg_barrier();
-  }
-  if (threadIdx.x == 0) b.ba_tile_sum[tile_off[blockIdx.y] + t] = (uint32_t)min(red[0], (uint64_t)0xffffffffu);
-}
-
-__global__ void __launch_bounds__(256) k_ba_tile_scan(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off,
-                                                      uint64_t *totals) {
-  const BatchDev b = global_view(b_in);
-  const uint32_t ci = chunks[blockIdx.x];
-  const ChunkDesc &cd = b.chunks[ci];
-  const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
-  const uint64_t ntiles = (total + kBaTile - 1) / kBaTile;
-  uint32_t *ts = b.ba_tile_sum + tile_off[blockIdx.x];
-  __shared__ uint64_t part[256];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  wg_barrier();
-  for (uint64_t t0 = 0; t0 < ntiles; t0 += 256) {
-    uint64_t t = t0 + threadIdx.x;
-    uint64_t v = t < ntiles ? ts[t] : 0;
-    part[threadIdx.x] = v;
-    wg_barrier();
-    for (uint32_t d = 1; d < 256; d <<= 1) {
-      uint64_t a = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-      wg_barrier();
-      part[threadIdx.x] += a;
-      wg_barrier();
-    }
-    if (t < ntiles) ts[t] = (uint32_t)(carry + part[threadIdx.x] - v);  // exclusive tile base (< 2^31 checked on host)
-    wg_barrier();
-    if (threadIdx.x == 255) carry += part[255];
-    wg_barrier();
-  }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
-}
-
-__global__ void __launch_bounds__(256) k_ba_apply(BatchDev b_in, const uint32_t *chunks, const uint64_t *tile_off) {
-  const BatchDev b = global_view(b_in);
-  const uint32_t ci = chunks[blockIdx.y];
-  const ChunkDesc &cd = b.chunks[ci];
-  const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
-  const uint64_t t = blockIdx.x;
-  int32_t *offs = gp_u64<int32_t>(cd.offsets);
-  if (t == 0 && threadIdx.x == 0) offs[0] = 0;
-  if (t * kBaTile >= total) return;
-  const uint32_t base = b.ba_tile_sum[tile_off[blockIdx.y] + t];
-  // 16 values per thread
-  const uint64_t v0 = t * kBaTile + threadIdx.x * 16;
-  const uint64_t v1 = min(v0 + 16, min(total, (t + 1) * kBaTile));
-  uint32_t loc[16];
-  uint32_t s = 0;
-  for (uint64_t v = v0; v < v1; v++) {
-    loc[v - v0] = (uint32_t)offs[v + 1];
-    s += loc[v - v0];
-  }
-  __shared__ uint32_t part[256];
-  part[threadIdx.x] = s;
-  wg_barrier();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    uint32_t a = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-    wg_barrier();
-    part[threadIdx.x] += a;
-    wg_barrier();
-  }
-  uint32_t run = base + part[threadIdx.x] - s;
-  wg_barrier();
-  for (uint64_t v = v0; v < v1; v++) {
-    run += loc[v - v0];
-    offs[v + 1] = (int32_t)run;
-  }
-}
-
-// Payload gather: value v's bytes from ba_src[v] to payload + offsets[v]. One value per thread.
-__global__ void __launch_bounds__(256) k_ba_gather(BatchDev b_in, const uint32_t *chunks) {
-  const BatchDev b = global_view(b_in);
-  const uint32_t ci = chunks[blockIdx.y];
-  const ChunkDesc &cd = b.chunks[ci];
-  const uint32_t lp = cd.first_page + cd.num_pages - 1;
-  const uint64_t total = cd.num_pages ? b.page_vbase[lp] + b.page_nn_v[lp] : 0;
-  const int32_t *offs = gp_u64<const int32_t>(cd.offsets);
-  uint8_t *pay = gp_u64<uint8_t>(cd.payload);
-  for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (uint64_t)gridDim.x * 256) {
-    const uint64_t sa = (gp_u64<const uint64_t>(cd.ba_index))[v];
-    if (!sa) continue;  // DELTA_BYTE_ARRAY values: k_dba_gather
-    const uint8_t *src = gp_u64<const uint8_t>(sa);
-    int32_t o0 = offs[v], o1 = offs[v + 1];
-    uint8_t *dst = pay + o0;
-    uint32_t l = (uint32_t)(o1 - o0);
-    uint32_t k = 0;
-    for (; k + 4 <= l; k += 4) {
-      uint32_t x = ld32(src + k);
-      dst[k] = (uint8_t)x; dst[k + 1] = (uint8_t)(x >> 8); dst[k + 2] = (uint8_t)(x >> 16); dst[k + 3] = (uint8_t)(x >> 24);
-    }
-    for (; k < l; k++) dst[k] = src[k];
-  }
-}
-
-// ---------------------------------------------------------------------------
 // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY values (type_bytearray.go:117-140, :216-240).
 // The lengths streams were decoded into the page's scratch by WI_DLENS items (k_values);
 // one workgroup per page turns them into value lengths (offsets[v+1], scanned later by the
@@ -2495,21 +2119,6 @@ __global__ void __launch_bounds__(256) k_ba_gather(BatchDev b_in, const uint32_t
 // p_{a_(t-1)}) from its suffix). The links come from pointer jumping over the page's values
 // (k_ba_delta); k_dba_gather copies the pieces after the payload offsets are known.
 // ---------------------------------------------------------------------------
-DEV uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, uint64_t *total) {
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint64_t incl = wave_incl_scan64_dpp(v);
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  uint64_t before = 0, tot = 0;
-  for (uint32_t q = 0; q < nw; q++) {
-    const uint64_t t = wsum[q];
-    before += q < wv ? t : 0ull;
-    tot += t;
-  }
-  __syncthreads();
-  *total = tot;
-  return before + incl - v;
-}
 
 __global__ void __launch_bounds__(256) k_ba_delta(BatchDev b_in) {
   const BatchDev b = global_view(b_in);
@@ -2622,7 +2231,7 @@ __global__ void __launch_bounds__(256) k_dba_gather(BatchDev b_in) {
   const PageDesc &pd = b.pages[pi];
   if (pd.vkind != VK_DBA) return;
   const ChunkDesc &cd = b.chunks[pd.chunk];
-  if (b.chunk_err[pd.chunk] != ~0ull || !cd.payload) return;
+  if (!cd.payload || ba_page_failed(b, pd)) return;
   const uint32_t nn = min(b.page_nn_v[pi], bd.cap), cap = bd.cap;
   const uint64_t vb = b.page_vbase[pi];
   const int32_t *pre = gp_u64<const int32_t>(bd.scratch) + cap, *anc = pre + 2 * (uint64_t)cap;
@@ -2963,11 +2572,6 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
   hipLaunchKernelGGL(k_snappy, dim3(njobs), dim3(64 * kSnappyWaves), 0, s, b, jobs);
   return hipGetLastError();
 }
-hipError_t launch_dict_ba(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
-  if (!l.n_dict_ba) return hipSuccess;
-  hipLaunchKernelGGL(k_dict_ba, dim3(l.n_dict_ba), dim3(64), 0, s, b, l.dict_ba_chunks);
-  return hipGetLastError();
-}
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (l.n_level_pages_bw1)
     hipLaunchKernelGGL((k_levels_t<true, kLvThreads>), dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b,
@@ -2984,7 +2588,7 @@ hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) 
 }
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_scan_pages) return hipSuccess;
-  hipLaunchKernelGGL(k_scan_runs, dim3(l.n_scan_pages), dim3(64), 0, s, b, l.scan_pages);
+  hipLaunchKernelGGL(k_scan_runs, dim3(l.n_scan_pages), dim3(256), 0, s, b, l.scan_pages);
   return hipGetLastError();
 }
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
@@ -3013,23 +2617,4 @@ hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s
   return hipGetLastError();
 }
 
-}  // namespace pq
-
-// The BYTE_ARRAY launchers need per-chunk tile offsets; they live in host.cpp
-// (which owns that table) and call these entry points.
-namespace pq {
-hipError_t launch_ba_offsets_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, const uint64_t *tile_off,
-                                  uint32_t max_tiles, uint64_t *totals, hipStream_t s) {
-  if (!nchunks) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_tile_sums, dim3(max_tiles, nchunks), dim3(256), 0, s, b, chunks, tile_off);
-  hipLaunchKernelGGL(k_ba_tile_scan, dim3(nchunks), dim3(256), 0, s, b, chunks, tile_off, totals);
-  hipLaunchKernelGGL(k_ba_apply, dim3(max_tiles, nchunks), dim3(256), 0, s, b, chunks, tile_off);
-  return hipGetLastError();
-}
-hipError_t launch_ba_gather_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, uint32_t grid_x,
-                                 hipStream_t s) {
-  if (!nchunks) return hipSuccess;
-  hipLaunchKernelGGL(k_ba_gather, dim3(grid_x, nchunks), dim3(256), 0, s, b, chunks);
-  return hipGetLastError();
-}
 }  // namespace pq

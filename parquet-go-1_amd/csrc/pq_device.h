@@ -61,7 +61,7 @@ __host__ __device__ inline uint64_t err_key(uint32_t phase, uint32_t page, uint3
 }
 enum : uint32_t { ST_DICT = 0, ST_REP = 1, ST_DEF = 2, ST_VALUES = 3 };  // ST_DECOMP = 4 below
 
-struct PageDesc {        // 96 B
+struct PageDesc {        // 104 B
   uint64_t data;         // device address of the page payload (decompressed)
   uint32_t rep_off, rep_len;  // hybrid streams, relative to data (no length prefix)
   uint32_t def_off, def_len;
@@ -82,6 +82,8 @@ struct PageDesc {        // 96 B
   uint16_t pad0;
   uint32_t delta_mbvc;   // DELTA: values per miniblock
   uint32_t ba_delta;     // VK_DLBA / VK_DBA: index of the page's BaDelta entry
+  uint32_t ba_tile;      // byte-array chunks: global index of the page's first BA tile (kBaTile values)
+  uint32_t pad1;
 };
 
 struct ChunkDesc {       // 192 B
@@ -93,8 +95,9 @@ struct ChunkDesc {       // 192 B
   // dictionary (decoded on device into an aligned buffer)
   uint64_t dict_raw;     // device address of the dictionary page payload
   uint32_t dict_raw_len, dict_count;
-  uint64_t dict_values;  // aligned fixed-width values, or BYTE_ARRAY payload (== dict_raw + 4 offsets)
-  uint64_t dict_offsets; // BYTE_ARRAY: int32[dict_count+1] positions of each entry's bytes in dict_raw
+  uint64_t dict_values;  // fixed-width values (== dict_raw)
+  uint64_t dict_offsets; // byte-array layout: uint2[dict_count] (position of the entry's bytes in
+                         // dict_raw, length), built by the host's dictionary-page walk
   // outputs
   uint64_t values;       // fixed width
   uint64_t def_levels;   // uint8 or 0
@@ -104,16 +107,21 @@ struct ChunkDesc {       // 192 B
   uint64_t payload;      // BYTE_ARRAY bytes
   uint64_t list_offsets; // int32[records+1]
   uint64_t ba_index;     // scratch: int32 dictionary index per value (BYTE_ARRAY dict)
-  uint64_t payload_capacity;
+  uint64_t payload_capacity;  // BYTE_ARRAY payload bytes allocated (k_ba_emit writes no more)
   uint64_t page_nn;      // device uint32[num_pages]: decoded non-null counts
   uint64_t page_rec;     // device uint32[num_pages]: records (rep==0) per page
   uint64_t page_vbase;   // device uint64[num_pages]: value bases (copied from / checked against PageDesc)
   uint64_t page_rbase;   // device uint64[num_pages]: record bases
-  uint64_t pad[2];
+  uint32_t ba_tile0, ba_ntiles;  // byte-array chunks: the chunk's BA tiles [ba_tile0, +ba_ntiles)
+  uint32_t dict_max_len;         // longest dictionary entry (byte-array layout)
+  uint32_t slot_shift;           // byte-array dictionary materialised in 2^slot_shift-byte slots
+                                 // [u32 length | bytes] (4, 5 or 6; 0: entries over 60 bytes, no table)
+  uint64_t dict_slots;           // device address of the slot table (k_dict_slots, every decode)
 };
 
 // Chunk flags
-enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8 };
+enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8,
+                 CF_BA_SYNC = 16 };  // byte-array payload without an upload-time bound: sized after the scan
 
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,

@@ -78,7 +78,8 @@ class BatchStats(ctypes.Structure):
 
 
 _LIB = None
-ABI_VERSION = 2  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+TIMER_SLOTS = 16  # PQGPU_TIMER_SLOTS
+ABI_VERSION = 3  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -86,7 +87,7 @@ _EXPORTS = [
     "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
     "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
-    "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages",
+    "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
 ]
 
 
@@ -134,6 +135,7 @@ def lib():
                                      ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         "pqgpu_batch_chunk_pages": ([P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), P, P, P, P, ctypes.c_int32, E],
                                     ctypes.c_int),
+        "pqgpu_batch_kernel_bytes": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -355,14 +357,16 @@ class Batch:
         return ms.value, n.value, name.value.decode()
 
     def kernel_times(self):
-        """{kernel name: (average ms per launch, launches)} for every timed launch slot."""
+        """{kernel name: (average ms per launch, launches, algorithmic bytes per launch)} for every
+        timed launch slot that ran."""
         out = {}
-        for k in range(12):  # PQGPU_TIMER_SLOTS
-            ms, n = ctypes.c_double(), ctypes.c_int64()
+        for k in range(TIMER_SLOTS):
+            ms, n, nb = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
             name = ctypes.create_string_buffer(64)
             lib().pqgpu_batch_kernel_slot(self._h, k, ctypes.byref(ms), ctypes.byref(n), name, 64)
+            lib().pqgpu_batch_kernel_bytes(self._h, k, ctypes.byref(nb))
             if n.value:
-                out[name.value.decode()] = (ms.value, n.value)
+                out[name.value.decode()] = (ms.value, n.value, nb.value)
         return out
 
     def pages(self, cid):

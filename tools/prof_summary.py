@@ -1,56 +1,83 @@
-"""Summarise a rocprofv3 kernel trace (SQLite .db or *_kernel_stats.csv / *_kernel_trace.csv) per kernel."""
+"""Summarise tools/prof.sh output into profiles/<round>_pmc_<config>.json: per kernel the
+kernel-trace average duration, FETCH_SIZE / WRITE_SIZE per launch (FETCH_SIZE doubled: gfx950
+wide streaming reads count half, MI355X_MICROARCH.md §HBM), the corrected HBM bytes, and the SQ
+counters (waves, stall buckets, LDS bank-conflict cycles / LDS cycles). bench.py reads
+`hbm_bytes_corrected` of its dominant kernel as roofline.traffic.
+usage: python tools/prof_summary.py <config> [round]"""
 import csv
 import glob
+import json
 import os
-import sqlite3
 import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def from_db(path):
-    c = sqlite3.connect(path)
-    q = ("select name, count(*), avg(duration), min(duration), max(duration), sum(duration), max(grid_x), "
-         "max(workgroup_x), max(vgpr_count), max(sgpr_count), max(lds_size), max(scratch_size) "
-         "from kernels group by name order by sum(duration) desc")
-    return list(c.execute(q))
+def short(name):
+    n = name.split("(")[0].split("<")[0]
+    for p in ("pq::", "void "):
+        n = n.replace(p, "")
+    return n.strip()
 
 
-def from_trace_csv(path):
-    rows = {}
+def per_dispatch(path):
+    """{counter: {kernel: [value per dispatch]}} (values summed over XCD / SE instances)."""
+    acc = defaultdict(float)
+    names = {}
     for r in csv.DictReader(open(path)):
-        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        k = r["Kernel_Name"]
-        e = rows.setdefault(k, [k, 0, 0, 1 << 62, 0, 0, 0, 0, 0, 0, 0, 0])
-        e[1] += 1
-        e[5] += d
-        e[3] = min(e[3], d)
-        e[4] = max(e[4], d)
-        e[6] = max(e[6], int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0))
-        e[7] = max(e[7], int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 0)) or 0))
-        e[8] = max(e[8], int(r.get("VGPR_Count", 0) or 0))
-        e[9] = max(e[9], int(r.get("SGPR_Count", 0) or 0))
-        e[10] = max(e[10], int(r.get("LDS_Block_Size", r.get("Lds_Size", 0)) or 0))
-        e[11] = max(e[11], int(r.get("Scratch_Size", 0) or 0))
-    out = []
-    for e in rows.values():
-        e[2] = e[5] / e[1]
-        out.append(tuple(e))
-    return sorted(out, key=lambda x: -x[5])
+        d = int(r["Dispatch_Id"])
+        acc[(r["Counter_Name"], d)] += float(r["Counter_Value"])
+        names[d] = short(r["Kernel_Name"])
+    out = defaultdict(lambda: defaultdict(list))
+    for (c, d), v in sorted(acc.items(), key=lambda x: x[0][1]):
+        out[c][names[d]].append(v)
+    return out
 
 
-def main(path):
-    if os.path.isdir(path):
-        dbs = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
-        csvs = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
-        path = (csvs or dbs)[0]
-    rows = from_db(path) if path.endswith(".db") else from_trace_csv(path)
-    print(f"# source: {os.path.basename(path)} (durations in microseconds)")
-    print(f"{'kernel':60s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} {'total_us':>11s} "
-          f"{'grid':>8s} {'wg':>4s} {'vgpr':>5s} {'sgpr':>5s} {'lds':>6s} {'scratch':>7s}")
-    for r in rows:
-        name = r[0].split("(")[0][:60]
-        print(f"{name:60s} {r[1]:6d} {r[2] / 1e3:10.2f} {r[3] / 1e3:10.2f} {r[4] / 1e3:10.2f} {r[5] / 1e3:11.1f} "
-              f"{r[6]:8d} {r[7]:4d} {r[8]:5d} {r[9]:5d} {r[10]:6d} {r[11]:7d}")
+def main(cfg, rnd="r02"):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{cfg}")
+    res = defaultdict(dict)
+    trace = glob.glob(os.path.join(src, "stats", "**", "*kernel_trace.csv"), recursive=True)
+    if trace:
+        dur = defaultdict(list)
+        for r in csv.DictReader(open(trace[0])):
+            dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for k, v in dur.items():
+            res[k]["trace_avg_us"] = round(sum(v) / len(v), 2)
+            res[k]["trace_dispatches"] = len(v)
+    for sub in ("fetch", "write", "sq"):
+        f = glob.glob(os.path.join(src, sub, "**", "*counter_collection.csv"), recursive=True)
+        if not f:
+            continue
+        for c, ks in per_dispatch(f[0]).items():
+            for k, v in ks.items():
+                res[k][c] = round(sum(v) / len(v), 1)
+    for k, r in res.items():
+        if "FETCH_SIZE" in r or "WRITE_SIZE" in r:
+            fk, wk = r.get("FETCH_SIZE", 0.0), r.get("WRITE_SIZE", 0.0)
+            r["hbm_bytes_raw"] = int((fk + wk) * 1024)
+            r["hbm_bytes_corrected"] = int((2 * fk + wk) * 1024)
+        if r.get("SQ_LDS_IDX_ACTIVE"):
+            r["lds_bank_conflict_frac"] = round(r.get("SQ_LDS_BANK_CONFLICT", 0) / r["SQ_LDS_IDX_ACTIVE"], 4)
+        if r.get("SQ_WAVE_CYCLES") and r.get("trace_avg_us"):
+            # SQ_WAVE_CYCLES counts quad-cycles of resident waves: mean resident waves per CU
+            # at the clock the chip holds (~2.1 GHz under load assumed)
+            r["mean_waves_per_cu"] = round(4 * r["SQ_WAVE_CYCLES"] / (r["trace_avg_us"] * 1e-6 * 2.1e9) / 256, 2)
+        if r.get("SQ_WAVE_CYCLES"):
+            w = r["SQ_WAVE_CYCLES"]
+            r["stall_frac"] = {"wait_any": round(r.get("SQ_WAIT_ANY", 0) / w, 3),
+                               "wait_inst_any": round(r.get("SQ_WAIT_INST_ANY", 0) / w, 3),
+                               "active_inst_any": round(r.get("SQ_ACTIVE_INST_ANY", 0) / w, 3)}
+    out = {"source": "tools/prof.sh (rocprofv3: kernel trace; --pmc FETCH_SIZE, WRITE_SIZE and 8 SQ counters, "
+                     "separate passes)", "config": cfg,
+           "command": f"python3 bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu-baseline",
+           "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads, MI355X_MICROARCH.md HBM section)",
+           "kernels": res}
+    path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{cfg}.json")
+    json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:])
