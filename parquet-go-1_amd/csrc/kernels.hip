@@ -390,32 +390,38 @@ struct LevelSink {
 //      stream links p -> p + adv (EXIT when that leaves the chunk); anything else (errors,
 //      runs cut by EOF, longer varints) is a stop: a self-link.
 //  P2  doubling: J[j+1][p] = J[j][J[j][p]] for j < kLvLevels (jumps of 2^j runs, saturating
-//      at a stop or the chunk exit); every level is kept.
+//      at a stop or the chunk exit), in two ping-pong tables; J[0] is kept.
 //  P3  one lane follows the true chain from the chunk entry by 2^kLvLevels-run jumps and
-//      marks each node it lands on.
-//  P4  marking, top down: for j = kLvLevels-1 .. 0 every marked node marks J[j][node]. A
-//      chain node at distance d from the entry is reached through the binary digits of d,
-//      so afterwards exactly the chain's nodes are marked (a lane that sees a mark set in
-//      the same round only marks further chain nodes early).
-//  P5  value indices: a workgroup prefix sum, in position order, of the marked runs'
-//      value counts; the chain's last node gives the next chunk's entry.
-//  P6  fill: every marked run is expanded by the thread that owns its position (bit
-//      width 1 with validity output only ORs whole 32-bit words of payload into the LDS
-//      bitmap; other widths go through LevelSink::piece); runs longer than kLvLongRun
-//      values are expanded by the whole workgroup.
+//      records each node it lands on: the checkpoints (at most 64: a run takes >= 2 bytes).
+//  P4  wave 0, lane w: from checkpoint w, walk the next 2^kLvLevels runs over J[0] and mark
+//      them: afterwards exactly the chain's nodes are marked.
+//  P5  value indices: a workgroup prefix sum, in position order, of the marked runs' value
+//      counts; the chain's last node gives the next chunk's entry.
+//  P6  fill: every marked run is expanded by the thread that owns its position (bit width 1
+//      with validity output only ORs whole 32-bit words of payload into an LDS bitmap; other
+//      widths go through LevelSink::piece); runs longer than kLvLongRun values are expanded
+//      by the whole workgroup.
 // A stop on the chain is decoded exactly (decode_hdr, the reference's full header
 // semantics): an error or a bit-packed run cut by EOF ends the stream; a valid run the
 // fast form could not take (a long varint) is expanded and the next chunk starts after it.
 // Runs past the one that reaches num_values are never read, as in the reference's
 // decodePackedArray loop; results, error class and error value position are identical.
+// The page's latency (not bandwidth) sets the kernel's time, so the workgroup's footprint
+// is kept small (26 KB LDS, 80 VGPRs): six pages are resident per CU.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLvThreads = 256;
 constexpr uint32_t kLvChunk = 2048;             // candidate header positions per chunk
 #ifndef PQ_LV_LEVELS
-#define PQ_LV_LEVELS 5
+#define PQ_LV_LEVELS 4
 #endif
-constexpr uint32_t kLvLevels = PQ_LV_LEVELS;    // J[kLvLevels] jumps 2^kLvLevels runs
-constexpr uint32_t kLvPer = kLvChunk / kLvThreads;  // positions per thread (contiguous in P5/P6)
+#ifndef PQ_LV_WPE
+#define PQ_LV_WPE 6  // k_levels_bw1 waves per SIMD (= resident pages per CU)
+#endif
+constexpr uint32_t kLvLevels = PQ_LV_LEVELS;    // checkpoints every 2^kLvLevels runs
+constexpr uint32_t kLvSeg = 1u << kLvLevels;    // runs per walker
+constexpr uint32_t kLvMaxCkp = kLvChunk / 2 / kLvSeg;  // chain nodes <= kLvChunk / 2
+static_assert(kLvMaxCkp <= 64, "one walker lane per checkpoint");
+constexpr uint32_t kLvPer = kLvChunk / kLvThreads;  // positions per thread in P1
 constexpr uint32_t kLvStageB = kLvChunk + 256;  // staged bytes: the chunk + headers / payload past its end
 constexpr uint32_t kLvLongRun = 512;            // runs longer than this expand cooperatively
 constexpr uint32_t kLvMaxLong = 64;
@@ -425,12 +431,15 @@ enum : uint32_t { LV_RUN = 0, LV_STOP_NEED = 1, LV_STOP_ERR = 2, LV_STOP_TRUNC =
 
 struct LevelLDS {
   uint32_t stage[kLvStageB / 4 + 4];
-  uint16_t J[kLvLevels + 1][kLvChunk];  // J[j][i]: chunk offset 2^j runs after i; i = stop; kLvExit
-  uint8_t mark[kLvChunk];
+  uint16_t J0[kLvChunk];                // J0[i]: chunk offset of the next run after i; i = stop; kLvExit
+  uint16_t JA[kLvChunk], JB[kLvChunk];  // doubling ping-pong
+  uint16_t ckp[kLvMaxCkp];
+  uint8_t mark[kLvChunk];               // chain nodes of the chunk
   uint64_t wsum[kLvThreads / 64];
+  uint32_t nckp;
   uint32_t long_f[kLvMaxLong], long_cnt[kLvMaxLong], long_bp[kLvMaxLong], long_val[kLvMaxLong];
   uint32_t nlong, stop_kind, stop_code, stop_vpos, next_e;
-  unsigned long long done_out;
+  uint64_t total;
   uint64_t cnt[16];
   uint32_t bits[kSegSlots / 32];
 };
@@ -539,14 +548,13 @@ DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uin
 // Decode `need` level values of one stream into the sink; every thread of the workgroup
 // calls this (control flow outside per-lane work is workgroup-uniform). Chunks are fixed
 // stream ranges [k * kLvChunk, (k + 1) * kLvChunk); the chain enters chunk k where it left
-// chunk k - 1 (chunks a long run jumps over are skipped). Thread t owns chunk positions
-// [8t, 8t + 8): their headers are decoded once (P1) and kept in registers for the fill.
+// chunk k - 1 (chunks a long run jumps over are skipped).
 template <bool BW1>
 DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
   static_assert(kLvPer == 8, "8 positions per thread");
   const uint8_t *s = sk.s;
   const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   const uint32_t i0 = tid * kLvPer;
   constexpr uint32_t kWords = kLvStageB / 4 + 4, kWpt = (kWords + kLvThreads - 1) / kLvThreads;
   uint32_t pre[kWpt];
@@ -578,8 +586,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     if (cs + kLvChunk < n) { fetch(cs + kLvChunk); fetched = cs + kLvChunk; }  // lands during this chunk
     wg_barrier();
     st.lap(0);
-    // ---- P1: links of positions [i0, i0 + 8) from five staged words; headers kept in registers
-    uint32_t nv[kLvPer], val[kLvPer], bpm = 0, stopm = 0;
+    // ---- P1: links of positions [i0, i0 + 8) from five staged words; value counts kept
+    uint32_t nv[kLvPer];
     {
       uint32_t W[5];
 #pragma unroll
@@ -600,57 +608,58 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         const uint32_t rval = rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u));
         const bool ok = i < clen && t != 0 && cnt != 0 && (uint64_t)c + adv <= n && (isbp || bw >= 32 || (rval >> bw) == 0);
         nv[k] = ok ? (isbp ? cnt * 8 : cnt) : 0u;
-        val[k] = isbp ? c + Lv : rval;
-        bpm |= (ok && isbp) ? 1u << k : 0u;
-        stopm |= ok ? 0u : 1u << k;
         jj[k] = !ok ? i : ((uint64_t)i + adv >= clen ? (uint32_t)kLvExit : i + (uint32_t)adv);
       }
-      *(uint4 *)&L.J[0][i0] = make_uint4(jj[0] | (jj[1] << 16), jj[2] | (jj[3] << 16), jj[4] | (jj[5] << 16), jj[6] | (jj[7] << 16));
+      *(uint4 *)&L.J0[i0] = make_uint4(jj[0] | (jj[1] << 16), jj[2] | (jj[3] << 16), jj[4] | (jj[5] << 16), jj[6] | (jj[7] << 16));
       *(uint2 *)&L.mark[i0] = make_uint2(0u, 0u);
     }
     wg_barrier();
     st.lap(1);
-    // ---- P2: doubling (every level kept for the marking)
-    const uint32_t levels = PQ_ABLATE(sk, 3) ? 0u : kLvLevels;  // diagnostic: serial walk of every run
-    for (uint32_t lv = 0; lv < levels; lv++) {
-      const uint4 A = *(const uint4 *)&L.J[lv][i0];
+    // ---- P2: doubling into the ping-pong tables
+    const uint16_t *top = L.J0;
+    for (uint32_t lv = 0; lv < kLvLevels; lv++) {
+      uint16_t *dst = (lv & 1) ? L.JB : L.JA;
+      const uint4 A = *(const uint4 *)&top[i0];
       const uint32_t a[8] = {A.x & 0xffffu, A.x >> 16, A.y & 0xffffu, A.y >> 16, A.z & 0xffffu, A.z >> 16, A.w & 0xffffu, A.w >> 16};
       uint32_t r[8];
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++) {
         const bool fix = a[k] == kLvExit || a[k] == i0 + k;
-        const uint32_t b2 = L.J[lv][fix ? i0 + k : a[k]];
+        const uint32_t b2 = top[fix ? i0 + k : a[k]];
         r[k] = fix ? a[k] : b2;
       }
-      *(uint4 *)&L.J[lv + 1][i0] = make_uint4(r[0] | (r[1] << 16), r[2] | (r[3] << 16), r[4] | (r[5] << 16), r[6] | (r[7] << 16));
+      *(uint4 *)&dst[i0] = make_uint4(r[0] | (r[1] << 16), r[2] | (r[3] << 16), r[4] | (r[5] << 16), r[6] | (r[7] << 16));
+      top = dst;
       wg_barrier();
     }
     st.lap(2);
-    // ---- P3: the chain by 2^levels-run jumps (one lane)
+    // ---- P3: the checkpoints, by 2^kLvLevels-run jumps (one lane)
     if (tid == 0) {
       __builtin_amdgcn_s_setprio(3);
-      uint32_t p = e0;
+      uint32_t p = e0, k = 0;
       for (;;) {
-        L.mark[p] = 1;
-        const uint32_t q = L.J[levels][p];
-        if (q == kLvExit || q == p) break;
+        L.ckp[k++] = (uint16_t)p;
+        const uint32_t q = top[p];
+        if (q == kLvExit || q == p || k == kLvMaxCkp) break;
         p = q;
       }
+      L.nckp = k;
       __builtin_amdgcn_s_setprio(0);
     }
     wg_barrier();
-    // ---- P4: marking, top down
-    for (int lv = (int)levels - 1; lv >= 0; lv--) {
-      const uint2 M = *(const uint2 *)&L.mark[i0];
-      const uint4 A = *(const uint4 *)&L.J[lv][i0];
-      const uint32_t a[8] = {A.x & 0xffffu, A.x >> 16, A.y & 0xffffu, A.y >> 16, A.z & 0xffffu, A.z >> 16, A.w & 0xffffu, A.w >> 16};
-      const uint64_t m = ((uint64_t)M.y << 32) | M.x;
-#pragma unroll
-      for (uint32_t k = 0; k < 8; k++)
-        if (((m >> (8 * k)) & 0xffu) && a[k] != kLvExit) L.mark[a[k]] = 1;
-      wg_barrier();
-    }
     st.lap(3);
+    // ---- P4 (wave 0): one walker per checkpoint marks its 2^kLvLevels runs
+    if (tid < L.nckp) {
+      uint32_t p = L.ckp[tid];
+      for (uint32_t k = 0; k < kLvSeg; k++) {
+        L.mark[p] = 1;
+        const uint32_t q = L.J0[p];
+        if (q == p || q == kLvExit) break;
+        p = q;
+      }
+    }
+    wg_barrier();
+    st.lap(4);
     // ---- P5: value counts of this thread's marked runs, workgroup scan
     uint32_t mbits = 0;
     {
@@ -664,11 +673,16 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     uint64_t mine = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 8; k++) mine += (mbits >> k) & 1u ? nv[k] : 0u;
-    if (mbits & stopm) {  // a stop on the chain: the exact decoder (hybrid_decoder.go:142-165)
-      sk_k = __builtin_ctz(mbits & stopm);
-      sh = decode_hdr(L.stage, cs, s, cs + i0 + sk_k, n, bw, rs);
-      mine += sh.err ? 0u : min(sh.nvals, sh.okvals);
+    for (uint32_t mm = mbits; mm; mm &= mm - 1) {
+      const uint32_t k = __builtin_ctz(mm);
+      if (L.J0[i0 + k] == i0 + k) {  // a stop on the chain: the exact decoder (hybrid_decoder.go:142-165)
+        sk_k = k;
+        sh = decode_hdr(L.stage, cs, s, cs + i0 + k, n, bw, rs);
+        mine += sh.err ? 0u : min(sh.nvals, sh.okvals);
+        break;
+      }
     }
+    const uint32_t lane = lane_id(), wv = tid >> 6;
     const uint64_t incl = wave_incl_scan64_dpp(mine);
     if (lane == 63) L.wsum[wv] = incl;
     wg_barrier();
@@ -679,8 +693,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       before += q < wv ? t : 0ull;
       total += t;
     }
+    if (tid == 0) L.total = total;
     uint64_t v = (uint64_t)done + before + incl - mine;  // value index of this thread's first marked run
-    st.lap(4);
     // ---- P6: fill (and the chain's end: exit position or the exact stop)
     while (mbits) {
       const uint32_t k = __builtin_ctz(mbits);
@@ -703,8 +717,9 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         }
         break;
       }
-      lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(nv[k], rem), (bpm >> k) & 1u, val[k]);
-      if (L.J[0][i0 + k] == kLvExit) L.next_e = p + fast_hdr(L.stage, cs, p, n, bw, rs).adv;  // the chain's last node
+      const FastHdr f = fast_hdr(L.stage, cs, p, n, bw, rs);
+      lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(nv[k], rem), f.bp, f.value);
+      if (L.J0[i0 + k] == kLvExit) L.next_e = p + f.adv;  // the chain's last node
       v += nv[k];
     }
     st.lap(5);
@@ -723,7 +738,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     if (nlong) wg_barrier();
     st.lap(6);
     const uint32_t kind = L.stop_kind;
-    const uint64_t ndone = (uint64_t)done + total;
+    const uint64_t ndone = (uint64_t)done + L.total;
     if (kind != LV_RUN) {
       if (kind == LV_STOP_ERR || kind == LV_STOP_TRUNC) sk.error(L.stop_vpos, L.stop_code);
       break;
@@ -737,10 +752,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
 
 // BW1: every level stream of the pages is a bit-width-1 definition stream with validity
 // output only (flat OPTIONAL columns: max_def == 1, max_rep == 0).
-template <bool BW1, int NT>
-__global__ void __launch_bounds__(NT) k_levels_t(BatchDev b_in, const uint32_t *pages) {
-  const BatchDev b = global_view(b_in);
-  __shared__ LevelLDS lds;
+template <bool BW1>
+DEV void levels_page(const BatchDev &b, const uint32_t *pages, LevelLDS &lds) {
   const uint32_t pi = pages[blockIdx.x];
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
@@ -820,6 +833,20 @@ __global__ void __launch_bounds__(NT) k_levels_t(BatchDev b_in, const uint32_t *
   st.lap(6);
   st.flush(0);
   if (tid == 0) b.page_nn[pi] = nn;
+}
+
+// Flat OPTIONAL columns (bit width 1, validity only): held to 80 VGPRs so six workgroups fit
+// per CU (24 KB LDS each): the kernel is latency-bound per page, so resident pages set its time.
+__global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu(PQ_LV_WPE))) k_levels_bw1(BatchDev b_in,
+                                                                                               const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelLDS lds;
+  levels_page<true>(b, pages, lds);
+}
+__global__ void __launch_bounds__(kLvThreads) k_levels(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelLDS lds;
+  levels_page<false>(b, pages, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -2574,11 +2601,9 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (l.n_level_pages_bw1)
-    hipLaunchKernelGGL((k_levels_t<true, kLvThreads>), dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b,
-                       l.level_pages_bw1);
+    hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
   if (l.n_level_pages)
-    hipLaunchKernelGGL((k_levels_t<false, kLvThreads>), dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b,
-                       l.level_pages);
+    hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
   return hipGetLastError();
 }
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

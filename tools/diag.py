@@ -7,11 +7,12 @@ os.environ.setdefault("PQGPU_LIB", os.path.join(os.path.dirname(os.path.dirname(
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
-import bench  # noqa: E402
 import pqgpu  # noqa: E402
+from tools import workloads  # noqa: E402
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4 * 4194304
-data, _ = bench.gen_cfg2(rows)
+out = workloads.gen_cfg2(rows)
+data = out[0] if isinstance(out, tuple) else out
 ctx = pqgpu.Context(0)
 f = pqgpu.File(data)
 b = pqgpu.Batch(ctx)
