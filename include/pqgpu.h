@@ -15,9 +15,10 @@
  *    and a message mirroring the reference's error text.
  *  - Error classes mirror the Go error values the reference returns; the
  *    numbering is shared with the CPU oracle (oracle/oracle.h).
- *  - Thread safety: one pqgpu_ctx per GPU; a ctx and its batches are used
- *    by one host thread at a time (the reference FileReader is not
- *    goroutine-safe either, file_reader.go:18).
+ *  - Thread safety: one pqgpu_ctx per GPU; a batch is used by one host
+ *    thread at a time (the reference FileReader is not goroutine-safe
+ *    either, file_reader.go:18); different batches of one ctx may be driven
+ *    from different threads on different streams (the pipeline does).
  */
 #ifndef PQGPU_H
 #define PQGPU_H
@@ -28,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 3
+#define PQGPU_ABI_VERSION 4
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -198,6 +199,12 @@ int pqgpu_batch_sync(pqgpu_batch *b, void *stream, pqgpu_error *err);
 int pqgpu_batch_num_chunks(const pqgpu_batch *b);
 /* Per-chunk status after sync (the error of that chunk alone). */
 int pqgpu_batch_chunk_status(const pqgpu_batch *b, int32_t chunk_id, pqgpu_error *err);
+/* A failed chunk returns its error; when the failure is a page's readValues
+ * error (err->page >= 0, not a decompression or CRC error, which the
+ * reference raises in readPages before any value is read), *out still
+ * describes the decoded pages before the failing page — the rows the
+ * reference's lazy page reader returns before it fails (data_store.go:236-260).
+ * Otherwise *out is zeroed. */
 int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t chunk_id, pqgpu_chunk_result *out, pqgpu_error *err);
 /* Per-page split of a decoded chunk, the reference's pageReader granularity
  * (ColumnStore.readNextPage data_store.go:236-260 reads one page at a time):
@@ -209,7 +216,8 @@ int pqgpu_batch_chunk_pages(const pqgpu_batch *b, int32_t chunk_id, int32_t *num
                             int64_t *slot_count, int64_t *value_first, int64_t *value_count, int32_t cap,
                             pqgpu_error *err);
 /* Copy one chunk's outputs to host buffers sized from pqgpu_batch_chunk_result
- * (any pointer may be NULL to skip that array). */
+ * (any pointer may be NULL to skip that array); for a chunk that failed in a
+ * page, the pages before it are copied and the error is returned. */
 int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values, int32_t *offsets, uint8_t *payload,
                            uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
                            pqgpu_error *err);
@@ -230,6 +238,50 @@ int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *l
 /* Algorithmic bytes (sections read + outputs written, counted once) of one launch
  * of timer slot `slot` for the last synced decode: the roofline numerator of that kernel. */
 int pqgpu_batch_kernel_bytes(const pqgpu_batch *b, int slot, int64_t *bytes);
+
+/* Device-to-device (or host) copy on the library's own HIP runtime, for
+ * callers that hold device pointers of a chunk result, e.g. when gathering
+ * a row-group shard into one column: hipMemcpy, hipMemcpyDefault. */
+int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_error *err);
+
+/* ---- streaming row-group pipeline -------------------------------------
+ * FileReader.readRowGroupData (chunk_reader.go:375-404) called for row group
+ * after row group (file_reader.go:187-198), as a stream: host worker threads
+ * plan row group k + 1 .. k + depth - 1 (page-header walk, GZIP and
+ * dictionary pages, pinned staging) and enqueue its H2D copy and decode on
+ * its own stream while the GPU decodes row group k. Each row group is one
+ * batch holding the requested columns; batches come back in row-group order. */
+typedef struct pqgpu_pipeline pqgpu_pipeline;
+typedef struct {
+  int32_t depth;         /* row groups in flight (batches); >= 2 double-buffers, default 3 */
+  int32_t threads;       /* host planner threads; 0 = depth */
+  int32_t validate_crc;  /* WithCRC32Validation (file_reader.go:134-139) */
+  int32_t pad;
+} pqgpu_pipeline_opts;
+typedef struct {
+  int64_t row_groups;      /* row groups returned so far */
+  int64_t rows;
+  int64_t chunks;
+  int64_t failed_chunks;
+  int64_t input_bytes;     /* staged page bytes uploaded (H2D) */
+  int64_t output_bytes;    /* decoded bytes materialised */
+  double wall_ms;          /* pipeline create .. last row group returned */
+  double plan_ms;          /* host page-header walks + staging, summed over threads */
+  double upload_ms;        /* host side of pqgpu_batch_upload (descriptors, pinned copy), summed */
+  double h2d_ms;           /* GPU: upload enqueue .. done, summed over row groups */
+  double decode_ms;        /* GPU: decode launches .. done, summed over row groups */
+} pqgpu_pipeline_stats;
+/* rgs / cols may be NULL for all row groups / all columns. */
+int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const int32_t *rgs, int32_t n_rgs, const int32_t *cols,
+                          int32_t n_cols, const pqgpu_pipeline_opts *opts, pqgpu_pipeline **out, pqgpu_error *err);
+/* The next row group, decoded and synced: *batch holds its chunks (column
+ * order of `cols`), *rg its index; the batch stays valid until
+ * pqgpu_pipeline_release. At the end *batch is NULL and PQ_OK is returned.
+ * The return value is the batch's first chunk error (as pqgpu_batch_sync). */
+int pqgpu_pipeline_next(pqgpu_pipeline *p, pqgpu_batch **batch, int32_t *rg, pqgpu_error *err);
+int pqgpu_pipeline_release(pqgpu_pipeline *p, pqgpu_batch *batch);
+int pqgpu_pipeline_stats_get(const pqgpu_pipeline *p, pqgpu_pipeline_stats *out);
+void pqgpu_pipeline_destroy(pqgpu_pipeline *p);
 
 #ifdef __cplusplus
 }

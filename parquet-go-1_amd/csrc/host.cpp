@@ -23,16 +23,10 @@
 #include <vector>
 
 #include "../../include/pqgpu.h"
+#include "ctx.h"
 #include "format.h"
 #include "kernels.h"
 #include "pq_device.h"
-
-namespace pq {
-hipError_t launch_ba_offsets_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, const uint64_t *tile_off,
-                                  uint32_t max_tiles, uint64_t *totals, hipStream_t s);
-hipError_t launch_ba_gather_impl(const BatchDev &b, const uint32_t *chunks, uint32_t nchunks, uint32_t grid_x,
-                                 hipStream_t s);
-}  // namespace pq
 
 using namespace pq;
 
@@ -56,11 +50,6 @@ static void clear_err(pqgpu_error *e) {
     }                                                                                                  \
   } while (0)
 
-struct pqgpu_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
-};
 
 struct pqgpu_file {
   FileMeta meta;
@@ -252,6 +241,9 @@ struct HostChunk {
   bool ba_sync = false;       // no upload-time payload bound: size it after the scan (host sync)
   uint64_t payload_off = 0;   // offset in the batch payload arena (bounded chunks)
   uint64_t payload_bound = 0; // its size (k_ba_emit writes nothing past it)
+  // a chunk that failed in page k (readValues): the decoded prefix, pages [0, k)
+  bool partial = false;
+  int64_t part_slots = 0, part_nn = 0, part_records = 0, part_payload = 0;
   uint64_t payload_cap = 0;
   uint8_t *payload = nullptr;  // the chunk's payload (arena slice, or own allocation when ba_sync)
   bool payload_own = false;
@@ -1552,6 +1544,23 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     clear_err(&hc.dev_err);
     hc.dev_err.chunk = (int)c;
     if (!hc.err.code && keys[c] != ~0ull) decode_key(keys[c], (int)c, &hc.dev_err);
+    // a page's readValues error leaves the pages before it decoded (the reference's lazy page
+    // reader returns their rows first, data_store.go:236-260); decompression and CRC errors are
+    // readPages errors (chunk_reader.go:161-180): nothing of the chunk is returned
+    hc.partial = !hc.err.code && hc.dev_err.code && hc.dev_err.page >= 0 && hc.dev_err.code != PQ_ERR_DECOMPRESS &&
+                 hc.dev_err.code != PQ_ERR_CRC && (uint32_t)hc.dev_err.page < hc.num_pages;
+    if (hc.partial) {
+      const uint32_t fp = hc.first_page + (uint32_t)hc.dev_err.page;
+      hc.part_slots = (int64_t)b->pages[fp].slot_base;
+      hc.part_nn = (int64_t)vbase[fp];
+      hc.part_records = (int64_t)rbase[fp];
+      hc.part_payload = 0;
+      if (hc.value_width == 0 && hc.part_nn > 0 && hc.o_offsets) {
+        int32_t end = 0;
+        HIPCHECK(hipMemcpy(&end, A + hc.o_offsets + 4 * (uint64_t)hc.part_nn, 4, hipMemcpyDeviceToHost), err);
+        hc.part_payload = end;
+      }
+    }
     if (!hc.err.code && hc.sync_err && !hc.dev_err.code)
       set_err(&hc.dev_err, PQ_ERR_UNSUPPORTED, (int)c, -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
     if (!ba_tot.empty() && hc.value_width == 0) hc.payload_bytes = (int64_t)ba_tot[c];
@@ -1909,13 +1918,13 @@ int pqgpu_batch_chunk_pages(const pqgpu_batch *b, int32_t id, int32_t *num_pages
 int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_result *out, pqgpu_error *err) {
   int e = pqgpu_batch_chunk_status(b, id, err);
   memset(out, 0, sizeof(*out));
-  if (e) return e;
+  if (e && (e == PQ_ERR_ARG || !b->chunks[(size_t)id].partial)) return e;
   const HostChunk &hc = b->chunks[(size_t)id];
   uint8_t *A = b->d_arena;
-  out->num_slots = (int64_t)hc.num_slots;
-  out->num_values = hc.nn;
-  out->num_records = hc.records;
-  out->payload_bytes = hc.payload_bytes;
+  out->num_slots = e ? hc.part_slots : (int64_t)hc.num_slots;
+  out->num_values = e ? hc.part_nn : hc.nn;
+  out->num_records = e ? hc.part_records : hc.records;
+  out->payload_bytes = e ? hc.part_payload : hc.payload_bytes;
   out->physical_type = hc.col.physical_type;
   out->value_width = hc.value_width;
   out->max_def = hc.col.max_def;
@@ -1927,15 +1936,15 @@ int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_resul
   out->rep_levels = hc.o_rep ? A + hc.o_rep : nullptr;
   out->validity = hc.o_valid ? (uint32_t *)(A + hc.o_valid) : nullptr;
   out->list_offsets = hc.o_lists ? (int32_t *)(A + hc.o_lists) : nullptr;
-  return PQ_OK;
+  return e;
 }
 
 int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32_t *offsets, uint8_t *payload,
                            uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
                            pqgpu_error *err) {
   pqgpu_chunk_result r;
-  int e = pqgpu_batch_chunk_result(b, id, &r, err);
-  if (e) return e;
+  const int e = pqgpu_batch_chunk_result(b, id, &r, err);
+  if (e && !r.num_slots) return e;  // nothing decoded (a failing chunk's prefix is copied)
   NEED_CTX(b, err);
   HIPCHECK(hipSetDevice(b->ctx->device), err);
   auto cp = [&](void *dst, const void *src, size_t n) -> hipError_t {
@@ -1949,6 +1958,18 @@ int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32
   HIPCHECK(cp(rep_levels, r.rep_levels, (size_t)r.num_slots), err);
   HIPCHECK(cp(validity, r.validity, (size_t)((r.num_slots + 31) / 32) * 4), err);
   HIPCHECK(cp(list_offsets, r.list_offsets, r.list_offsets ? (size_t)(r.num_records + 1) * 4 : 0), err);
+  return e;
+}
+
+int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_error *err) {
+  clear_err(err);
+  if (!ctx) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "no device context");
+    return PQ_ERR_ARG;
+  }
+  if (!bytes) return PQ_OK;
+  HIPCHECK(hipSetDevice(ctx->device), err);
+  HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDefault), err);
   return PQ_OK;
 }
 

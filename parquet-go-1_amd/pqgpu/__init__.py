@@ -77,9 +77,24 @@ class BatchStats(ctypes.Structure):
                 ("snappy_pages", ctypes.c_int64), ("snappy_kernel_bytes", ctypes.c_int64)]
 
 
+class PipelineOpts(ctypes.Structure):
+    _fields_ = [("depth", ctypes.c_int32), ("threads", ctypes.c_int32), ("validate_crc", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+class PipelineStats(ctypes.Structure):
+    _fields_ = [("row_groups", ctypes.c_int64), ("rows", ctypes.c_int64), ("chunks", ctypes.c_int64),
+                ("failed_chunks", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
+                ("wall_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
+                ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _LIB = None
 TIMER_SLOTS = 16  # PQGPU_TIMER_SLOTS
-ABI_VERSION = 3  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+ABI_VERSION = 4  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -88,6 +103,8 @@ _EXPORTS = [
     "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
     "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
+    "pqgpu_copy", "pqgpu_pipeline_create", "pqgpu_pipeline_next", "pqgpu_pipeline_release", "pqgpu_pipeline_stats_get",
+    "pqgpu_pipeline_destroy",
 ]
 
 
@@ -136,6 +153,13 @@ def lib():
         "pqgpu_batch_chunk_pages": ([P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), P, P, P, P, ctypes.c_int32, E],
                                     ctypes.c_int),
         "pqgpu_batch_kernel_bytes": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+        "pqgpu_copy": ([P, P, P, ctypes.c_size_t, E], ctypes.c_int),
+        "pqgpu_pipeline_create": ([P, P, P, ctypes.c_int32, P, ctypes.c_int32, ctypes.POINTER(PipelineOpts),
+                                   ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_pipeline_next": ([P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
+        "pqgpu_pipeline_release": ([P, P], ctypes.c_int),
+        "pqgpu_pipeline_stats_get": ([P, ctypes.POINTER(PipelineStats)], ctypes.c_int),
+        "pqgpu_pipeline_destroy": ([P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -381,13 +405,26 @@ class Batch:
         _check(lib().pqgpu_batch_chunk_pages(self._h, cid, ctypes.byref(n), *ptr, n.value, ctypes.byref(err)), err)
         return out.T.copy()
 
-    def result(self, cid, copy=True):
-        """ColumnData for chunk `cid` (raises DecodeError if that chunk failed)."""
+    def result(self, cid, copy=True, partial=False):
+        """ColumnData for chunk `cid` (raises DecodeError if that chunk failed). partial=True returns
+        (ColumnData of the pages decoded before a failing page, or None; DecodeError or None): the
+        rows the reference's lazy page reader returns before the page that fails
+        (data_store.go:236-260)."""
         err = Error()
         r = ChunkResult()
-        _check(lib().pqgpu_batch_chunk_result(self._h, cid, ctypes.byref(r), ctypes.byref(err)), err)
+        rc = lib().pqgpu_batch_chunk_result(self._h, cid, ctypes.byref(r), ctypes.byref(err))
+        if partial:
+            e = DecodeError(err) if rc else None
+            if rc and not r.num_slots:
+                return None, e
+            data = self._copy(cid, r, err) if copy else r
+            return data, e
+        _check(rc, err)
         if not copy:
             return r
+        return self._copy(cid, r, err)
+
+    def _copy(self, cid, r, err):
         info = self._infos[cid]
         ns, nv = r.num_slots, r.num_values
         t = r.physical_type
@@ -412,10 +449,86 @@ class Batch:
         def ptr(a):
             return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
-        _check(lib().pqgpu_batch_copy_chunk(self._h, cid, ptr(vals), ptr(offs), ptr(pay), ptr(dl), ptr(rl),
-                                            ptr(valid), ptr(lists), ctypes.byref(err)), err)
+        rc = lib().pqgpu_batch_copy_chunk(self._h, cid, ptr(vals), ptr(offs), ptr(pay), ptr(dl), ptr(rl),
+                                          ptr(valid), ptr(lists), ctypes.byref(err))
+        if rc and not r.num_slots:
+            _check(rc, err)
         payload = pay[: r.payload_bytes].tobytes() if pay is not None else None
         return ColumnData(info, r, vals, offs, payload, dl, rl, valid, lists)
+
+
+class _PipelineBatch(Batch):
+    """A batch owned by a Pipeline (valid until the pipeline moves past it)."""
+
+    def __init__(self, handle, infos):
+        self.ctx = None
+        self._h = handle
+        self._files = []
+        self._infos = infos
+
+    def close(self):
+        self._h = ctypes.c_void_p()
+
+
+class Pipeline:
+    """pqgpu_pipeline: row groups of `f` streamed through `depth` batches (host planning and H2D
+    of later row groups overlap the decode of earlier ones). Iterating yields
+    (row_group, batch, error or None) in row-group order; a yielded batch is released when the
+    iteration moves on. Chunk ids in a batch follow `cols`."""
+
+    def __init__(self, ctx, f, row_groups=None, cols=None, depth=3, threads=0, validate_crc=False):
+        self.ctx, self.f = ctx, f
+        self.cols = list(range(f.num_columns)) if cols is None else list(cols)
+        self._infos = [f.column(c) for c in self.cols]
+        rgs = None if row_groups is None else (ctypes.c_int32 * len(row_groups))(*row_groups)
+        cs = (ctypes.c_int32 * len(self.cols))(*self.cols)
+        opts = PipelineOpts(depth, threads, int(validate_crc), 0)
+        self._h = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_pipeline_create(ctx._h, f._h, rgs, len(row_groups) if row_groups is not None else 0, cs,
+                                           len(self.cols), ctypes.byref(opts), ctypes.byref(self._h),
+                                           ctypes.byref(err)), err)
+        self._out = None
+
+    def __iter__(self):
+        while True:
+            self._release()
+            b, rg, err = ctypes.c_void_p(), ctypes.c_int32(), Error()
+            rc = lib().pqgpu_pipeline_next(self._h, ctypes.byref(b), ctypes.byref(rg), ctypes.byref(err))
+            if not b.value:
+                _check(rc, err)
+                return
+            self._out = _PipelineBatch(b, self._infos)
+            yield rg.value, self._out, (DecodeError(err) if rc else None)
+
+    def _release(self):
+        if self._out is not None:
+            lib().pqgpu_pipeline_release(self._h, self._out._h)
+            self._out.close()
+            self._out = None
+
+    def stats(self):
+        s = PipelineStats()
+        lib().pqgpu_pipeline_stats_get(self._h, ctypes.byref(s))
+        return s.as_dict()
+
+    def close(self):
+        if self._h:
+            self._release()
+            lib().pqgpu_pipeline_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def copy(ctx, dst, src, nbytes):
+    """pqgpu_copy: hipMemcpy(hipMemcpyDefault) on the library's HIP runtime (integer addresses)."""
+    err = Error()
+    _check(lib().pqgpu_copy(ctx._h, ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, ctypes.byref(err)), err)
 
 
 class FileReader:

@@ -53,26 +53,29 @@ def device_values(batch, chunk_ids, device):
     """This rank's decoded values of `chunk_ids` (fixed-width columns) concatenated into one
     torch tensor on `device`, copied device to device from the batch's output arena (no host
     round trip). The element type is the column's 8-byte lane (int64 view) or int32.
-    torch must initialise HIP before libpqgpu is loaded (bench.py does): torch ships its own
-    libamdhip64 (soname libamdhip64.so.7), which libpqgpu then binds to, so the process has one
-    HIP runtime and the two share device pointers."""
-    import ctypes
+    The copies go through pqgpu_copy, i.e. the HIP runtime libpqgpu itself is bound to. torch must
+    initialise HIP before libpqgpu is loaded (bench.py does): torch ships its own libamdhip64
+    (soname libamdhip64.so.7), which libpqgpu then binds to, so the process has one HIP runtime
+    and the two share device pointers."""
     import torch
+    from . import copy as pq_copy
     rs = [batch.result(c, copy=False) for c in chunk_ids]
     width = {r.value_width for r in rs}
     if len(width) != 1 or width.pop() not in (4, 8):
         raise ValueError("device_values: one fixed width of 4 or 8 bytes expected")
     dt = torch.int64 if rs[0].value_width == 8 else torch.int32
     out = torch.empty(sum(r.num_values for r in rs), dtype=dt, device=device)
-    hip = ctypes.CDLL("libamdhip64.so")
     torch.cuda.synchronize(device)
     at = 0
     for r in rs:
         nb = r.num_values * r.value_width
         if nb:
-            rc = hip.hipMemcpy(ctypes.c_void_p(out.data_ptr() + at), ctypes.c_void_p(r.values), ctypes.c_size_t(nb),
-                               ctypes.c_int(3))  # hipMemcpyDeviceToDevice
-            if rc != 0:
-                raise RuntimeError(f"hipMemcpy device to device failed ({rc})")
+            pq_copy(batch_ctx(batch), out.data_ptr() + at, r.values, nb)
         at += nb
     return out
+
+
+def batch_ctx(batch):
+    if batch.ctx is None:
+        raise ValueError("device_values needs a batch with a device context")
+    return batch.ctx
