@@ -367,6 +367,59 @@ static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "(unused)", "(unused)", "(unused)"};
 
+// The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
+// with a device context lives in pinned host memory, so upload's H2D copy reads it directly
+// (no bounce copy). Capacity is kept across reset(): a reused batch (the pipeline's) plans
+// into memory that is already pinned and touched.
+struct StageBuf {
+  uint8_t *p = nullptr;
+  size_t n = 0, cap = 0;
+  bool pinned = false;
+  StageBuf() = default;
+  StageBuf(const StageBuf &) = delete;
+  StageBuf &operator=(const StageBuf &) = delete;
+  ~StageBuf() { release(); }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else free(p);
+    }
+    p = nullptr;
+    n = cap = 0;
+  }
+  bool reserve(size_t want) {
+    if (want <= cap) return true;
+    size_t c = std::max<size_t>(want, cap ? cap * 2 : (size_t)1 << 20);
+    uint8_t *q = nullptr;
+    if (pinned) {
+      if (hipHostMalloc((void **)&q, c, hipHostMallocDefault) != hipSuccess) q = nullptr;
+    } else {
+      q = (uint8_t *)malloc(c);
+    }
+    if (!q) return false;
+    if (n) memcpy(q, p, n);
+    uint8_t *old = p;
+    const bool was = pinned;
+    p = q;
+    cap = c;
+    if (old) {
+      if (was) (void)hipHostFree(old);
+      else free(old);
+    }
+    return true;
+  }
+  // new bytes are uninitialised unless `fill` >= 0
+  void resize(size_t m, int fill = -1) {
+    if (m > cap && !reserve(m)) throw std::bad_alloc();
+    if (fill >= 0 && m > n) memset(p + n, fill, m - n);
+    n = m;
+  }
+  size_t size() const { return n; }
+  uint8_t *data() { return p; }
+  const uint8_t *data() const { return p; }
+  void clear() { n = 0; }
+};
+
 struct pqgpu_batch {
   pqgpu_ctx *ctx = nullptr;
   std::vector<HostChunk> chunks;
@@ -374,7 +427,8 @@ struct pqgpu_batch {
   std::vector<BaDelta> ba_delta;          // DELTA_LENGTH / DELTA_BYTE_ARRAY pages (PageDesc::ba_delta)
   std::vector<uint64_t> ba_delta_scratch; // arena offset of each entry's scratch
   uint64_t o_ba_delta = 0;
-  std::vector<uint8_t> stage;
+  StageBuf stage;
+  hipStream_t last_stream = nullptr;  // the stream of the last upload (its H2D reads `stage`)
   // SNAPPY data pages decompressed on the device by k_snappy (default; PQ_HOST_SNAPPY=1
   // decompresses them on the host like GZIP). Pages carry PF_DEV_SNAPPY and `data` = job index
   // until upload, which places their output in a region after the stage.
@@ -420,8 +474,6 @@ struct pqgpu_batch {
   // device
   uint8_t *d_stage = nullptr;
   size_t d_stage_cap = 0;
-  uint8_t *h_pinned = nullptr;
-  size_t h_pinned_cap = 0;
   uint8_t *d_arena = nullptr;
   size_t d_arena_cap = 0;
   uint64_t arena_size = 0;
@@ -474,8 +526,10 @@ static int chunk_fail(pqgpu_batch *b, HostChunk &hc, int32_t id, int code, int p
 }
 
 static uint64_t stage_append(pqgpu_batch *b, const uint8_t *src, int64_t n) {
-  uint64_t off = align_up(b->stage.size(), 16);
+  const size_t end = b->stage.size();
+  uint64_t off = align_up(end, 16);
   b->stage.resize(off + (size_t)n);
+  if (off > end) memset(b->stage.data() + end, 0, off - end);  // alignment gap: zero, as before
   if (n) memcpy(b->stage.data() + off, src, (size_t)n);
   return off;
 }
@@ -1179,16 +1233,15 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMalloc(&b->d_stage, dsz), err);
     b->d_stage_cap = dsz;
   }
-  if (ssz > b->h_pinned_cap) {
-    if (b->h_pinned) (void)hipHostFree(b->h_pinned);
-    b->h_pinned = nullptr;
-    b->h_pinned_cap = 0;
-    HIPCHECK(hipHostMalloc((void **)&b->h_pinned, ssz, hipHostMallocDefault), err);
-    b->h_pinned_cap = ssz;
+  {
+    // the stage is pinned host memory: the H2D copy reads it directly (64 zero bytes after it)
+    const size_t used = b->stage.size();
+    b->stage.resize(ssz, 0);
+    memset(b->stage.data() + used, 0, ssz - used);
+    b->stage.resize(used);
+    HIPCHECK(hipMemcpyAsync(b->d_stage, b->stage.data(), ssz, hipMemcpyHostToDevice, s), err);
+    b->last_stream = s;
   }
-  memcpy(b->h_pinned, b->stage.data(), b->stage.size());
-  memset(b->h_pinned + b->stage.size(), 0, ssz - b->stage.size());
-  HIPCHECK(hipMemcpyAsync(b->d_stage, b->h_pinned, ssz, hipMemcpyHostToDevice, s), err);
 
   uint8_t *A = b->d_arena;
   auto dp = [&](uint64_t o) { return (uint64_t)(A + o); };
@@ -1762,6 +1815,7 @@ int pqgpu_batch_create(pqgpu_ctx *ctx, pqgpu_batch **out, pqgpu_error *err) {
   // validated (add_chunk) but upload/decode report PQ_ERR_HIP.
   pqgpu_batch *b = new pqgpu_batch();
   b->ctx = ctx;
+  b->stage.pinned = ctx != nullptr;  // plan-only batches stage in pageable memory
   *out = b;
   return PQ_OK;
 }
@@ -1787,7 +1841,6 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);
-  if (b->h_pinned) (void)hipHostFree(b->h_pinned);
   b->timer.destroy();
   delete b;
 }
@@ -1795,6 +1848,7 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
 int pqgpu_batch_reset(pqgpu_batch *b) {
   if (b->ctx) {
     (void)hipStreamSynchronize(b->ctx->stream);
+    if (b->last_stream) (void)hipStreamSynchronize(b->last_stream);  // an H2D copy may still read the stage
     free_payloads(b);
   }
   b->chunks.clear();
@@ -1837,6 +1891,8 @@ int pqgpu_batch_add_file_chunk(pqgpu_batch *b, const pqgpu_file *f, int rg, int 
     if (err) { err->chunk = id; hc.err = *err; }
     return e;
   }
+  // the chunk's staged bytes are about its compressed size (SNAPPY data pages stay compressed)
+  b->stage.reserve(b->stage.size() + (size_t)std::max<int64_t>(cm.total_compressed_size, 0) + 4096);
   return add_chunk_impl(b, f->buf, f->len, &ci, &cm, validate_crc, chunk_id, err);
 }
 

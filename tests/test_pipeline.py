@@ -162,3 +162,22 @@ def test_gpu_pipeline_release_protocol(gpu_ctx):
     assert L.pqgpu_pipeline_next(h, ctypes.byref(b2), ctypes.byref(rg), ctypes.byref(err)) in (0, 5, 1, 2, 3)
     assert b2.value and rg.value == 1
     L.pqgpu_pipeline_destroy(h)
+
+
+@pytest.mark.gpu
+def test_gpu_pipeline_cfg5_replica(gpu_ctx):
+    """cfg5's generator: pyarrow row-group templates replicated behind a rewritten footer
+    (SNAPPY V1, 64 columns) — every chunk through the pipeline equals the oracle."""
+    import workloads as W
+    data, _ = W.gen_cfg5(rows=3 * 20000, rg_rows=20000)
+    orc = {(rg, col): r for rg, col, r in pqtest.oracle_decode(data)}
+    f = pqgpu.File(data)
+    p = pqgpu.Pipeline(gpu_ctx, f, depth=2, threads=2)
+    n = 0
+    for rg, b, err in p:
+        assert err is None
+        for col in range(f.num_columns):
+            pqtest.assert_chunk_equal(b.result(col), orc[(rg, col)], f"cfg5 rg{rg} col{col}")
+        n += 1
+    assert n == 3
+    p.close()

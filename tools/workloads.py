@@ -10,6 +10,9 @@ from numpy buffers so that the largest (cfg4, 16 Mi records) takes seconds, not 
   cfg3  BYTE_ARRAY REQUIRED, 65,536-entry dictionary (lengths 4-28), 16-bit indices, V1,
         33,554,432 rows, 8 row groups of 4,194,304 (one dictionary per row group)
   cfg4  LIST<INT32> + MAP<BYTE_ARRAY, INT64>, 16,777,216 records, V1, 4 row groups
+  cfg5  64 REQUIRED columns (16 each: INT32 dictionary bw 8, INT64 DELTA, DOUBLE PLAIN, INT64
+        PLAIN), SNAPPY, V1, row groups of 3,906,250 rows: a few row-group templates written by
+        pyarrow, their bytes replicated behind a rewritten footer
 """
 import io
 
@@ -132,3 +135,103 @@ def gen_cfg4(records=16_777_216, rg_rows=RG_ROWS, page_rows=65_536, seed=5, firs
 
 
 GENERATORS = {"cfg1": gen_cfg1, "cfg2": gen_cfg2, "cfg3": gen_cfg3, "cfg4": gen_cfg4}
+
+
+CFG5_RG_ROWS = 3_906_250
+
+
+def cfg5_template(rows=CFG5_RG_ROWS, seed=6, page_rows=65_536):
+    """One cfg5 row group as a pyarrow file: 16 x INT32 RLE_DICTIONARY (256 distinct int32s,
+    8-bit indices), 16 x INT64 DELTA_BINARY_PACKED (running sums of uniform [0, 2^16) steps),
+    16 x DOUBLE PLAIN (uniform [0, 1)), 16 x INT64 PLAIN (uniform), REQUIRED, SNAPPY, V1, pages
+    of 65,536 rows (DELTA page non-null counts then avoid 1 mod 256, App. A Q1)."""
+    import pyarrow as pa
+    rng = np.random.default_rng(seed)
+    arrays, fields = [], []
+    for j in range(16):
+        d = rng.integers(-2**31, 2**31, 256, dtype=np.int64).astype(np.int32)
+        arrays.append(pa.array(d[rng.integers(0, 256, rows)]))
+        fields.append(pa.field(f"i32dict_{j}", pa.int32(), nullable=False))
+    for j in range(16):
+        arrays.append(pa.array(np.cumsum(rng.integers(0, 2**16, rows)).astype(np.int64)))
+        fields.append(pa.field(f"i64delta_{j}", pa.int64(), nullable=False))
+    for j in range(16):
+        arrays.append(pa.array(rng.random(rows)))
+        fields.append(pa.field(f"f64_{j}", pa.float64(), nullable=False))
+    for j in range(16):
+        arrays.append(pa.array(rng.integers(-2**62, 2**62, rows, dtype=np.int64)))
+        fields.append(pa.field(f"i64_{j}", pa.int64(), nullable=False))
+    t = pa.Table.from_arrays(arrays, schema=pa.schema(fields))
+    enc = {f"i64delta_{j}": "DELTA_BINARY_PACKED" for j in range(16)}
+    enc.update({f"f64_{j}": "PLAIN" for j in range(16)})
+    enc.update({f"i64_{j}": "PLAIN" for j in range(16)})
+    return _write(t, use_dictionary=[f"i32dict_{j}" for j in range(16)], column_encoding=enc, compression="snappy",
+                  data_page_version="1.0", row_group_size=rows, max_rows_per_page=page_rows,
+                  dictionary_pagesize_limit=1 << 20)
+
+
+def replicate_row_groups(templates, n):
+    """A file of `n` row groups whose row group g is the (only) row group of templates[g mod T],
+    byte for byte, behind a footer written here (rawpq's Thrift writer) with every column chunk's
+    offsets moved to its copy. Decoding needs nothing else of the template footers."""
+    import pyarrow.parquet as pq
+    import rawpq as R
+    metas = [pq.ParquetFile(io.BytesIO(t)).metadata for t in templates]
+    m0 = metas[0]
+    sch = m0.schema
+    schema = [[(4, R.BIN, "schema"), (5, R.I32, len(sch))]]
+    for c in range(len(sch)):
+        col = sch.column(c)
+        schema.append(R.schema_leaf(col.name, col.physical_type, "REQUIRED"))
+    codec = {"UNCOMPRESSED": 0, "SNAPPY": 1, "GZIP": 2}
+    out = bytearray(b"PAR1")
+    rgs, total_rows = [], 0
+    for g in range(n):
+        t, md = templates[g % len(templates)], metas[g % len(templates)].row_group(0)
+        cols = [md.column(c) for c in range(md.num_columns)]
+        start = [c.dictionary_page_offset if c.has_dictionary_page else c.data_page_offset for c in cols]
+        lo = min(start)
+        hi = max(s + c.total_compressed_size for s, c in zip(start, cols))
+        shift = len(out) - lo
+        out += t[lo:hi]
+        ccs = []
+        for s0, c in zip(start, cols):
+            md_f = [(1, R.I32, R.TYPES[c.physical_type]), (2, R.LIST, (R.I32, [R.ENC[e] for e in c.encodings])),
+                    (3, R.LIST, (R.BIN, c.path_in_schema.split("."))), (4, R.I32, codec[c.compression]),
+                    (5, R.I64, c.num_values), (6, R.I64, c.total_uncompressed_size),
+                    (7, R.I64, c.total_compressed_size), (9, R.I64, c.data_page_offset + shift)]
+            if c.has_dictionary_page:
+                md_f.append((11, R.I64, c.dictionary_page_offset + shift))
+            ccs.append([(2, R.I64, s0 + shift), (3, R.STRUCT, md_f)])
+        rgs.append([(1, R.LIST, (R.STRUCT, ccs)), (2, R.I64, md.total_byte_size), (3, R.I64, md.num_rows)])
+        total_rows += md.num_rows
+    fmd = R.tstruct([(1, R.I32, 1), (2, R.LIST, (R.STRUCT, schema)), (3, R.I64, total_rows),
+                     (4, R.LIST, (R.STRUCT, rgs)), (6, R.BIN, "cfg5 row-group templates replicated")])
+    out += fmd + len(fmd).to_bytes(4, "little") + b"PAR1"
+    return bytes(out)
+
+
+def gen_cfg5(rows=8 * CFG5_RG_ROWS, rg_rows=CFG5_RG_ROWS, seed=6, first_rg=0, templates=2):
+    """cfg5 (configs[4]) row groups [first_rg, first_rg + rows / rg_rows): row group g is template
+    (g mod templates), each template drawn from default_rng([seed, t])."""
+    nrg = max(1, -(-rows // rg_rows))
+    tpl = [cfg5_template(rg_rows, seed=[seed, (first_rg + k) % templates]) for k in range(min(templates, nrg))]
+    order = [tpl[(first_rg + g) % templates - first_rg % templates if len(tpl) == templates else g % len(tpl)]
+             for g in range(nrg)]
+    return replicate_rows(order), None
+
+
+def replicate_rows(templates_in_order):
+    """replicate_row_groups over an explicit per-row-group template list."""
+    uniq, idx = [], []
+    for t in templates_in_order:
+        for k, u in enumerate(uniq):
+            if u is t:
+                idx.append(k)
+                break
+        else:
+            uniq.append(t)
+            idx.append(len(uniq) - 1)
+    if idx == [k % len(uniq) for k in range(len(idx))]:
+        return replicate_row_groups(uniq, len(idx))
+    return replicate_row_groups(list(templates_in_order), len(idx))
