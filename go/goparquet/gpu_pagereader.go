@@ -5,11 +5,12 @@
 // hybrid_decoder.go:16-27), so only a file inside package goparquet can stand
 // behind them. Copy this file next to chunk_reader.go and apply the three-line
 // hook of INTEGRATION.md (a `gpu` field on FileReader / fileReaderOptions and a
-// call at the top of readChunk). With WithGPUDecoder(ctx) a FileReader decodes
-// each selected column chunk on the GPU in one batch (every page, levels and
-// values) and hands ColumnStore.readNextPage (data_store.go:236-260) one
-// gpuPageReader per data page, exactly the (values, dLevel, rLevel) triple the
-// CPU pageReaders return, including the error of the first failing page.
+// call at the top of readRowGroupData). With WithGPUDecoder(ctx) a FileReader
+// decodes each row group's selected column chunks on the GPU in one batch
+// (every page, levels and values) and hands ColumnStore.readNextPage
+// (data_store.go:236-260) one gpuPageReader per data page, exactly the
+// (values, dLevel, rLevel) triple the CPU pageReaders return: the pages before
+// a failing page decode normally and the failing page returns its error.
 package goparquet
 
 import (
@@ -60,8 +61,20 @@ func (p *gpuPageReader) readValues(size int) ([]interface{}, *packedArray, *pack
 	return p.values, p.dLevel, p.rLevel, nil
 }
 
-// readChunkGPU replaces readChunk + readPages (chunk_reader.go:182-362) for one chunk.
-func (f *FileReader) readChunkGPU(ctx context.Context, col *Column, chunk *parquet.ColumnChunk) ([]pageReader, bool, error) {
+// gpuChunkInput reads one column chunk's bytes and describes it for the decoder (the part of
+// readChunk, chunk_reader.go:299-362, before readPages).
+func (f *FileReader) gpuChunkInput(col *Column, chunk *parquet.ColumnChunk) ([]byte, gpudecode.ColumnInfo, gpudecode.ChunkMeta, error) {
+	var ci gpudecode.ColumnInfo
+	var cm gpudecode.ChunkMeta
+	if chunk.FilePath != nil {
+		return nil, ci, cm, fmt.Errorf("nyi: data is in another file: '%s'", *chunk.FilePath)
+	}
+	if chunk.MetaData == nil {
+		return nil, ci, cm, fmt.Errorf("missing meta data for Column %c", col.Index())
+	}
+	if typ := *col.Element().Type; chunk.MetaData.Type != typ {
+		return nil, ci, cm, fmt.Errorf("wrong type in Column chunk metadata, expected %s was %s", typ, chunk.MetaData.Type)
+	}
 	md := chunk.MetaData
 	start := md.DataPageOffset
 	if md.DictionaryPageOffset != nil {
@@ -69,59 +82,107 @@ func (f *FileReader) readChunkGPU(ctx context.Context, col *Column, chunk *parqu
 	}
 	buf := make([]byte, md.TotalCompressedSize)
 	if _, err := f.reader.Seek(start, io.SeekStart); err != nil {
-		return nil, false, err
+		return nil, ci, cm, err
 	}
 	n, err := io.ReadFull(f.reader, buf)
 	if err != nil && err != io.ErrUnexpectedEOF {
-		return nil, false, err
+		return nil, ci, cm, err
 	}
-	buf = buf[:n]
 	el := col.Element()
-	ci := gpudecode.ColumnInfo{
+	ci = gpudecode.ColumnInfo{
 		PhysicalType: int(*el.Type), MaxDef: int(col.MaxDefinitionLevel()), MaxRep: int(col.MaxRepetitionLevel()),
 	}
 	if el.TypeLength != nil {
 		ci.TypeLength = int(*el.TypeLength)
 	}
-	cm := gpudecode.ChunkMeta{
+	cm = gpudecode.ChunkMeta{
 		PhysicalType: int(md.Type), Codec: int(md.Codec), NumValues: md.NumValues,
 		TotalCompressedSize: md.TotalCompressedSize, DataPageOffset: md.DataPageOffset - start,
-		DictionaryPageOffset: -1, HasFilePath: chunk.FilePath != nil,
+		DictionaryPageOffset: -1, HasFilePath: false,
 	}
 	if md.DictionaryPageOffset != nil {
 		cm.DictionaryPageOffset = 0
 	}
+	return buf[:n], ci, cm, nil
+}
+
+// readRowGroupDataGPU replaces readRowGroupData (chunk_reader.go:375-404) when the reader has a
+// GPU: every selected column chunk of the row group goes into ONE batch (one set of kernel
+// launches for all its pages), decoded once; then the columns are handed their pages in column
+// order, returning the first error where the reference's loop would meet it: a readChunk /
+// readPages error (headers, CRC, decompression) for that column's turn; a readValues error only
+// from its page on (the pages before it read normally).
+func (f *FileReader) readRowGroupDataGPU(ctx context.Context) error {
+	rowGroup := f.meta.RowGroups[f.rowGroupPosition-1]
+	dataCols := f.schemaReader.Columns()
+
+	f.schemaReader.resetData()
+	f.schemaReader.setNumRecords(rowGroup.NumRows)
 	b, err := gpudecode.NewBatch(f.gpu)
 	if err != nil {
-		return nil, false, err
+		return err
 	}
 	defer b.Close()
-	id, err := b.AddChunk(buf, ci, cm, f.schemaReader.validateCRC)
-	if err != nil {
-		return nil, false, err // readChunk / readPages error (page headers, dictionary page)
+	type planned struct {
+		col *Column
+		id  int32
+		err error // readChunk error of this column (returned at its turn)
+	}
+	var cols []planned
+	for _, c := range dataCols {
+		idx := c.Index()
+		if len(rowGroup.Columns) <= idx {
+			cols = append(cols, planned{col: c, err: fmt.Errorf("column index %d is out of bounds", idx)})
+			break
+		}
+		chunk := rowGroup.Columns[idx]
+		if !f.schemaReader.isSelectedByPath(c.path) {
+			if err := f.skipChunk(c, chunk); err != nil {
+				cols = append(cols, planned{col: c, err: err})
+				break
+			}
+			c.data.skipped = true
+			continue
+		}
+		buf, ci, cm, err := f.gpuChunkInput(c, chunk)
+		if err != nil {
+			cols = append(cols, planned{col: c, err: err})
+			break
+		}
+		id, err := b.AddChunk(buf, ci, cm, f.schemaReader.validateCRC)
+		cols = append(cols, planned{col: c, id: id, err: err})
+		if err != nil {
+			break // readPages failed on the host: the reference returns before later columns
+		}
 	}
 	if err := b.Decode(); err != nil {
-		return nil, false, err
+		return err
 	}
 	_ = b.Sync()
-	failPage := -1
-	var failErr error
-	if err := b.Status(id); err != nil {
-		de, ok := err.(*gpudecode.DecodeError)
-		if !ok || de.Page < 0 {
-			return nil, false, err
+	for _, p := range cols {
+		if p.err != nil {
+			return p.err
 		}
-		failPage, failErr = de.Page, fmt.Errorf("read values from page failed: %w", err)
+		res, rerr := b.Result(p.id)
+		if rerr != nil && gpudecode.ReadPagesError(rerr) {
+			return rerr // decompression / CRC: readPages fails before any value is read
+		}
+		failPage := -1
+		var failErr error
+		if rerr != nil {
+			failPage, failErr = rerr.(*gpudecode.DecodeError).Page, fmt.Errorf("read values from page failed: %w", rerr)
+		}
+		useDict := res != nil && res.DictionaryPage
+		if err := readPageData(p.col, gpuPages(p.col, res, failPage, failErr), useDict); err != nil {
+			return err
+		}
 	}
-	res, rerr := b.Result(id)
-	if rerr != nil && failPage < 0 {
-		return nil, false, rerr
-	}
-	return gpuPages(col, res, failPage, failErr), md.DictionaryPageOffset != nil, nil
+	return nil
 }
 
 // gpuPages splits a decoded chunk into per-page readers; pages from the failing
-// one on return its error (the reference never reads past it).
+// one on return its error (the reference never reads past it). For a failing
+// chunk `res` holds the decoded pages before the failing page.
 func gpuPages(col *Column, res *gpudecode.Chunk, failPage int, failErr error) []pageReader {
 	if res == nil {
 		return []pageReader{&gpuPageReader{err: failErr, n: 1}}

@@ -46,8 +46,20 @@ var (
 // error readChunk/readPages return; otherwise the page whose readValues fails).
 type DecodeError struct {
 	Chunk, Page int
+	Code        int // enum pqgpu_status
 	Msg         string
 	err         error
+}
+
+// ReadPagesError reports whether err is one the reference raises while reading a chunk's pages
+// (readChunk / readPages: page headers, CRC, decompression, chunk_reader.go:161-263) rather than
+// from one page's readValues: no value of the chunk is returned for it.
+func ReadPagesError(err error) bool {
+	de, ok := err.(*DecodeError)
+	if !ok {
+		return true
+	}
+	return de.Page < 0 || de.Code == int(C.PQ_ERR_CRC) || de.Code == int(C.PQ_ERR_DECOMPRESS)
 }
 
 func (e *DecodeError) Error() string { return e.Msg }
@@ -81,7 +93,7 @@ func toErr(rc C.int, e *C.pqgpu_error) error {
 	if rc == C.PQ_OK {
 		return nil
 	}
-	return &DecodeError{Chunk: int(e.chunk), Page: int(e.page), Msg: C.GoString(&e.msg[0]), err: classErr(rc)}
+	return &DecodeError{Chunk: int(e.chunk), Page: int(e.page), Code: int(rc), Msg: C.GoString(&e.msg[0]), err: classErr(rc)}
 }
 
 // Context is one GPU (pqgpu_ctx). Not safe for concurrent use: one goroutine
@@ -240,19 +252,24 @@ type Chunk struct {
 	Validity                                 []uint32 // bit i = slot i is non-null; nil when MaxDef == 0
 	ListOffsets                              []int32  // MaxRep > 0: record starts, NumRecords+1 entries
 	Pages                                    []Page
+	DictionaryPage                           bool // a dictionary page was read (readChunk's useDict)
 }
 
-// Result copies chunk id's outputs to host memory.
+// Result copies chunk id's outputs to host memory. When a page's readValues failed, it returns
+// the pages before that page (the rows the reference's lazy page reader returns first,
+// data_store.go:236-260) together with the error; for any other error the chunk is nil.
 func (b *Batch) Result(id int32) (*Chunk, error) {
 	var e C.pqgpu_error
 	var r C.pqgpu_chunk_result
-	if err := toErr(C.pqgpu_batch_chunk_result(b.b, C.int32_t(id), &r, &e), &e); err != nil {
-		return nil, err
+	failed := toErr(C.pqgpu_batch_chunk_result(b.b, C.int32_t(id), &r, &e), &e)
+	if failed != nil && r.num_slots == 0 {
+		return nil, failed
 	}
 	ch := &Chunk{
 		PhysicalType: int(r.physical_type), ValueWidth: int(r.value_width),
 		MaxDef: int(r.max_def), MaxRep: int(r.max_rep),
 		NumSlots: int64(r.num_slots), NumValues: int64(r.num_values), NumRecords: int64(r.num_records),
+		DictionaryPage: r.dictionary_page != 0,
 	}
 	var vp, op, pp, dp, rp, valp, lp unsafe.Pointer
 	if r.values != nil {
@@ -282,7 +299,7 @@ func (b *Batch) Result(id int32) (*Chunk, error) {
 		lp = unsafe.Pointer(&ch.ListOffsets[0])
 	}
 	if err := toErr(C.pqgpu_batch_copy_chunk(b.b, C.int32_t(id), vp, (*C.int32_t)(op), (*C.uint8_t)(pp),
-		(*C.uint8_t)(dp), (*C.uint8_t)(rp), (*C.uint32_t)(valp), (*C.int32_t)(lp), &e), &e); err != nil {
+		(*C.uint8_t)(dp), (*C.uint8_t)(rp), (*C.uint32_t)(valp), (*C.int32_t)(lp), &e), &e); err != nil && failed == nil {
 		return nil, err
 	}
 	if ch.Values != nil {
@@ -302,7 +319,7 @@ func (b *Batch) Result(id int32) (*Chunk, error) {
 		return nil, err
 	}
 	ch.Pages = pages
-	return ch, nil
+	return ch, failed
 }
 
 func (b *Batch) pages(id int32) ([]Page, error) {

@@ -71,7 +71,14 @@ typedef struct {
   int32_t max_rep;         /* Column.MaxRepetitionLevel() */
   int32_t repetition;      /* leaf parquet.FieldRepetitionType */
   char path[236];          /* dotted ColumnPath */
+  /* Nested (Arrow-style) output, per REPEATED node on the path, outermost first
+   * (max_rep entries, at most PQGPU_MAX_NEST): the definition level before the
+   * node (the list is non-null from it) and at the node (the list has an
+   * element from it). Filled by pqgpu_file_column from the schema. */
+  int32_t list_null_def[8];
+  int32_t list_def[8];
 } pqgpu_column_info;
+#define PQGPU_MAX_NEST 8
 
 /* The subset of parquet.ColumnMetaData that readChunk consults
  * (chunk_reader.go:299-362). Offsets are absolute file offsets. */
@@ -119,6 +126,21 @@ typedef struct {
   uint8_t *rep_levels;
   uint32_t *validity;
   int32_t *list_offsets;
+  /* Nested (Arrow-style) arrays of a repeated leaf (nest_levels = max_rep when
+   * max_rep <= PQGPU_MAX_NEST, else 0). List level k (0 = outermost REPEATED
+   * node) has num_lists[k] lists; list j spans child entries
+   * [lvl_offsets[k][j], lvl_offsets[k][j+1]) — the lists of level k+1, or for
+   * the innermost level the leaf's element slots; bit j of lvl_validity[k] =
+   * list j is non-null (null and empty lists both have no children). The leaf
+   * has num_elements element slots; bit e of element_validity = element e is
+   * non-null, and `values` holds the non-null elements in order. */
+  int32_t nest_levels;
+  int32_t dictionary_page;  /* 1 when the chunk had a dictionary page (readChunk's useDict) */
+  int64_t num_lists[8];
+  int32_t *lvl_offsets[8];
+  uint32_t *lvl_validity[8];
+  int64_t num_elements;
+  uint32_t *element_validity;
 } pqgpu_chunk_result;
 
 /* Per-batch statistics, for the roofline accounting. */
@@ -221,6 +243,10 @@ int pqgpu_batch_chunk_pages(const pqgpu_batch *b, int32_t chunk_id, int32_t *num
 int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values, int32_t *offsets, uint8_t *payload,
                            uint8_t *def_levels, uint8_t *rep_levels, uint32_t *validity, int32_t *list_offsets,
                            pqgpu_error *err);
+/* Copy list level `level`'s offsets (num_lists + 1) and validity words, and
+ * the element validity words, of a nested chunk to host buffers (any may be NULL). */
+int pqgpu_batch_copy_nested(const pqgpu_batch *b, int32_t chunk_id, int32_t level, int32_t *offsets,
+                            uint32_t *validity, uint32_t *element_validity, pqgpu_error *err);
 int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out);
 /* Diagnostics: 64 device counters filled by in-kernel phase stamps when the
  * environment has PQ_DEBUG_STAMPS=1 at upload time. */

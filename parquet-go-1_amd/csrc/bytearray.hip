@@ -106,12 +106,6 @@ DEV void global_put(uint8_t *dst, const uint8_t *src, uint32_t len) {
   for (; k < len; k++) dst[k] = src[k];
 }
 
-DEV void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
-
 // ---------------------------------------------------------------------------
 // Dictionary slots: entry i at slots + (i << slot_shift) = [u32 length | bytes | zero pad].
 // One thread per entry; blockIdx.y = the chunk (list of chunks with a slot table).

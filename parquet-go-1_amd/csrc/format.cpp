@@ -252,14 +252,19 @@ static void read_row_group(ThriftReader &t, RowGroup *g, int64_t remaining) {
 }
 
 // schema.go:893-924 readColumnSchema
+// `lists`: (definition level before, at) of every REPEATED ancestor, outermost first
+using ListLevels = std::vector<std::pair<int32_t, int32_t>>;
 static Status read_column_schema(FileMeta *f, size_t base, int32_t idx, const std::string &path, int d, int r,
-                                 int32_t *next) {
+                                 int32_t *next, const ListLevels &lists) {
   const SchemaElement &s = f->schema[base + (size_t)idx];
   if (s.name.empty()) return Status::Err(PQ_ERR_INVALID, "name in schema is empty");
   if (!s.has_rep) return Status::Err(PQ_ERR_INVALID, "field RepetitionType is nil");
+  const int d0 = d;
   if (s.rep != 0) d++;
   if (s.rep == 2) r++;
   Leaf l;
+  for (const auto &x : lists) { l.list_null_def.push_back(x.first); l.list_def.push_back(x.second); }
+  if (s.rep == 2) { l.list_null_def.push_back(d0); l.list_def.push_back(d); }
   l.type = s.type;
   l.type_length = s.has_type_length ? s.type_length : 0;
   l.max_def = d;
@@ -275,7 +280,7 @@ static Status read_column_schema(FileMeta *f, size_t base, int32_t idx, const st
 
 // schema.go:926-990 readGroupSchema
 static Status read_group_schema(FileMeta *f, size_t base, int32_t n, int32_t idx, const std::string &path, int d,
-                                int r, int32_t *next, int depth) {
+                                int r, int32_t *next, int depth, const ListLevels &lists) {
   if (depth > 1000 || n <= idx) return Status::Err(PQ_ERR_INVALID, "schema index out of bound");
   const SchemaElement &s = f->schema[base + (size_t)idx];
   if (s.has_type) return Status::Err(PQ_ERR_INVALID, "field Type is not nil");
@@ -283,14 +288,17 @@ static Status read_group_schema(FileMeta *f, size_t base, int32_t n, int32_t idx
   if (s.num_children <= 0) return Status::Err(PQ_ERR_INVALID, "the field NumChildren is zero");
   int32_t l = s.num_children;
   if ((int64_t)n <= (int64_t)idx + l) return Status::Err(PQ_ERR_INVALID, "not enough element in the schema list");
+  const int d0 = d;
   if (s.has_rep && s.rep != 0) d++;
   if (s.has_rep && s.rep == 2) r++;
+  ListLevels sub = lists;
+  if (s.has_rep && s.rep == 2) sub.emplace_back(d0, d);
   std::string p = path.empty() ? s.name : path + "." + s.name;
   idx++;
   for (int32_t k = 0; k < l; k++) {
     if (n <= idx) return Status::Err(PQ_ERR_INVALID, "schema index is out of bounds");
-    Status st = !f->schema[base + (size_t)idx].has_type ? read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1)
-                                                        : read_column_schema(f, base, idx, p, d, r, &idx);
+    Status st = !f->schema[base + (size_t)idx].has_type ? read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1, sub)
+                                                        : read_column_schema(f, base, idx, p, d, r, &idx, sub);
     if (!st.ok()) return st;
   }
   *next = idx;
@@ -327,8 +335,8 @@ Status OpenFile(const uint8_t *buf, int64_t len, FileMeta *out) {
   if (out->schema.empty()) return Status::Err(PQ_ERR_INVALID, "no schema element found");
   int32_t n = (int32_t)out->schema.size() - 1;
   for (int32_t idx = 0; idx < n;) {
-    Status st = !out->schema[1 + (size_t)idx].has_type ? read_group_schema(out, 1, n, idx, "", 0, 0, &idx, 0)
-                                                      : read_column_schema(out, 1, idx, "", 0, 0, &idx);
+    Status st = !out->schema[1 + (size_t)idx].has_type ? read_group_schema(out, 1, n, idx, "", 0, 0, &idx, 0, {})
+                                                      : read_column_schema(out, 1, idx, "", 0, 0, &idx, {});
     if (!st.ok()) return Status::Err(st.code, "creating schema failed: " + st.msg);
   }
   return Status::Ok();

@@ -80,6 +80,10 @@ struct RowGroup {
 struct Leaf {
   int32_t type = 0, type_length = 0, max_def = 0, max_rep = 0, rep = 0;
   std::string path;
+  // per REPEATED node on the path, outermost first (max_rep entries): the definition level
+  // before the node (a list at that level is non-null from here) and at the node (it has
+  // an element from here)
+  std::vector<int32_t> list_null_def, list_def;
 };
 struct FileMeta {
   std::vector<SchemaElement> schema;

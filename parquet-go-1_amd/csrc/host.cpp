@@ -233,6 +233,10 @@ struct HostChunk {
   uint32_t dict_len = 0, dict_count = 0;
   // device outputs (offsets into the arena)
   uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0;
+  // nested (Arrow-style) output: list levels (0: none), per level offsets / validity, elements
+  uint32_t nest = 0, nest_tile0 = 0;
+  uint64_t o_lvl_off[PQGPU_MAX_NEST] = {}, o_lvl_valid[PQGPU_MAX_NEST] = {}, o_elem_valid = 0;
+  int64_t num_lists[PQGPU_MAX_NEST] = {}, num_elems = 0;
   // byte-array dictionaries: (position, length) of every entry, from the host's walk of the
   // dictionary page (page_dict.go:35-72 + byteArrayPlainDecoder type_bytearray.go:24-55)
   std::vector<uint32_t> dict_ent;
@@ -365,7 +369,7 @@ struct KernelTimer {
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
-    "(unused)", "(unused)", "(unused)"};
+    "k_nest_count", "k_nest_emit", "(unused)"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -448,7 +452,9 @@ struct pqgpu_batch {
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
   uint32_t n_delta_tiles = 0;
-  std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages;
+  std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_tiles, nest_chunks;
+  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0;
+  uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
   std::vector<uint32_t> page_nn_init;
@@ -967,6 +973,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->base_chunks.clear();
   b->ba_chunks.clear();
   b->rec_pages.clear();
+  b->nest_tiles.clear();
+  b->nest_chunks.clear();
   b->run_base.assign(np, 0);
   b->tile_base.assign(np, 0);
   b->page_nn_init.assign(np, 0);
@@ -989,6 +997,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
     hc.o_valid = (!hc.err.code && hc.col.max_def > 0) ? take(((hc.num_slots + 31) / 32 + 2) * 4) : 0;
+    // nested output: list validity bitmaps and element validity (OR-ed by k_nest_emit)
+    hc.nest = 0;
+    if (!hc.err.code && hc.col.max_rep > 0 && hc.col.max_rep <= PQGPU_MAX_NEST) {
+      bool ok = true;
+      for (int k = 0; k < hc.col.max_rep; k++)
+        ok &= hc.col.list_def[k] > 0 && hc.col.list_def[k] <= hc.col.max_def && hc.col.list_null_def[k] < hc.col.list_def[k];
+      if (ok) hc.nest = (uint32_t)hc.col.max_rep;
+    }
+    const uint64_t words = ((hc.num_slots + 31) / 32 + 2) * 4;
+    for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) hc.o_lvl_valid[k] = k < hc.nest ? take(words) : 0;
+    hc.o_elem_valid = hc.nest ? take(words) : 0;
   }
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
@@ -1012,6 +1031,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     hc.o_def = hc.col.max_def > 1 ? take(ns) : 0;
     hc.o_rep = hc.col.max_rep > 0 ? take(ns) : 0;
     hc.o_lists = hc.col.max_rep > 0 ? take((ns + 1) * 4) : 0;
+    for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) hc.o_lvl_off[k] = k < hc.nest ? take((ns + 1) * 4) : 0;
+    if (hc.nest) b->nest_chunks.push_back(c);
     hc.o_offsets = is_ba ? take((ns + 1) * 4) : 0;
     hc.o_ba_index = 0;
     b->base_chunks.push_back(c);
@@ -1055,7 +1076,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.col.max_def == 1 && hc.col.max_rep == 0) b->level_pages_bw1.push_back(p);
       else if (hc.col.max_def > 0 || hc.col.max_rep > 0) b->level_pages.push_back(p);
       else b->page_nn_init[p] = pd.num_slots;
-      if (hc.col.max_rep > 0) b->rec_pages.push_back(p);
+      if (hc.col.max_rep > 0 && !hc.nest) b->rec_pages.push_back(p);  // nested chunks: k_nest_emit
       const uint32_t ns_p = pd.num_slots;
       auto tiles = [&](uint8_t kind, uint32_t tile) {
         for (uint32_t v0 = 0; v0 < ns_p; v0 += tile) b->items.push_back(WorkItem{p, v0, std::min(v0 + tile, ns_p), kind, {0, 0, 0}});
@@ -1105,6 +1126,19 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
     }
   }
+  // nested tiles (nested.hip kNestTile = 4,096 slots), grouped by the chunks' list levels so that
+  // each k_nest_emit<R> launch covers one group; a chunk's tiles are contiguous
+  for (uint32_t r = 0; r <= PQGPU_MAX_NEST + 1; r++) b->nest_first[r] = 0;
+  for (uint32_t r = 1; r <= PQGPU_MAX_NEST; r++) {
+    b->nest_first[r] = (uint32_t)b->nest_tiles.size();
+    for (uint32_t c : b->nest_chunks) {
+      HostChunk &hc = b->chunks[c];
+      if (hc.nest != r) continue;
+      hc.nest_tile0 = (uint32_t)b->nest_tiles.size();
+      for (uint64_t k = 0; k < (hc.num_slots + 4095) / 4096; k++) b->nest_tiles.push_back(c);
+    }
+  }
+  b->nest_first[PQGPU_MAX_NEST + 1] = (uint32_t)b->nest_tiles.size();
   // k_ba_emit block order: class 0 / 1 = chunks whose pages are all dictionary pages with a
   // slot table of 16/32-byte / 64-byte slots, class 2 = the rest. Within a class, chunk c's
   // tiles (in order) go to queue c mod 8 and block b takes tile b / 8 of queue b mod 8: blocks
@@ -1200,6 +1234,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_base = take(b->base_chunks.size() * 4);
   b->l_ba = take(b->ba_chunks.size() * 4);
   b->l_rec = take(b->rec_pages.size() * 4);
+  b->l_nest_tiles = take(b->nest_tiles.size() * 4);
+  b->l_nest_chunks = take(b->nest_chunks.size() * 4);
+  b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * kNestCnt * 4);
+  b->o_nest_base = take((uint64_t)b->nest_tiles.size() * kNestCnt * 8);
+  b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
   b->arena_size = a;
   if (a > b->d_arena_cap) {
     if (b->d_arena) (void)hipFree(b->d_arena);
@@ -1296,6 +1335,15 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.rep_levels = hc.o_rep ? dp(hc.o_rep) : 0;
     cd.validity = hc.o_valid ? dp(hc.o_valid) : 0;
     cd.list_offsets = hc.o_lists ? dp(hc.o_lists) : 0;
+    cd.nest = hc.nest;
+    cd.nest_tile0 = hc.nest_tile0;
+    for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) {
+      cd.list_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_def[k] : 0);
+      cd.list_null_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_null_def[k] : 0);
+      cd.lvl_offsets[k] = hc.o_lvl_off[k] ? dp(hc.o_lvl_off[k]) : 0;
+      cd.lvl_validity[k] = hc.o_lvl_valid[k] ? dp(hc.o_lvl_valid[k]) : 0;
+    }
+    cd.elem_validity = hc.o_elem_valid ? dp(hc.o_elem_valid) : 0;
     cd.offsets = hc.o_offsets ? dp(hc.o_offsets) : 0;
     cd.ba_index = hc.o_ba_index ? dp(hc.o_ba_index) : 0;
   }
@@ -1337,6 +1385,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
+  HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 4), err);
+  HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
   HIPCHECK(up(b->l_delta, b->delta_pages.data(), b->delta_pages.size() * 4), err);
   // the host copies above read from std::vector memory: wait before those vectors change
@@ -1371,6 +1421,9 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.ba_delta = (const BaDelta *)(A + b->o_ba_delta);
   d.page_vbase = (uint64_t *)(A + b->o_vbase);
   d.page_rbase = (uint64_t *)(A + b->o_rbase);
+  d.nest_cnt = (uint32_t *)(A + b->o_nest_cnt);
+  d.nest_base = (uint64_t *)(A + b->o_nest_base);
+  d.nest_tot = (uint64_t *)(A + b->o_nest_tot);
   d.runs = (HybRun *)(A + b->o_runs);
   d.run_base = (const uint64_t *)(A + b->o_run_base);
   d.run_count = (uint32_t *)(A + b->o_run_count);
@@ -1411,6 +1464,11 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.slot_grid_x = b->slot_grid_x;
   l.rec_pages = (const uint32_t *)(A + b->l_rec);
   l.n_rec_pages = (uint32_t)b->rec_pages.size();
+  l.nest_tiles = (const uint32_t *)(A + b->l_nest_tiles);
+  l.n_nest_tiles = (uint32_t)b->nest_tiles.size();
+  for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
+  l.nest_chunks = (const uint32_t *)(A + b->l_nest_chunks);
+  l.n_nest_chunks = (uint32_t)b->nest_chunks.size();
   l.delta_pages = (const uint32_t *)(A + b->l_delta);
   l.n_delta_pages = (uint32_t)b->delta_pages.size();
   l.n_delta_tiles = b->n_delta_tiles;
@@ -1531,6 +1589,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->any_ba_sync) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc copies above read host memory
   }
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
+  // nested (Arrow-style) arrays of repeated leaves (nested.hip)
+  HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
+  HIPCHECK(launch_nest_scan(d, l, s), err);
+  HIPCHECK(timed(b, 14, s, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, s); }), err);
   b->decoded = true;
   return PQ_OK;
 }
@@ -1582,6 +1644,11 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipMemcpy(rbase.data(), A + b->o_rbase, np * 8, hipMemcpyDeviceToHost), err);
     HIPCHECK(hipMemcpy(rec.data(), A + b->o_rec, np * 4, hipMemcpyDeviceToHost), err);
   }
+  std::vector<uint64_t> nest_tot;
+  if (!b->nest_chunks.empty()) {
+    nest_tot.resize((size_t)nc * kNestCnt);
+    HIPCHECK(hipMemcpy(nest_tot.data(), A + b->o_nest_tot, (size_t)nc * kNestCnt * 8, hipMemcpyDeviceToHost), err);
+  }
   std::vector<uint64_t> ba_tot;
   if (!b->ba_chunks.empty()) {
     ba_tot.resize(nc);
@@ -1617,6 +1684,9 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!hc.err.code && hc.sync_err && !hc.dev_err.code)
       set_err(&hc.dev_err, PQ_ERR_UNSUPPORTED, (int)c, -1, "BYTE_ARRAY chunk payload exceeds 2 GiB");
     if (!ba_tot.empty() && hc.value_width == 0) hc.payload_bytes = (int64_t)ba_tot[c];
+    for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++)
+      hc.num_lists[k] = k < hc.nest ? (int64_t)nest_tot[(size_t)c * kNestCnt + k] : 0;
+    hc.num_elems = hc.nest ? (int64_t)nest_tot[(size_t)c * kNestCnt + hc.nest] : 0;
     if (hc.num_pages) {
       uint32_t lp = hc.first_page + hc.num_pages - 1;
       hc.nn = (int64_t)(vbase[lp] + nn[lp]);
@@ -1668,7 +1738,15 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         if (hc.slot_shift) kb[12] += (int64_t)hc.dict_len + 8 * (int64_t)hc.dict_count + ((int64_t)hc.dict_count << hc.slot_shift);
         (void)ba_dict_nn;
       }
-      if (hc.o_lists) kb[7] += (int64_t)hc.num_slots + 4 * (hc.records + 1);
+      if (hc.o_lists && !hc.nest) kb[7] += (int64_t)hc.num_slots + 4 * (hc.records + 1);
+      if (hc.nest) {  // levels read by both nested kernels; offsets and bitmaps written by k_nest_emit
+        const int64_t lv = (int64_t)hc.num_slots * (hc.o_def ? 2 : 1) + (hc.o_def ? 0 : (int64_t)hc.num_slots / 8);
+        kb[13] += lv;
+        kb[14] += lv + (hc.num_elems + 7) / 8 + 4 * (hc.records + 1);  // + record offsets
+        for (uint32_t k = 0; k < hc.nest; k++) kb[14] += 4 * (hc.num_lists[k] + 1) + (hc.num_lists[k] + 7) / 8;
+        out_bytes += (hc.num_elems + 7) / 8;
+        for (uint32_t k = 0; k < hc.nest; k++) out_bytes += 4 * (hc.num_lists[k] + 1) + (hc.num_lists[k] + 7) / 8;
+      }
     }
   }
   kb[0] = lvl_bytes;
@@ -1779,6 +1857,10 @@ int pqgpu_file_column(const pqgpu_file *f, int col, pqgpu_column_info *out) {
   out->max_rep = l.max_rep;
   out->repetition = l.rep;
   snprintf(out->path, sizeof(out->path), "%s", l.path.c_str());
+  for (size_t k = 0; k < l.list_def.size() && k < PQGPU_MAX_NEST; k++) {
+    out->list_def[k] = l.list_def[k];
+    out->list_null_def[k] = l.list_null_def[k];
+  }
   return PQ_OK;
 }
 
@@ -1992,7 +2074,37 @@ int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_resul
   out->rep_levels = hc.o_rep ? A + hc.o_rep : nullptr;
   out->validity = hc.o_valid ? (uint32_t *)(A + hc.o_valid) : nullptr;
   out->list_offsets = hc.o_lists ? (int32_t *)(A + hc.o_lists) : nullptr;
+  out->dictionary_page = hc.has_dict ? 1 : 0;
+  out->nest_levels = e ? 0 : (int32_t)hc.nest;  // a failing chunk's prefix carries no nested arrays
+  for (uint32_t k = 0; k < PQGPU_MAX_NEST && !e; k++) {
+    out->num_lists[k] = hc.num_lists[k];
+    out->lvl_offsets[k] = hc.o_lvl_off[k] ? (int32_t *)(A + hc.o_lvl_off[k]) : nullptr;
+    out->lvl_validity[k] = hc.o_lvl_valid[k] ? (uint32_t *)(A + hc.o_lvl_valid[k]) : nullptr;
+  }
+  out->num_elements = e ? 0 : hc.num_elems;
+  out->element_validity = (!e && hc.o_elem_valid) ? (uint32_t *)(A + hc.o_elem_valid) : nullptr;
   return e;
+}
+
+int pqgpu_batch_copy_nested(const pqgpu_batch *b, int32_t id, int32_t level, int32_t *offsets, uint32_t *validity,
+                            uint32_t *element_validity, pqgpu_error *err) {
+  pqgpu_chunk_result r;
+  const int e = pqgpu_batch_chunk_result(b, id, &r, err);
+  if (e) return e;
+  NEED_CTX(b, err);
+  if (level < 0 || level >= r.nest_levels) {
+    set_err(err, PQ_ERR_ARG, id, -1, "no such list level");
+    return PQ_ERR_ARG;
+  }
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  const int64_t n = r.num_lists[level];
+  if (offsets) HIPCHECK(hipMemcpy(offsets, r.lvl_offsets[level], (size_t)(n + 1) * 4, hipMemcpyDeviceToHost), err);
+  if (validity) HIPCHECK(hipMemcpy(validity, r.lvl_validity[level], (size_t)((n + 31) / 32) * 4, hipMemcpyDeviceToHost), err);
+  if (element_validity)
+    HIPCHECK(hipMemcpy(element_validity, r.element_validity, (size_t)((r.num_elements + 31) / 32) * 4,
+                       hipMemcpyDeviceToHost),
+             err);
+  return PQ_OK;
 }
 
 int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32_t *offsets, uint8_t *payload,

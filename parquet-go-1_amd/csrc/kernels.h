@@ -20,6 +20,9 @@ struct BatchDev {
   uint32_t *page_rec;             // [npages] records (rep == 0) per page
   uint64_t *page_vbase;           // [npages] value base within chunk
   uint64_t *page_rbase;           // [npages] record base within chunk
+  uint32_t *nest_cnt;             // [ntiles][kNestCnt] lists starting per level, then elements, per tile
+  uint64_t *nest_base;            // [ntiles][kNestCnt] their exclusive prefix within the chunk
+  uint64_t *nest_tot;             // [nchunks][kNestCnt] chunk totals
   HybRun *runs;                   // run tables of hybrid value streams
   const uint64_t *run_base;       // [npages] first entry of each page's run table
   uint32_t *run_count;            // [npages]
@@ -44,6 +47,7 @@ struct BatchDev {
 };
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
+constexpr uint32_t kNestCnt = 9;       // nested counters per page: lists of levels 1..8, then elements
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
                                         // page's BA tiles are its dictionary tiles)
@@ -61,6 +65,9 @@ struct LaunchLists {
   const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
   uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
+  const uint32_t *nest_tiles; uint32_t n_nest_tiles;     // chunk of every 4,096-slot nested tile
+  uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
+  const uint32_t *nest_chunks; uint32_t n_nest_chunks;
   const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)
   uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE
 };
@@ -76,6 +83,9 @@ hipError_t launch_ba_sums(const BatchDev &b, const LaunchLists &l, hipStream_t s
 hipError_t launch_ba_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_ba_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages

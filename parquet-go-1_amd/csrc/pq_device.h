@@ -117,6 +117,12 @@ struct ChunkDesc {       // 192 B
   uint32_t slot_shift;           // byte-array dictionary materialised in 2^slot_shift-byte slots
                                  // [u32 length | bytes] (4, 5 or 6; 0: entries over 60 bytes, no table)
   uint64_t dict_slots;           // device address of the slot table (k_dict_slots, every decode)
+  // nested (Arrow-style) output, max_rep > 0: nest = number of list levels (0: not produced)
+  uint32_t nest, nest_tile0;      // list levels; first k_nest tile of the chunk
+  uint8_t list_null_def[8], list_def[8];  // per REPEATED node: non-null from / has an element from
+  uint64_t lvl_offsets[8];       // int32[num_lists + 1] per level
+  uint64_t lvl_validity[8];      // uint32 bitmap per level
+  uint64_t elem_validity;        // uint32 bitmap over the leaf's element slots
 };
 
 // Chunk flags

@@ -49,7 +49,8 @@ class Error(ctypes.Structure):
 
 class ColumnInfo(ctypes.Structure):
     _fields_ = [("physical_type", ctypes.c_int32), ("type_length", ctypes.c_int32), ("max_def", ctypes.c_int32),
-                ("max_rep", ctypes.c_int32), ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 236)]
+                ("max_rep", ctypes.c_int32), ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 236),
+                ("list_null_def", ctypes.c_int32 * 8), ("list_def", ctypes.c_int32 * 8)]
 
 
 class ChunkMeta(ctypes.Structure):
@@ -65,7 +66,10 @@ class ChunkResult(ctypes.Structure):
                 ("value_width", ctypes.c_int32), ("max_def", ctypes.c_int32), ("max_rep", ctypes.c_int32),
                 ("values", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("payload", ctypes.c_void_p),
                 ("def_levels", ctypes.c_void_p), ("rep_levels", ctypes.c_void_p), ("validity", ctypes.c_void_p),
-                ("list_offsets", ctypes.c_void_p)]
+                ("list_offsets", ctypes.c_void_p), ("nest_levels", ctypes.c_int32), ("dictionary_page", ctypes.c_int32),
+                ("num_lists", ctypes.c_int64 * 8), ("lvl_offsets", ctypes.c_void_p * 8),
+                ("lvl_validity", ctypes.c_void_p * 8), ("num_elements", ctypes.c_int64),
+                ("element_validity", ctypes.c_void_p)]
 
 
 class BatchStats(ctypes.Structure):
@@ -104,7 +108,7 @@ _EXPORTS = [
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
     "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
     "pqgpu_copy", "pqgpu_pipeline_create", "pqgpu_pipeline_next", "pqgpu_pipeline_release", "pqgpu_pipeline_stats_get",
-    "pqgpu_pipeline_destroy",
+    "pqgpu_pipeline_destroy", "pqgpu_batch_copy_nested",
 ]
 
 
@@ -154,6 +158,7 @@ def lib():
                                     ctypes.c_int),
         "pqgpu_batch_kernel_bytes": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
         "pqgpu_copy": ([P, P, P, ctypes.c_size_t, E], ctypes.c_int),
+        "pqgpu_batch_copy_nested": ([P, ctypes.c_int32, ctypes.c_int32, P, P, P, E], ctypes.c_int),
         "pqgpu_pipeline_create": ([P, P, P, ctypes.c_int32, P, ctypes.c_int32, ctypes.POINTER(PipelineOpts),
                                    ctypes.POINTER(P), E], ctypes.c_int),
         "pqgpu_pipeline_next": ([P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
@@ -454,7 +459,22 @@ class Batch:
         if rc and not r.num_slots:
             _check(rc, err)
         payload = pay[: r.payload_bytes].tobytes() if pay is not None else None
-        return ColumnData(info, r, vals, offs, payload, dl, rl, valid, lists)
+        cd = ColumnData(info, r, vals, offs, payload, dl, rl, valid, lists)
+        cd.nested = []  # Arrow-style list levels, outermost first: (offsets int32[n+1], validity bits uint8[n])
+        cd.element_validity = None
+        for k in range(r.nest_levels):
+            n = r.num_lists[k]
+            lo = np.zeros(n + 1, np.int32)
+            lv = np.zeros(max((n + 31) // 32, 1), np.uint32)
+            ev = np.zeros(max((r.num_elements + 31) // 32, 1), np.uint32) if k == 0 else None
+            _check(lib().pqgpu_batch_copy_nested(self._h, cid, k, lo.ctypes.data_as(ctypes.c_void_p),
+                                                 lv.ctypes.data_as(ctypes.c_void_p),
+                                                 None if ev is None else ev.ctypes.data_as(ctypes.c_void_p),
+                                                 ctypes.byref(err)), err)
+            cd.nested.append((lo, np.unpackbits(lv.view(np.uint8), bitorder="little")[:n]))
+            if ev is not None:
+                cd.element_validity = np.unpackbits(ev.view(np.uint8), bitorder="little")[: r.num_elements]
+        return cd
 
 
 class _PipelineBatch(Batch):

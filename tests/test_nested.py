@@ -1,0 +1,164 @@
+"""Arrow-style nested arrays of repeated leaves (nested.hip): per REPEATED node on the leaf's path,
+list offsets into the next level (innermost: into the leaf's element slots) and list validity (a
+null list and an empty list both have no children), plus element validity.
+
+The arrays are a function of the leaf's (rep, def) levels and its path (the levels themselves are
+pinned against the reference's tests and the oracle elsewhere). `nested_ref` restates that
+function slot by slot (the record assembly rules of ColumnStore.get data_store.go:262-309 and
+Column.getData schema.go:216-312: rLevel < maxR starts a new object, dLevel < maxD is a null or
+absent value), and is pinned here by (1) the Dremel / Twitter documents of the reference's tests
+(data_store_test.go:227-390), whose nesting is written out by hand below, and (2) pyarrow's own
+ListArray / MapArray reading of the cfg4 fixtures (an independent Dremel -> Arrow implementation).
+The GPU must equal `nested_ref` applied to the oracle's levels."""
+import io
+
+import numpy as np
+import pytest
+
+import pqtest
+import py_oracle as O
+import test_ref_goldens as G
+
+
+def nested_ref(rep, dfn, max_def, list_null_def, list_def):
+    """[(offsets, validity) per list level, outermost first], element validity."""
+    R = len(list_def)
+    offs = [[] for _ in range(R)]
+    valid = [[] for _ in range(R)]
+    cnt = [0] * (R + 1)  # lists per level 1..R, then leaf elements
+    elem = []
+    for r, d in zip(rep, dfn):
+        for k in range(1, R + 1):
+            if r < k and d >= (list_def[k - 2] if k >= 2 else 0):
+                offs[k - 1].append(cnt[k])  # children of the level-k list before this slot
+                valid[k - 1].append(int(d >= list_null_def[k - 1]))
+                cnt[k - 1] += 1
+        if d >= list_def[R - 1]:
+            elem.append(int(d == max_def))
+            cnt[R] += 1
+    for k in range(R):
+        offs[k].append(cnt[k + 1])
+    return [(np.array(o, np.int64), np.array(v, np.uint8)) for o, v in zip(offs, valid)], np.array(elem, np.uint8)
+
+
+# Hand-derived nesting of the reference's documents: path -> (levels [(offsets, validity)], element validity)
+GOLDEN = {
+    ("dremel", "Links.Backward"): ([([0, 0, 2], [1, 1])], [1, 1]),  # r1: Links present, no Backward (empty)
+    ("dremel", "Links.Forward"): ([([0, 3, 4], [1, 1])], [1, 1, 1, 1]),
+    ("dremel", "Name.Language.Code"): ([([0, 3, 4], [1, 1]), ([0, 2, 2, 3, 3], [1, 1, 1, 1])], [1, 1, 1]),
+    ("dremel", "Name.Language.Country"): ([([0, 3, 4], [1, 1]), ([0, 2, 2, 3, 3], [1, 1, 1, 1])], [1, 0, 1]),
+    ("dremel", "Name.URL"): ([([0, 3, 4], [1, 1])], [1, 1, 0, 1]),
+    ("twitter", "level1.level2"): ([([0, 2, 4], [1, 1]), ([0, 3, 7, 8, 10], [1, 1, 1, 1])], [1] * 10),
+    ("one_repeated", "DocID"): ([([0, 2, 2], [1, 1])], [1, 1]),
+}
+
+
+def _levels_of(f, col):
+    ci = f.column(col)
+    return list(ci.list_null_def[:ci.max_rep]), list(ci.list_def[:ci.max_rep]), ci.max_def
+
+
+def _check_nested(got_levels, got_elem, want_levels, want_elem, where):
+    assert len(got_levels) == len(want_levels), where
+    for k, ((go, gv), (wo, wv)) in enumerate(zip(got_levels, want_levels)):
+        np.testing.assert_array_equal(np.asarray(go, np.int64), np.asarray(wo, np.int64), err_msg=f"{where} L{k} offsets")
+        np.testing.assert_array_equal(np.asarray(gv, np.uint8), np.asarray(wv, np.uint8), err_msg=f"{where} L{k} validity")
+    np.testing.assert_array_equal(np.asarray(got_elem, np.uint8), np.asarray(want_elem, np.uint8), err_msg=f"{where} elements")
+
+
+@pytest.mark.parametrize("doc,path", sorted(GOLDEN))
+def test_ref_documents(doc, path):
+    """nested_ref on the reference tests' levels gives the documents' nesting."""
+    import pqgpu
+    data = G.build(doc)
+    f = pqgpu.File(data)
+    col = f.column_paths().index(path)
+    lnd, ld, md = _levels_of(f, col)
+    _, cols, _ = G.DOCS[doc]
+    _, _, _, _, dl, rl = cols[col]
+    got_levels, got_elem = nested_ref(rl, dl, md, lnd, ld)
+    want_levels, want_elem = GOLDEN[(doc, path)]
+    _check_nested(got_levels, got_elem, want_levels, want_elem, f"{doc} {path}")
+
+
+def _nested_fixtures():
+    return [n for n in pqtest.ALL if n.startswith("cfg4")]
+
+
+@pytest.mark.parametrize("name", _nested_fixtures())
+def test_ref_matches_pyarrow(name):
+    """nested_ref on the oracle's levels equals pyarrow's list / map offsets and validity."""
+    import pyarrow.parquet as pq
+    import pqgpu
+    data = pqtest.load(name)
+    f = pqgpu.File(data)
+    of = O.File(data)
+    pf = pq.ParquetFile(io.BytesIO(data))
+    paths = f.column_paths()
+    for rg in range(f.num_row_groups):
+        tbl = pf.read_row_group(rg)
+        for col, path in enumerate(paths):
+            ci = f.column(col)
+            if ci.max_rep == 0:
+                continue
+            r = of.read_chunk(rg, col)
+            lnd, ld, md = _levels_of(f, col)
+            levels, elem = nested_ref(r.rep_levels, r.def_levels, md, lnd, ld)
+            arr = tbl.column(path.split(".")[0]).combine_chunks()
+            offs = np.asarray(arr.offsets, np.int64)
+            np.testing.assert_array_equal(levels[0][0], offs - offs[0], err_msg=f"{name} rg{rg} {path} offsets")
+            np.testing.assert_array_equal(levels[0][1], np.asarray(arr.is_valid(), np.uint8),
+                                          err_msg=f"{name} rg{rg} {path} validity")
+            child = arr.values if not hasattr(arr, "keys") else (arr.keys if path.endswith(".key") else arr.items)
+            child = child.slice(offs[0], offs[-1] - offs[0])
+            np.testing.assert_array_equal(elem, np.asarray(child.is_valid(), np.uint8),
+                                          err_msg=f"{name} rg{rg} {path} elements")
+
+
+def _gpu_nested_all(gpu_ctx, data):
+    import pqgpu
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = {}
+    for rg in range(f.num_row_groups):
+        for col in range(f.num_columns):
+            ids[(rg, col)] = b.add_file_chunk(f, rg, col)[0]
+    b.decode()
+    b.sync()
+    return f, b, ids
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("doc", sorted({d for d, _ in GOLDEN}))
+@pytest.mark.parametrize("v2", [False, True])
+def test_gpu_ref_documents(gpu_ctx, doc, v2):
+    f, b, ids = _gpu_nested_all(gpu_ctx, G.build(doc, v2))
+    for (rg, col), cid in ids.items():
+        path = f.column_paths()[col]
+        if (doc, path) not in GOLDEN:
+            continue
+        r = b.result(cid)
+        want_levels, want_elem = GOLDEN[(doc, path)]
+        _check_nested(r.nested, r.element_validity, want_levels, want_elem, f"gpu {doc} {path}")
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", _nested_fixtures() + ["edge_nulls_v1", "types_v2"])
+def test_gpu_nested_vs_ref(gpu_ctx, name):
+    if name not in pqtest.ALL:
+        pytest.skip("fixture absent")
+    data = pqtest.load(name)
+    of = O.File(data)
+    f, b, ids = _gpu_nested_all(gpu_ctx, data)
+    for (rg, col), cid in ids.items():
+        ci = f.column(col)
+        r = b.result(cid)
+        if ci.max_rep == 0:
+            assert not r.nested
+            continue
+        o = of.read_chunk(rg, col)
+        lnd, ld, md = _levels_of(f, col)
+        want_levels, want_elem = nested_ref(o.rep_levels, o.def_levels, md, lnd, ld)
+        _check_nested(r.nested, r.element_validity, want_levels, want_elem, f"{name} rg{rg} col{col}")
+    b.close()
