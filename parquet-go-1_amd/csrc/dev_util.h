@@ -89,6 +89,8 @@ DEV BatchDev global_view(BatchDev b) {
   b.ba_state = gp(b.ba_state); b.ba_totals = gp(b.ba_totals);
   b.dblk = gp(b.dblk); b.dblk_base = gp(b.dblk_base); b.dblk_n = gp(b.dblk_n); b.dblk_sum = gp(b.dblk_sum);
   b.ba_delta = gp(b.ba_delta);
+  b.lv_runs = gp(b.lv_runs); b.lv_run_base = gp(b.lv_run_base); b.lv_meta = gp(b.lv_meta);
+  b.lv_tile_run = gp(b.lv_tile_run); b.lv_tile0 = gp(b.lv_tile0);
   if (b.dbg) b.dbg = gp(b.dbg);
   return b;
 }

@@ -369,7 +369,7 @@ struct KernelTimer {
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
-    "k_nest_count", "k_nest_emit", "(unused)"};
+    "k_nest_count", "k_nest_emit", "k_level_fill"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -457,6 +457,11 @@ struct pqgpu_batch {
   uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
+  // generic level streams: run tables ([np][2] bases) and k_level_fill tiles
+  std::vector<uint64_t> lv_run_base;
+  std::vector<uint32_t> lv_tile0, lv_tiles;
+  uint64_t lv_run_total = 0;
+  uint64_t o_lv_runs = 0, o_lv_run_base = 0, o_lv_meta = 0, o_lv_tile_run = 0, o_lv_tile0 = 0, l_lv_tiles = 0;
   std::vector<uint32_t> page_nn_init;
   std::vector<uint64_t> page_vbase_out;  // after sync: per-page value bases / non-null counts
   std::vector<uint32_t> page_nn_out;
@@ -977,6 +982,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->nest_chunks.clear();
   b->run_base.assign(np, 0);
   b->tile_base.assign(np, 0);
+  b->lv_run_base.assign(2 * (size_t)np, 0);
+  b->lv_tile0.assign(np, 0);
+  b->lv_tiles.clear();
+  b->lv_run_total = 0;
   b->page_nn_init.assign(np, 0);
   b->ba_tile_page.clear();
   b->ba_tile_order.clear();
@@ -1073,9 +1082,30 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
       PageDesc &pd = b->pages[p];
       in_bytes += pd.rep_len + pd.def_len + pd.val_len;
-      if (hc.col.max_def == 1 && hc.col.max_rep == 0) b->level_pages_bw1.push_back(p);
-      else if (hc.col.max_def > 0 || hc.col.max_rep > 0) b->level_pages.push_back(p);
-      else b->page_nn_init[p] = pd.num_slots;
+      if (hc.col.max_def == 1 && hc.col.max_rep == 0) {
+        b->level_pages_bw1.push_back(p);
+      } else if (hc.col.max_def > 0 || hc.col.max_rep > 0) {
+        // generic: one k_levels workgroup per stream (page << 1 | 0 rep, 1 def) writing a run
+        // table of at most one entry per two stream bytes; k_level_fill tiles expand them
+        if (hc.col.max_rep > 0) {
+          b->level_pages.push_back(p << 1);
+          b->lv_run_base[2 * (size_t)p] = b->lv_run_total;
+          b->lv_run_total += pd.rep_len / 2 + 2;
+        }
+        if (hc.col.max_def > 0) {
+          b->level_pages.push_back(p << 1 | 1);
+          b->lv_run_base[2 * (size_t)p + 1] = b->lv_run_total;
+          b->lv_run_total += pd.def_len / 2 + 2;
+        } else {
+          b->page_nn_init[p] = pd.num_slots;
+        }
+        b->lv_tile0[p] = (uint32_t)b->lv_tiles.size();
+        const uint64_t sb = pd.slot_base, ns = pd.num_slots;
+        const uint64_t nt = ns ? (sb + ns - 1) / kLfTileHost - sb / kLfTileHost + 1 : 0;
+        b->lv_tiles.insert(b->lv_tiles.end(), nt, p);
+      } else {
+        b->page_nn_init[p] = pd.num_slots;
+      }
       if (hc.col.max_rep > 0 && !hc.nest) b->rec_pages.push_back(p);  // nested chunks: k_nest_emit
       const uint32_t ns_p = pd.num_slots;
       auto tiles = [&](uint8_t kind, uint32_t tile) {
@@ -1212,6 +1242,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_vbase = take((uint64_t)np * 8);
   b->o_rbase = take((uint64_t)np * 8);
   b->o_runs = take(b->run_total * sizeof(HybRun));
+  b->o_lv_runs = take(b->lv_run_total * 8);
+  b->o_lv_run_base = take((uint64_t)np * 16);
+  b->o_lv_meta = take((uint64_t)np * 16);
+  b->o_lv_tile_run = take((uint64_t)b->lv_tiles.size() * 8);
+  b->o_lv_tile0 = take((uint64_t)np * 4);
+  b->l_lv_tiles = take((uint64_t)b->lv_tiles.size() * 4);
   b->o_run_base = take((uint64_t)np * 8);
   b->o_tile_base = take((uint64_t)np * 8);
   b->o_items = take(b->items.size() * sizeof(WorkItem));
@@ -1381,6 +1417,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_slot, b->slot_chunks.data(), b->slot_chunks.size() * 4), err);
   HIPCHECK(up(b->l_level, b->level_pages.data(), b->level_pages.size() * 4), err);
   HIPCHECK(up(b->l_level_bw1, b->level_pages_bw1.data(), b->level_pages_bw1.size() * 4), err);
+  HIPCHECK(up(b->o_lv_run_base, b->lv_run_base.data(), b->lv_run_base.size() * 8), err);
+  HIPCHECK(up(b->o_lv_tile0, b->lv_tile0.data(), b->lv_tile0.size() * 4), err);
+  HIPCHECK(up(b->l_lv_tiles, b->lv_tiles.data(), b->lv_tiles.size() * 4), err);
   HIPCHECK(up(b->l_scan, b->scan_pages.data(), b->scan_pages.size() * 4), err);
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
@@ -1425,6 +1464,11 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.nest_base = (uint64_t *)(A + b->o_nest_base);
   d.nest_tot = (uint64_t *)(A + b->o_nest_tot);
   d.runs = (HybRun *)(A + b->o_runs);
+  d.lv_runs = (uint2 *)(A + b->o_lv_runs);
+  d.lv_run_base = (const uint64_t *)(A + b->o_lv_run_base);
+  d.lv_meta = (uint32_t *)(A + b->o_lv_meta);
+  d.lv_tile_run = (uint32_t *)(A + b->o_lv_tile_run);
+  d.lv_tile0 = (const uint32_t *)(A + b->o_lv_tile0);
   d.run_base = (const uint64_t *)(A + b->o_run_base);
   d.run_count = (uint32_t *)(A + b->o_run_count);
   d.tile_first = (uint32_t *)(A + b->o_tile_first);
@@ -1448,6 +1492,8 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_level_pages = (uint32_t)b->level_pages.size();
   l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
+  l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
+  l.n_lv_tiles = (uint32_t)b->lv_tiles.size();
   l.n_ba_delta = (uint32_t)b->ba_delta.size();
   l.scan_pages = (const uint32_t *)(A + b->l_scan);
   l.n_scan_pages = (uint32_t)b->scan_pages.size();
@@ -1533,10 +1579,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(launch_ba_delta(d, l, v), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
     HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
@@ -1724,9 +1772,17 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           if (w == 0) ba_other_nn += nn[p];
         }
       }
-      if (hc.o_def) lvl_bytes += (int64_t)hc.num_slots;
-      if (hc.o_rep) lvl_bytes += (int64_t)hc.num_slots;
-      if (hc.o_valid) lvl_bytes += (int64_t)(hc.num_slots + 7) / 8;
+      {
+        // generic level streams: k_levels walks the streams (run tables), k_level_fill reads them
+        // again and writes the outputs; flat OPTIONAL: k_levels_bw1 writes the validity
+        int64_t lv_out = 0, lv_in = 0;
+        for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) lv_in += b->pages[p].rep_len + b->pages[p].def_len;
+        if (hc.o_def) lv_out += (int64_t)hc.num_slots;
+        if (hc.o_rep) lv_out += (int64_t)hc.num_slots;
+        if (hc.o_valid) lv_out += (int64_t)(hc.num_slots + 7) / 8;
+        if (hc.col.max_rep > 0 || hc.col.max_def > 1) kb[15] += lv_in + lv_out;
+        else lvl_bytes += lv_out;
+      }
       if (w) {
         val_bytes += hc.nn * w;
       } else {

@@ -40,6 +40,12 @@ struct BatchDev {
   uint32_t *dblk_n;               // [npages] blocks the header walk produced
   unsigned long long *dblk_sum;   // [total blocks] sum of each block's deltas (wrapping)
   const BaDelta *ba_delta;         // DELTA_LENGTH / DELTA_BYTE_ARRAY pages
+  // generic level streams (k_levels walk -> k_level_fill)
+  uint2 *lv_runs;                 // run tables: (first value index, bit-packed flag | payload position or RLE value)
+  const uint64_t *lv_run_base;    // [npages][2] first entry of the repetition / definition stream's table
+  uint32_t *lv_meta;              // [npages][4] repetition entries, values covered, definition entries, values covered
+  uint32_t *lv_tile_run;          // [fill tiles][2] run of the tile's first value (repetition, definition)
+  const uint32_t *lv_tile0;       // [npages] the page's first fill tile
   unsigned long long *dbg;        // diagnostic counters (PQ_DEBUG_STAMPS=1), else null
   uint32_t npages, nchunks;
   uint32_t spec;                  // 1: value bases came from the page headers (see k_bases)
@@ -53,7 +59,8 @@ constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-alig
                                         // page's BA tiles are its dictionary tiles)
 
 struct LaunchLists {
-  const uint32_t *level_pages; uint32_t n_level_pages;   // pages with rep or def streams (generic)
+  const uint32_t *level_pages; uint32_t n_level_pages;   // generic level streams: page << 1 | (0 rep, 1 def)
+  const uint32_t *lv_tiles; uint32_t n_lv_tiles;         // page of every k_level_fill tile
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
@@ -73,6 +80,8 @@ struct LaunchLists {
 };
 
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // generic level run tables
+constexpr uint32_t kLfTileHost = 8192;  // k_level_fill tile (kernels.hip kLfTile)
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);

@@ -300,6 +300,13 @@ struct LevelSink {
   uint32_t err_code, err_pos;
   uint32_t stage_len;    // bytes held by the LDS stage passed to window()/piece()
   uint32_t ablate;       // diagnostic build: BatchDev::ablate
+  // generic widths (run tables for k_level_fill)
+  uint2 *runs;           // the stream's run table
+  uint32_t *trun;        // first run of each of the page's fill tiles (stride 2)
+  uint32_t tile_a;       // page slot_base mod kLfTile
+  uint32_t ntiles;       // the page's fill tiles
+  uint32_t covered;      // values the run table covers (num_values unless the stream failed)
+  uint32_t nruns;        // run-table entries
 
   DEV static void or_bits(uint32_t *dst, uint64_t g, uint64_t m) {
     if (!m) return;
@@ -427,6 +434,13 @@ constexpr uint32_t kLvLongRun = 512;            // runs longer than this expand 
 constexpr uint32_t kLvMaxLong = 64;
 constexpr uint16_t kLvExit = 0xffff;
 constexpr uint32_t kNoEntry = 0xffffffffu;
+constexpr uint32_t kLvRunShift = 48;  // generic widths: run counts in the P5 scan's high bits
+constexpr uint64_t kLvValMask = (1ull << kLvRunShift) - 1;
+constexpr uint32_t kLfTile = kLfTileHost;  // values per k_level_fill tile (aligned on the chunk's slots)
+// Fill tiles of a page: the kLfTile-slot blocks of the chunk that hold any of its slots.
+DEV uint32_t lf_tiles(uint64_t slot_base, uint32_t ns) {
+  return ns ? (uint32_t)((slot_base + ns - 1) / kLfTile - slot_base / kLfTile + 1) : 0u;
+}
 enum : uint32_t { LV_RUN = 0, LV_STOP_NEED = 1, LV_STOP_ERR = 2, LV_STOP_TRUNC = 3 };
 
 struct LevelLDS {
@@ -438,7 +452,7 @@ struct LevelLDS {
   uint64_t wsum[kLvThreads / 64];
   uint32_t nckp;
   uint32_t long_f[kLvMaxLong], long_cnt[kLvMaxLong], long_bp[kLvMaxLong], long_val[kLvMaxLong];
-  uint32_t nlong, stop_kind, stop_code, stop_vpos, next_e;
+  uint32_t nlong, nput, stop_kind, stop_code, stop_vpos, next_e;
   uint64_t total;
   uint64_t cnt[16];
   uint32_t bits[kSegSlots / 32];
@@ -568,6 +582,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     }
   };
   uint32_t entry = 0, done = 0, fetched = 0;  // fetched: chunk start the registers hold
+  uint32_t runs_done = 0;                      // generic widths: run-table entries written so far
   fetch(0);
   for (;;) {
     if (done >= need) break;
@@ -582,7 +597,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       const uint32_t k = tid + j * kLvThreads;
       if (k < kWords) L.stage[k] = pre[j];
     }
-    if (tid == 0) { L.nlong = 0; L.stop_kind = LV_RUN; L.next_e = kNoEntry; }
+    if (tid == 0) { L.nlong = 0; L.nput = 0; L.stop_kind = LV_RUN; L.next_e = kNoEntry; }
     if (cs + kLvChunk < n) { fetch(cs + kLvChunk); fetched = cs + kLvChunk; }  // lands during this chunk
     wg_barrier();
     st.lap(0);
@@ -673,6 +688,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     uint64_t mine = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 8; k++) mine += (mbits >> k) & 1u ? nv[k] : 0u;
+    // generic widths: the marked runs' count rides in bits 48.. of the scan (values < 2^41)
+    if constexpr (!BW1) mine += (uint64_t)__popc(mbits) << kLvRunShift;
     for (uint32_t mm = mbits; mm; mm &= mm - 1) {
       const uint32_t k = __builtin_ctz(mm);
       if (L.J0[i0 + k] == i0 + k) {  // a stop on the chain: the exact decoder (hybrid_decoder.go:142-165)
@@ -693,8 +710,34 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       before += q < wv ? t : 0ull;
       total += t;
     }
+    uint64_t ex = before + incl - mine;
+    uint32_t ri = 0;  // generic widths: this thread's first entry in the chunk's part of the run table
+    if constexpr (!BW1) {
+      ri = runs_done + (uint32_t)(ex >> kLvRunShift);
+      ex &= kLvValMask;
+      total &= kLvValMask;
+    }
     if (tid == 0) L.total = total;
-    uint64_t v = (uint64_t)done + before + incl - mine;  // value index of this thread's first marked run
+    uint64_t v = (uint64_t)done + ex;  // value index of this thread's first marked run
+    // Generic widths: the marked runs go to the stream's run table in global memory, in chain
+    // order (first value index; bit-packed flag | payload position, or the RLE value), and the
+    // run holding each fill tile's first value is noted for k_level_fill. Runs past num_values
+    // and an error stop come last in chain order and are not written.
+    auto put = [&](uint32_t f, uint32_t cnt, uint32_t bp, uint32_t value) {
+      if constexpr (BW1) {
+        lv_fill_run<true>(L, sk, cs, send, f, cnt, bp, value);
+      } else {
+        sk.runs[ri] = make_uint2(f, bp ? 0x80000000u | value : value);
+        if (cnt && sk.ntiles) {  // fill tiles whose first value lies in [f, f + cnt): tile k > 0 starts at k * T - a
+          const uint64_t a = sk.tile_a;
+          uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
+          const uint64_t khi = min(((uint64_t)f + cnt - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+          for (; k <= khi; k++) sk.trun[2 * k] = ri;
+        }
+        ++ri;
+        atomicAdd(&L.nput, 1u);
+      }
+    };
     // ---- P6: fill (and the chain's end: exit position or the exact stop)
     while (mbits) {
       const uint32_t k = __builtin_ctz(mbits);
@@ -708,7 +751,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
           L.stop_code = sh.err == kErrLongVarint ? resolve_long_varint(s, p, n) : sh.err;
         } else {
           const uint32_t ok = min(sh.nvals, sh.okvals);
-          lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(ok, rem), sh.bp, sh.value);
+          put((uint32_t)v, min(ok, rem), sh.bp, sh.value);
           if (ok < sh.nvals && ok < rem) {
             L.stop_kind = LV_STOP_TRUNC; L.stop_vpos = (uint32_t)v + ok; L.stop_code = PQ_ERR_EOF;
           } else {
@@ -718,13 +761,14 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         break;
       }
       const FastHdr f = fast_hdr(L.stage, cs, p, n, bw, rs);
-      lv_fill_run<BW1>(L, sk, cs, send, (uint32_t)v, min(nv[k], rem), f.bp, f.value);
+      put((uint32_t)v, min(nv[k], rem), f.bp, f.value);
       if (L.J0[i0 + k] == kLvExit) L.next_e = p + f.adv;  // the chain's last node
       v += nv[k];
     }
     st.lap(5);
     wg_barrier();
-    // long runs: every thread expands 32-value pieces (64 for the generic sink)
+    if constexpr (!BW1) runs_done += L.nput;
+    // long runs (bit width 1): every thread expands 32-value pieces
     const uint32_t nlong = L.nlong;
     for (uint32_t r = 0; r < nlong; r++) {
       const uint32_t f = L.long_f[r], cnt = L.long_cnt[r], bp = L.long_bp[r], lval = L.long_val[r];
@@ -739,6 +783,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     st.lap(6);
     const uint32_t kind = L.stop_kind;
     const uint64_t ndone = (uint64_t)done + L.total;
+    sk.covered = (uint32_t)min(ndone, (uint64_t)need);
+    sk.nruns = runs_done;
     if (kind != LV_RUN) {
       if (kind == LV_STOP_ERR || kind == LV_STOP_TRUNC) sk.error(L.stop_vpos, L.stop_code);
       break;
@@ -843,10 +889,198 @@ __global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu
   __shared__ LevelLDS lds;
   levels_page<true>(b, pages, lds);
 }
-__global__ void __launch_bounds__(kLvThreads) k_levels(BatchDev b_in, const uint32_t *pages) {
+// Generic level streams (repetition levels, definition levels of max_def > 1): one workgroup
+// per (page, stream) — unit = page << 1 | (0: repetition, 1: definition). The walk writes the
+// stream's run table (and the run of every fill tile's first value); k_level_fill expands the
+// tables into levels, validity and counts with the whole chip, so a long page is not expanded
+// by one workgroup.
+__global__ void __launch_bounds__(kLvThreads) k_levels(BatchDev b_in, const uint32_t *units) {
   const BatchDev b = global_view(b_in);
   __shared__ LevelLDS lds;
-  levels_page<false>(b, pages, lds);
+  const uint32_t u = units[blockIdx.x], pi = u >> 1, which = u & 1;
+  const bool rep = which == 0;
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t tid = threadIdx.x, ns = pd.num_slots;
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
+  LevelSink sk;
+  sk.s = gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off);
+  sk.n = rep ? pd.rep_len : pd.def_len;
+  sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+  sk.out = nullptr;
+  sk.bits_lds = nullptr;
+  sk.bits_glob = nullptr;
+  sk.slot_base = pd.slot_base;
+  sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
+  sk.count = 0;
+  sk.err_code = 0;
+  sk.err_pos = 0;
+  sk.stage_len = kLvStageB;
+  sk.ablate = b.ablate;
+  sk.runs = b.lv_runs + b.lv_run_base[2 * pi + which];
+  sk.trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[pi] + which;
+  sk.tile_a = (uint32_t)(pd.slot_base & (kLfTile - 1));
+  sk.ntiles = lf_tiles(pd.slot_base, ns);
+  sk.covered = 0;
+  sk.nruns = 0;
+  if (!rep && tid == 0) b.page_nn[pi] = 0;  // k_level_fill adds the page's non-null count
+  if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+    if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+  } else {
+    lv_walk<false>(lds, sk, ns, st);
+  }
+  if (tid == 0) {
+    b.lv_meta[4 * pi + 2 * which] = sk.nruns;
+    b.lv_meta[4 * pi + 2 * which + 1] = sk.err_code ? 0u : sk.covered;  // a failed page is not expanded
+    if (sk.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
+  }
+  st.lap(6);
+  st.flush(0);
+}
+
+// k_level_fill: the run tables of the generic level streams expanded, one workgroup per fill
+// tile (kLfTile slots aligned on the chunk's slot index, so tiles own whole words of the level
+// arrays and of the validity bitmap). A thread expands kLfGroups groups of eight consecutive
+// values (group q of thread i: slots [q * 2048 + 8 i, + 8) of the tile), each one independent
+// of the others so that their loads overlap: the tile's runs are staged in LDS (or, past
+// kLfRuns of them, searched in global memory), the run of a group's first value is found by
+// binary search and the group advances from there. Outputs: u8 levels, validity (definition
+// level == max_def) and the page's counts (records: repetition level == 0; non-null values),
+// added atomically once per tile.
+constexpr uint32_t kLfGroups = kLfTile / (8 * kLvThreads);
+constexpr uint32_t kLfRuns = 2048;  // runs staged in LDS
+static_assert(kLfGroups * 8 * kLvThreads == kLfTile, "tile = groups x 8 values x threads");
+struct LevelFillLDS {
+  uint2 run[kLfRuns];
+  uint32_t vb[kLfTile / 32];
+  uint32_t cnt[kLvThreads / 64];
+};
+// The eight values of the group [g, g + 8) that lie in [vs, ve), from run table `R` (m runs):
+// one step per run the values cross (usually one, at a run boundary two), each step an RLE
+// broadcast or one read of the bit-packed payload, so the lanes of a wave stay converged.
+template <class RT>
+DEV void lf_group(const RT &R, uint32_t m, const uint8_t *src, uint32_t n, uint32_t bw, uint32_t cmp, int64_t g,
+                  uint32_t vs, uint32_t ve, uint64_t &word, uint32_t &eq) {
+  word = 0;
+  eq = 0;
+  if (vs >= ve) return;
+  uint32_t j = 0;
+  for (uint32_t step = 1u << (31 - __builtin_clz(m)); step; step >>= 1)
+    if (j + step < m && R(j + step).x <= vs) j += step;
+  const uint32_t bmask = (1u << bw) - 1u;
+  for (uint32_t v = vs; v < ve; j++) {
+    const uint2 r = R(j);
+    const uint32_t se = j + 1 < m ? min(ve, R(j + 1).x) : ve;  // this run's part of the group
+    const uint32_t cnt = se - v, sh = v - (uint32_t)g;
+    uint64_t pk;
+    uint32_t e;
+    if (!(r.y >> 31)) {  // RLE
+      pk = 0x0101010101010101ull * (uint64_t)(r.y & 0xffu);
+      e = r.y == cmp ? 0xffu : 0u;
+    } else if (bw <= 7) {  // bit-packed: one read for the segment
+      const uint64_t x = bits64c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v - r.x) * bw, cnt * bw);
+      pk = 0;
+      e = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; q++) {
+        const uint32_t lv = (uint32_t)(x >> (q * bw)) & bmask;
+        pk |= (uint64_t)lv << (8 * q);
+        e |= (uint32_t)(lv == cmp) << q;
+      }
+    } else {  // wide levels (max level >= 128): value by value
+      pk = 0;
+      e = 0;
+      for (uint32_t q = 0; q < cnt; q++) {
+        const uint32_t lv = bits32c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v + q - r.x) * bw, bw);
+        pk |= (uint64_t)(lv & 0xffu) << (8 * q);
+        e |= (uint32_t)(lv == cmp) << q;
+      }
+    }
+    const uint64_t bm = cnt >= 8 ? ~0ull : ((1ull << (8 * cnt)) - 1ull);
+    word |= (pk & bm) << (8 * sh);
+    eq |= (e & ((1u << cnt) - 1u)) << sh;
+    v = se;
+  }
+}
+__global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const uint32_t *tiles) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelFillLDS L;
+  const uint32_t t = blockIdx.x, pi = tiles[t], tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const PageDesc &pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint64_t sbase = pd.slot_base;
+  const uint32_t ns = pd.num_slots, a = (uint32_t)(sbase & (kLfTile - 1)), ntiles = lf_tiles(sbase, ns);
+  const uint32_t k = t - b.lv_tile0[pi];
+  const int64_t t0 = (int64_t)k * kLfTile - a;  // page value index of the tile's first (aligned) slot
+  const uint32_t lo = (uint32_t)max(t0, (int64_t)0), hi = (uint32_t)min(t0 + kLfTile, (int64_t)ns);
+  const uint8_t *page = gp_u64<const uint8_t>(pd.data);
+  for (uint32_t which = 0; which < 2; which++) {
+    const bool rep = which == 0;
+    if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
+    const uint32_t nr = b.lv_meta[4 * pi + 2 * which], cov = b.lv_meta[4 * pi + 2 * which + 1];
+    const uint32_t end = min(hi, cov);
+    if (lo >= end || nr == 0) continue;  // workgroup-uniform
+    const uint2 *runs = b.lv_runs + b.lv_run_base[2 * pi + which];
+    const uint32_t *trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[pi] + which;
+    const uint32_t r0 = trun[2 * k];
+    const bool more = k + 1 < ntiles && (int64_t)(k + 1) * kLfTile - a < (int64_t)cov;
+    const uint32_t m = (more ? trun[2 * (k + 1)] : nr - 1) - r0 + 1;
+    const bool staged = m <= kLfRuns;
+    if (staged)
+      for (uint32_t i = tid; i < m; i += kLvThreads) L.run[i] = runs[r0 + i];
+    wg_barrier();
+    const uint8_t *src = page + (rep ? pd.rep_off : pd.def_off);
+    const uint32_t n = rep ? pd.rep_len : pd.def_len, bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+    const uint32_t cmp = rep ? 0u : (uint32_t)cd.max_def;
+    uint8_t *out = rep ? gp_u64<uint8_t>(cd.rep_levels) : gp_u64<uint8_t>(cd.def_levels);
+    uint32_t *vbits = rep ? nullptr : gp_u64<uint32_t>(cd.validity);
+    uint32_t nc = 0;
+#pragma unroll 1
+    for (uint32_t q = 0; q < kLfGroups; q++) {
+      const int64_t g = t0 + (int64_t)(q * 8 * kLvThreads + 8 * tid);  // the group's values [g, g + 8)
+      const uint32_t vs = (uint32_t)max(g, (int64_t)lo), ve = (uint32_t)max(min(g + 8, (int64_t)end), (int64_t)vs);
+      uint64_t word;
+      uint32_t eq;
+      if (PQ_ABLATE(b, 2)) {
+        word = 0; eq = 0;
+      } else if (staged) {
+        lf_group([&](uint32_t i) { return L.run[i]; }, m, src, n, bw, cmp, g, vs, ve, word, eq);
+      } else {
+        lf_group([&](uint32_t i) { return runs[r0 + i]; }, m, src, n, bw, cmp, g, vs, ve, word, eq);
+      }
+      if (out && vs < ve) {
+        uint8_t *o = out + sbase;
+        if (vs == g && ve == g + 8 && !(reinterpret_cast<uintptr_t>(o + g) & 7)) {
+          *reinterpret_cast<uint2 *>(o + g) = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
+        } else {
+          for (uint32_t v = vs; v < ve; v++) o[v] = (uint8_t)(word >> (8 * (v - (uint32_t)g)));
+        }
+      }
+      nc += __popc(eq);
+      if (vbits) reinterpret_cast<uint8_t *>(L.vb)[q * kLvThreads + tid] = (uint8_t)eq;
+    }
+    // counts: one atomic per tile
+    const uint32_t wc = (uint32_t)wave_sum64(nc);
+    if (lane == 0) L.cnt[wv] = wc;
+    wg_barrier();
+    if (tid == 0) {
+      uint32_t c = 0;
+      for (uint32_t q = 0; q < kLvThreads / 64; q++) c += L.cnt[q];
+      if (c) atomicAdd(rep ? &b.page_rec[pi] : &b.page_nn[pi], c);
+    }
+    if (vbits) {
+      for (uint32_t w = tid; w < kLfTile / 32; w += kLvThreads) {
+        const int64_t w0 = t0 + 32 * (int64_t)w;  // the word's first value
+        if (w0 + 32 <= (int64_t)lo || w0 >= (int64_t)end) continue;
+        const uint32_t v = L.vb[w];
+        uint32_t *dst = vbits + ((sbase + (uint64_t)w0) >> 5);
+        if (w0 >= (int64_t)lo && w0 + 32 <= (int64_t)end) *dst = v;  // the tile owns the whole word
+        else if (v) atomicOr(dst, v);                                 // shared with a neighbouring page
+      }
+    }
+    wg_barrier();  // L is reused by the next stream
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2604,6 +2838,11 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
     hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
   if (l.n_level_pages)
     hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
+  return hipGetLastError();
+}
+hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (l.n_lv_tiles)
+    hipLaunchKernelGGL(k_level_fill, dim3(l.n_lv_tiles), dim3(kLvThreads), 0, s, b, l.lv_tiles);
   return hipGetLastError();
 }
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

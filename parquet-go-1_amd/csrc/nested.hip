@@ -54,7 +54,9 @@ DEV NestTile nest_tile(const BatchDev &b, const uint32_t *tile_chunk, uint32_t t
   return x;
 }
 
-// Per tile: how many entries of each counter (lists of levels 1..R, then leaf elements).
+// Per tile: how many entries of each counter (lists of levels 1..R, then leaf elements). A
+// thread takes 16 consecutive slots with one 16-byte load per level array (the level arrays
+// are 16-byte padded; a tile starts on a multiple of 4,096 slots).
 __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_t *tile_chunk) {
   const BatchDev b = global_view(b_in);
   const uint32_t t = blockIdx.x;
@@ -66,11 +68,24 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_
   __shared__ uint32_t part[kNestCnt][4];
   const uint32_t R = cd.nest, lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t c[kNestCnt] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint64_t s = x.s0 + threadIdx.x; s < x.s1; s += blockDim.x) {
-    const uint32_t r = rl[s], d = slot_def(cd, dl, vb, s);
+  const uint64_t s = x.s0 + 16 * (uint64_t)threadIdx.x;
+  if (s < x.s1) {
+    const uint32_t ns = (uint32_t)min((uint64_t)16, x.s1 - s);
+    const uint4 rv = *reinterpret_cast<const uint4 *>(rl + s);
+    uint4 dv = make_uint4(0, 0, 0, 0);
+    uint32_t vbits = 0;
+    if (dl) dv = *reinterpret_cast<const uint4 *>(dl + s);
+    else if (vb) vbits = vb[s >> 5] >> (s & 31);  // max_def == 1: the bit is the level
+    const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++)
-      if (j <= R) c[j] += nest_flag(cd, j, r, d);
+    for (uint32_t q = 0; q < 16; q++) {
+      const uint32_t r = (rw[q >> 2] >> (8 * (q & 3))) & 0xffu;
+      const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
+      const bool in = q < ns;
+#pragma unroll
+      for (uint32_t j = 0; j < kNestCnt; j++)
+        if (j <= R) c[j] += in && nest_flag(cd, j, r, d);
+    }
   }
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) {
@@ -100,57 +115,57 @@ __global__ void __launch_bounds__(64) k_nest_scan(BatchDev b_in, const uint32_t 
   b.nest_tot[(uint64_t)c * kNestCnt + j] = acc;
 }
 
-// Bitmap writer of one wave over a contiguous range of entries: bits are appended in order and
-// whole 32-bit words leave as plain stores (the wave alone owns them); the first and the last
-// word of the range may be shared with the neighbouring ranges and are OR-ed atomically.
-struct BitRun {
-  uint32_t *bm;
-  uint64_t word;   // index of the word being filled
-  uint32_t acc;    // its bits so far
-  uint32_t nbits;  // bits filled (from the word's bit 0)
-  bool first;      // the range's first word (shared with the previous range)
-  DEV void start(uint32_t *b, uint64_t at) {
-    bm = b;
-    word = at >> 5;
-    nbits = (uint32_t)(at & 31);
-    acc = 0;
-    first = true;
+// Bits of x at the positions set in m, packed towards bit 0 (Hacker's Delight 7-4, compress).
+DEV uint32_t compress32(uint32_t x, uint32_t m) {
+  x &= m;
+  uint32_t mk = ~m << 1;
+#pragma unroll
+  for (uint32_t i = 0; i < 5; i++) {
+    uint32_t mp = mk ^ (mk << 1);
+    mp ^= mp << 2;
+    mp ^= mp << 4;
+    mp ^= mp << 8;
+    mp ^= mp << 16;
+    const uint32_t mv = mp & m;
+    m = (m ^ mv) | (mv >> (1u << i));
+    const uint32_t t = x & mv;
+    x = (x ^ t) | (t >> (1u << i));
+    mk &= ~mp;
   }
-  DEV void flush_word() {
-    if (first) atomicOr(&bm[word], acc);
-    else bm[word] = acc;
-    first = false;
-    ++word;
-    acc = 0;
-    nbits = 0;
-  }
-  DEV void append(uint64_t m, uint32_t n) {  // the low n bits of m (n <= 64)
-    while (n) {
-      const uint32_t take = min(n, 32u - nbits);
-      const uint32_t part = (uint32_t)(take == 64 ? m : (m & ((1ull << take) - 1)));
-      acc |= part << nbits;
-      nbits += take;
-      m = take >= 64 ? 0 : m >> take;
-      n -= take;
-      if (nbits == 32) flush_word();
+  return x;
+}
+
+// nbits bits of the wave's LDS row (from bit 0) to bitmap bits [off, off + nbits): lane k writes
+// destination word k of the range; the first and the last word may be shared with neighbouring
+// ranges and are OR-ed atomically, the others are owned and stored.
+DEV void nest_put_bits(uint32_t *bm, uint64_t off, const uint32_t *row, uint32_t nbits, uint32_t lane) {
+  if (!nbits) return;
+  const uint32_t sh = (uint32_t)(off & 31);
+  const uint64_t w0 = off >> 5;
+  const uint32_t nw = (uint32_t)(((off + nbits + 31) >> 5) - w0);
+  for (uint32_t k = lane; k < nw; k += 64) {
+    const uint32_t v = (row[k] << sh) | (k && sh ? row[k - 1] >> (32 - sh) : 0u);
+    if (k == 0 || k == nw - 1) {
+      if (v) atomicOr(&bm[w0 + k], v);
+    } else {
+      bm[w0 + k] = v;
     }
   }
-  DEV void finish() {
-    if (nbits) atomicOr(&bm[word], acc);  // shared with the next range
-  }
-};
+}
 
-// Per tile: wave w owns 1,024 consecutive slots. Pass 1 counts each counter per wave (ballots);
-// one barrier gives every wave its first entry index; pass 2 walks the slots again 64 at a time
-// with a running index per counter: a level's lists in 64 slots are consecutive entries. Their
-// validity bits: each flagged lane writes its bit at its rank into a per-wave LDS row, a ballot
-// over the row reads them back packed, and a wave-uniform BitRun appends them to the bitmap.
-// List offsets are the child counter's index at the list's first slot. Counter 0 (a level-1
-// list starts: rep == 0) also gives the record offsets (ColumnStore.get's record split).
+// Per tile: wave w owns 1,024 consecutive slots, lane i sixteen of them (one 16-byte load per
+// level array). Per counter j a lane holds the 16-bit mask of its flagged slots; wave prefix
+// sums of their counts (and one workgroup exchange of the wave totals) give every entry its
+// index. List offsets (the child counter's index at the list's first slot) and record offsets
+// (counter 0: a level-1 list starts at rep == 0, ColumnStore.get's record split) are staged in a
+// per-wave LDS row in entry order and leave as contiguous stores; the entries' validity bits are
+// compressed out of the lane's slot mask, placed at their index in a per-wave LDS bit row and
+// written with a funnel shift to their place in the bitmap.
 // R: the chunks' list levels (the launch covers the tiles of chunks with nest == R, so every
 // per-counter array is indexed by compile-time constants and stays in registers).
 template <uint32_t R>
 __global__ void __launch_bounds__(256) k_nest_emit(BatchDev b_in, const uint32_t *tile_chunk, uint32_t first) {
+  constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   const uint32_t t = first + blockIdx.x;
   const NestTile x = nest_tile(b, tile_chunk, t);
@@ -160,77 +175,91 @@ __global__ void __launch_bounds__(256) k_nest_emit(BatchDev b_in, const uint32_t
   const uint32_t *vb = gp_u64<const uint32_t>(cd.validity);
   int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
   const uint32_t maxd = (uint32_t)cd.max_def;
-  __shared__ uint32_t wcnt[R + 1][4];
-  __shared__ uint8_t vrow[4][R + 1][64];
+  __shared__ uint32_t wtot[C][4];
+  __shared__ uint32_t ent[4][kNestWaveSlots];
+  __shared__ uint32_t brow[4][kNestWaveSlots / 32 + 1];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1;
-  const uint64_t w0 = x.s0 + (uint64_t)wv * kNestWaveSlots, w1 = min(w0 + kNestWaveSlots, x.s1);
-  // the wave's 16 x 64 slots' levels, loaded once (all loads in flight together), packed r | d << 8
-  constexpr uint32_t kSteps = kNestWaveSlots / 64;
-  uint32_t rd[kSteps];
-#pragma unroll
-  for (uint32_t k = 0; k < kSteps; k++) {
-    const uint64_t sl = w0 + 64 * k + lane;
-    rd[k] = sl < w1 ? (uint32_t)rl[sl] | (slot_def(cd, dl, vb, sl) << 8) : 0u;
+  const uint64_t s = x.s0 + (uint64_t)wv * kNestWaveSlots + 16 * (uint64_t)lane;
+  const uint32_t ns = s < x.s1 ? (uint32_t)min((uint64_t)16, x.s1 - s) : 0u;
+  uint4 rv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
+  uint32_t vbits = 0;
+  if (ns) {
+    rv = *reinterpret_cast<const uint4 *>(rl + s);
+    if (dl) dv = *reinterpret_cast<const uint4 *>(dl + s);
+    else if (vb) vbits = vb[s >> 5] >> (s & 31);  // max_def == 1: the bit is the level
   }
-  // pass 1: this wave's entries per counter
-  uint32_t cnt[R + 1] = {};
+  // the lane's flag and validity masks per counter
+  uint32_t f[C], vm[C];
 #pragma unroll
-  for (uint32_t k = 0; k < kSteps; k++) {
-    const uint64_t sl = w0 + 64 * k + lane;
-    const uint32_t r = rd[k] & 0xffu, d = rd[k] >> 8;
+  for (uint32_t j = 0; j < C; j++) f[j] = vm[j] = 0;
+  {
+    const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
-    for (uint32_t j = 0; j <= R; j++) cnt[j] += (uint32_t)__popcll(__ballot(sl < w1 && nest_flag(cd, j, r, d)));
-  }
-  if (lane == 0) {
+    for (uint32_t q = 0; q < 16; q++) {
+      const uint32_t r = (rw[q >> 2] >> (8 * (q & 3))) & 0xffu;
+      const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
+      const uint32_t in = q < ns ? 1u : 0u;
 #pragma unroll
-    for (uint32_t j = 0; j <= R; j++) wcnt[j][wv] = cnt[j];
-  }
-  wg_barrier();
-  uint64_t run[R + 1];
-  BitRun bits[R + 1];
-#pragma unroll
-  for (uint32_t j = 0; j <= R; j++) {
-    uint64_t v = b.nest_base[(uint64_t)t * kNestCnt + j];
-    for (uint32_t q = 0; q < wv; q++) v += wcnt[j][q];
-    run[j] = v;
-    bits[j].start(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), v);
-  }
-  // pass 2
-#pragma unroll 1
-  for (uint32_t k = 0; k < (PQ_ABLATE(b, 18) ? 0u : kSteps); k++) {  // diagnostic bit 18: no pass 2
-    const uint64_t my = w0 + 64 * k + lane;
-    if (w0 + 64 * k >= w1) break;  // wave-uniform
-    const uint32_t r = rd[k] & 0xffu, d = rd[k] >> 8;
-    uint64_t mask[R + 1];
-#pragma unroll
-    for (uint32_t j = 0; j <= R; j++) {
-      mask[j] = __ballot(my < w1 && nest_flag(cd, j, r, d));
-      if ((mask[j] >> lane) & 1ull)
-        vrow[wv][j][__popcll(mask[j] & lt)] = (uint8_t)(j < R ? d >= cd.list_null_def[j] : d == maxd);
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < R; j++) {
-      if (((mask[j] >> lane) & 1ull) && !PQ_ABLATE(b, 16)) {  // diagnostic bit 16: no offset stores
-        const uint32_t q = (uint32_t)__popcll(mask[j] & lt);
-        const uint32_t qc = (uint32_t)__popcll(mask[j + 1] & lt);  // children before this slot
-        gp_u64<int32_t>(cd.lvl_offsets[j])[run[j] + q] = (int32_t)(run[j + 1] + qc);
-        if (j == 0 && rec) rec[run[0] + q] = (int32_t)my;  // a record starts at this slot
+      for (uint32_t j = 0; j < C; j++) {
+        f[j] |= (in & (uint32_t)nest_flag(cd, j, r, d)) << q;
+        vm[j] |= (uint32_t)(j < R ? d >= cd.list_null_def[j] : d == maxd) << q;
       }
     }
-    wave_lds_sync();
+  }
+  // entry indices: wave prefix sums, then the waves before this one in the tile
+  uint32_t P[C], T[C];
 #pragma unroll
-    for (uint32_t j = 0; j <= R; j++) {
-      const uint32_t m = (uint32_t)__popcll(mask[j]);
-      const uint64_t v = __ballot(lane < m && vrow[wv][j][lane]);
-      if (!PQ_ABLATE(b, 17)) bits[j].append(v, m);  // diagnostic bit 17: no bitmaps
-      run[j] += m;
+  for (uint32_t j = 0; j < C; j++) {
+    const uint32_t c = (uint32_t)__popc(f[j]);
+    const uint32_t incl = (uint32_t)wave_incl_scan64_dpp(c);
+    P[j] = incl - c;
+    T[j] = (uint32_t)__shfl(incl, 63);
+    if (lane == 0) wtot[j][wv] = T[j];
+  }
+  wg_barrier();
+  uint64_t run[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    uint64_t v = b.nest_base[(uint64_t)t * kNestCnt + j];
+    for (uint32_t q = 0; q < wv; q++) v += wtot[j][q];
+    run[j] = v;
+  }
+  uint32_t *row = ent[wv];
+  // list offsets of each level, then the record offsets (level-1 list starts)
+#pragma unroll
+  for (uint32_t j = 0; j <= R; j++) {
+    const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
+    if (j == R && !rec) break;
+    if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
+    uint32_t m = f[lv], k = P[lv];
+    const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
+    while (m) {
+      const uint32_t i = __builtin_ctz(m);
+      m &= m - 1;
+      row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
     }
     wave_lds_sync();
+    int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
+    for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
+    wave_lds_sync();
   }
+  // validity bits of every counter's entries
+  uint32_t *bits = brow[wv];
 #pragma unroll
-  for (uint32_t j = 0; j <= R; j++)
-    if (!PQ_ABLATE(b, 17)) bits[j].finish();
+  for (uint32_t j = 0; j < C; j++) {
+    if (PQ_ABLATE(b, 17)) break;  // diagnostic bit 17: no bitmaps
+    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+    wave_lds_sync();
+    const uint32_t c = (uint32_t)__popc(f[j]);
+    if (c) {
+      const uint32_t comp = compress32(vm[j], f[j]), p = P[j], sh = p & 31;
+      atomicOr(&bits[p >> 5], comp << sh);
+      if (sh && sh + c > 32) atomicOr(&bits[(p >> 5) + 1], comp >> (32 - sh));
+    }
+    wave_lds_sync();
+    nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
+    wave_lds_sync();
+  }
   // the chunk's last tile closes every level's offsets and the record offsets
   const uint32_t nt = (uint32_t)((cd.num_slots + kNestTile - 1) / kNestTile);
   if (x.local == nt - 1 && threadIdx.x < R) {
