@@ -436,6 +436,9 @@ constexpr uint16_t kLvExit = 0xffff;
 constexpr uint32_t kNoEntry = 0xffffffffu;
 constexpr uint32_t kLvRunShift = 48;  // generic widths: run counts in the P5 scan's high bits
 constexpr uint64_t kLvValMask = (1ull << kLvRunShift) - 1;
+constexpr uint32_t kLvTileBuf = 64;
+constexpr uint32_t kLvSerialHops = 48;    // P0: hops one lane takes before the chunk goes to list ranking
+constexpr uint32_t kLvSerialBackoff = 4;  // chunks P0 is not tried after it ran out of hops  // fill-tile starts buffered per chunk (more go out directly)
 constexpr uint32_t kLfTile = kLfTileHost;  // values per k_level_fill tile (aligned on the chunk's slots)
 // Fill tiles of a page: the kLfTile-slot blocks of the chunk that hold any of its slots.
 DEV uint32_t lf_tiles(uint64_t slot_base, uint32_t ns) {
@@ -455,7 +458,11 @@ struct LevelLDS {
   uint32_t nlong, nput, stop_kind, stop_code, stop_vpos, next_e;
   uint64_t total;
   uint64_t cnt[16];
-  uint32_t bits[kSegSlots / 32];
+  union {
+    uint32_t bits[kSegSlots / 32];  // bit width 1: the page's first kSegSlots validity bits
+    uint2 rbuf[kLvChunk / 2];       // generic widths: the chunk's run-table entries
+  };
+  uint32_t tb_k[kLvTileBuf], tb_r[kLvTileBuf], ntb;  // generic widths: fill-tile starts of the chunk
 };
 
 // Fast candidate at stream position c: a header varint of at most 4 bytes whose run is
@@ -583,6 +590,35 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
   };
   uint32_t entry = 0, done = 0, fetched = 0;  // fetched: chunk start the registers hold
   uint32_t runs_done = 0;                      // generic widths: run-table entries written so far
+  // Generic widths: a chunk's run-table entries and fill-tile starts are collected in LDS and
+  // stored at the top of the next chunk, before its prefetch is issued. vmcnt counts stores too
+  // and loads and stores complete out of order, so the wait for a prefetch is a wait for every
+  // earlier store: stores issued late in a chunk would put their latency on the critical path.
+  uint32_t pend_n = 0, pend_t = 0, pend_base = 0;
+  auto flush = [&]() {
+    if constexpr (!BW1) {
+      for (uint32_t e = tid; e < pend_n; e += kLvThreads) sk.runs[pend_base + e] = L.rbuf[e];
+      for (uint32_t e = tid; e < pend_t; e += kLvThreads) sk.trun[2 * L.tb_k[e]] = L.tb_r[e];
+      pend_n = pend_t = 0;
+    }
+  };
+  // Generic widths: run-table entry idx (chain order) and the fill tiles whose first value it holds
+  auto put_run = [&](uint32_t idx, uint32_t f, uint32_t cnt, uint32_t bp, uint32_t value) {
+    if constexpr (!BW1) {
+      L.rbuf[idx - runs_done] = make_uint2(f, bp ? 0x80000000u | value : value);
+      if (cnt && sk.ntiles) {  // fill tiles whose first value lies in [f, f + cnt): tile k > 0 starts at k * T - a
+        const uint64_t a = sk.tile_a;
+        uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
+        const uint64_t khi = min(((uint64_t)f + cnt - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+        for (; k <= khi; k++) {
+          const uint32_t q = atomicAdd(&L.ntb, 1u);
+          if (q < kLvTileBuf) { L.tb_k[q] = (uint32_t)k; L.tb_r[q] = idx; }
+          else sk.trun[2 * k] = idx;
+        }
+      }
+      atomicAdd(&L.nput, 1u);
+    }
+  };
   fetch(0);
   for (;;) {
     if (done >= need) break;
@@ -597,7 +633,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       const uint32_t k = tid + j * kLvThreads;
       if (k < kWords) L.stage[k] = pre[j];
     }
-    if (tid == 0) { L.nlong = 0; L.nput = 0; L.stop_kind = LV_RUN; L.next_e = kNoEntry; }
+    if (tid == 0) { L.nlong = 0; L.nput = 0; L.ntb = 0; L.stop_kind = LV_RUN; L.next_e = kNoEntry; }
+    flush();
     if (cs + kLvChunk < n) { fetch(cs + kLvChunk); fetched = cs + kLvChunk; }  // lands during this chunk
     wg_barrier();
     st.lap(0);
@@ -727,15 +764,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       if constexpr (BW1) {
         lv_fill_run<true>(L, sk, cs, send, f, cnt, bp, value);
       } else {
-        sk.runs[ri] = make_uint2(f, bp ? 0x80000000u | value : value);
-        if (cnt && sk.ntiles) {  // fill tiles whose first value lies in [f, f + cnt): tile k > 0 starts at k * T - a
-          const uint64_t a = sk.tile_a;
-          uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
-          const uint64_t khi = min(((uint64_t)f + cnt - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
-          for (; k <= khi; k++) sk.trun[2 * k] = ri;
-        }
-        ++ri;
-        atomicAdd(&L.nput, 1u);
+        put_run(ri++, f, cnt, bp, value);
       }
     };
     // ---- P6: fill (and the chain's end: exit position or the exact stop)
@@ -767,7 +796,12 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     }
     st.lap(5);
     wg_barrier();
-    if constexpr (!BW1) runs_done += L.nput;
+    if constexpr (!BW1) {
+      pend_base = runs_done;
+      pend_n = L.nput;
+      pend_t = min(L.ntb, kLvTileBuf);
+      runs_done += pend_n;
+    }
     // long runs (bit width 1): every thread expands 32-value pieces
     const uint32_t nlong = L.nlong;
     for (uint32_t r = 0; r < nlong; r++) {
@@ -794,6 +828,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     entry = L.next_e;  // kNoEntry cannot happen: a chain that needs more values exits or stops
     if (entry == kNoEntry) { sk.error(done, PQ_ERR_INVALID); break; }
   }
+  flush();  // the last chunk's entries (written before its final barrier)
 }
 
 // BW1: every level stream of the pages is a bit-width-1 definition stream with validity
@@ -894,7 +929,8 @@ __global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu
 // stream's run table (and the run of every fill tile's first value); k_level_fill expands the
 // tables into levels, validity and counts with the whole chip, so a long page is not expanded
 // by one workgroup.
-__global__ void __launch_bounds__(kLvThreads) k_levels(BatchDev b_in, const uint32_t *units) {
+__global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu(PQ_LV_WPE))) k_levels(BatchDev b_in,
+                                                                                          const uint32_t *units) {
   const BatchDev b = global_view(b_in);
   __shared__ LevelLDS lds;
   const uint32_t u = units[blockIdx.x], pi = u >> 1, which = u & 1;

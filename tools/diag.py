@@ -10,8 +10,11 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-go-1_amd"))
 import pqgpu  # noqa: E402
 from tools import workloads  # noqa: E402
 
-rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4 * 4194304
-out = workloads.gen_cfg2(rows)
+cfg = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].isdigit() else "cfg2"
+args = [a for a in sys.argv[1:] if a.isdigit()]
+rows = int(args[0]) if args else None
+gen = getattr(workloads, "gen_" + cfg)
+out = gen(rows) if rows else gen()
 data = out[0] if isinstance(out, tuple) else out
 ctx = pqgpu.Context(0)
 f = pqgpu.File(data)
@@ -27,8 +30,8 @@ b.decode(); b.sync()
 dt = time.perf_counter() - t0
 d = b.debug_counters()
 pages = f.num_row_groups * 64 * 2
-print(f"decode {dt*1e3:.3f} ms for {rows} rows; {pages} level pages, {pages//2} DELTA pages")
-names = ["stage", "P1_links", "P1b_doubling", "P2_walk", "P3_fill", "P3_bar", "end", "chunk_top"]
+print(f"decode {dt*1e3:.3f} ms ({cfg}); per-page figures assume cfg2's {pages} level pages")
+names = ["stage", "P1_links", "P2_doubling", "P3_ckp", "P4_walkers", "P5_P6", "tail", "chunk_top"]
 for k, n in enumerate(names):
     v = int(d[k])
     print(f"levels {n:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
