@@ -330,10 +330,10 @@ static bool delta_tiled() {
   return t && atoi(t) != 0;
 }
 
-static bool spec_disabled() {
+static bool spec_disabled() {  // PQ_SPEC=0 or PQ_NO_SPEC=1: the reference's serial order
   const char *on = getenv("PQ_SPEC"), *off = getenv("PQ_NO_SPEC");
   if (off && atoi(off) != 0) return true;
-  return !(on && atoi(on) != 0);
+  return on && atoi(on) == 0;
 }
 
 struct KernelTimer {
@@ -468,8 +468,8 @@ struct pqgpu_batch {
   std::vector<uint32_t> page_nn_spec;   // header non-null counts (speculative mode)
   std::vector<uint64_t> page_vbase_spec; // their per-chunk exclusive prefix
   bool spec = false;                     // this upload runs values concurrently with k_levels
-  // Speculative concurrent schedule (values beside k_levels) is opt-in: PQ_SPEC=1. Measured on
-  // cfg2 it loses to the serial order (both kernels contend for LDS); see DESIGN.md.
+  // Speculative concurrent schedule (values beside k_levels) whenever every page's non-null count
+  // is known up front; PQ_SPEC=0 keeps the serial order. cfg2: 0.559 vs 0.595 ms per step.
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;

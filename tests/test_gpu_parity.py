@@ -100,7 +100,7 @@ def test_file_reader_mirror(gpu_ctx):
 
 def test_speculative_and_serial_schedules_agree(gpu_ctx, monkeypatch):
     """V2 pages carry num_nulls, so values run concurrently with the level decode on header
-    counts (host.cpp decode_impl); PQ_SPEC=0 (the default) keeps the reference's serial order. Both must
+    counts (host.cpp decode_impl, the default); PQ_SPEC=0 keeps the reference's serial order. Both must
     give the oracle's bytes, including on a file whose num_nulls header is wrong."""
     for name in ("cfg2_v2_small", "bad_v2_num_nulls", "edge_nulls_v2", "cfg4_v2"):
         data = pqtest.load(name)
