@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 4
+#define PQGPU_ABI_VERSION 5
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -175,6 +175,9 @@ void pqgpu_ctx_destroy(pqgpu_ctx *ctx);
 int pqgpu_file_open(const uint8_t *buf, size_t len, pqgpu_file **out, pqgpu_error *err);
 void pqgpu_file_close(pqgpu_file *f);
 int pqgpu_file_num_row_groups(const pqgpu_file *f);
+/* The borrowed file buffer passed to pqgpu_file_open, and its length. */
+const uint8_t *pqgpu_file_bytes(const pqgpu_file *f);
+size_t pqgpu_file_len(const pqgpu_file *f);
 int pqgpu_file_num_columns(const pqgpu_file *f);
 int64_t pqgpu_file_row_group_num_rows(const pqgpu_file *f, int rg);
 int pqgpu_file_column(const pqgpu_file *f, int col, pqgpu_column_info *out);
@@ -206,6 +209,60 @@ int pqgpu_batch_add_chunk(pqgpu_batch *b, const uint8_t *file_bytes, size_t file
  * (FileReader.readRowGroupData chunk_reader.go:375-404). */
 int pqgpu_batch_add_file_chunk(pqgpu_batch *b, const pqgpu_file *f, int rg, int col, int validate_crc,
                                int32_t *chunk_id, pqgpu_error *err);
+
+/* ---- on-device page index -------------------
+ * readPages' page-header loop (chunk_reader.go:182-263), the Thrift compact
+ * decode of every PageHeader (readThrift helpers.go:103-109) and readPageBlock's
+ * CRC32 check (chunk_reader.go:173-177), on the GPU, for column chunks whose
+ * bytes are resident in device memory: `dev_bytes` (16-byte aligned) holds
+ * file bytes [file_offset, file_offset + len), e.g. one row group's byte
+ * range copied H2D once. One wavefront per chunk walks the header chain;
+ * with validate_crc every checksummed block is checked by k_page_crc. The
+ * walk takes the valid case only: a chunk it cannot take (a Thrift error, a
+ * negative size, a block past the resident bytes) is marked
+ * PQGPU_IX_FALLBACK and pqgpu_batch_add_indexed_chunk walks it on the host,
+ * so every error keeps the reference's class, message and page. Synchronous
+ * (the page table is read back). */
+typedef struct pqgpu_page_index pqgpu_page_index;
+enum { PQGPU_IX_OK = 0, PQGPU_IX_FALLBACK = 1 };
+/* PageHeader flags */
+enum { PQGPU_PH_CRC = 1, PQGPU_PH_DATA_PAGE = 2, PQGPU_PH_DICTIONARY_PAGE = 4, PQGPU_PH_DATA_PAGE_V2 = 8,
+       PQGPU_PH_V2_COMPRESSED = 16, PQGPU_PH_CRC_CHECKED = 32, PQGPU_PH_CRC_OK = 64 };
+typedef struct {
+  int64_t header_offset;          /* file offset of the PageHeader */
+  int32_t header_len;             /* its Thrift bytes */
+  int32_t type;                   /* parquet.PageType */
+  int32_t uncompressed_page_size;
+  int32_t compressed_page_size;
+  int32_t crc;
+  int32_t flags;                  /* PQGPU_PH_* (which optional members are set) */
+  int32_t data_page[4];           /* DataPageHeader: num_values, encoding, def/rep level encoding */
+  int32_t dictionary_page[2];     /* DictionaryPageHeader: num_values, encoding */
+  int32_t data_page_v2[6];        /* DataPageHeaderV2: num_values, num_nulls, num_rows, encoding,
+                                     definition / repetition levels byte length */
+} pqgpu_page_header;
+int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_offset, int64_t len,
+                           const pqgpu_chunk_meta *metas, int32_t n_chunks, int32_t validate_crc, void *stream,
+                           pqgpu_page_index **out, pqgpu_error *err);
+int pqgpu_page_index_chunk(const pqgpu_page_index *ix, int32_t chunk, int32_t *num_pages, int32_t *status);
+int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, pqgpu_page_header *out);
+double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix);
+void pqgpu_page_index_destroy(pqgpu_page_index *ix);
+/* The host's PageHeader decode (the same fields), for comparison. */
+int pqgpu_parse_page_header(const uint8_t *buf, size_t len, pqgpu_page_header *out, int64_t *consumed);
+/* pqgpu_batch_add_chunk for chunk `ix_chunk` of an index (its chunk meta): the
+ * page headers and CRC verdicts come from the device walk, and UNCOMPRESSED
+ * data pages are not copied on the host — their blocks are copied device to
+ * device from the resident bytes at upload (k_page_gather), so `dev_bytes`
+ * must stay valid until pqgpu_batch_upload returns. `file_bytes` (host) is
+ * still read for page heads (V1 level lengths, value-decoder headers),
+ * dictionary and compressed pages, and for chunks that fell back. */
+int pqgpu_batch_add_indexed_chunk(pqgpu_batch *b, const pqgpu_page_index *ix, int32_t ix_chunk,
+                                  const uint8_t *file_bytes, size_t file_len, const pqgpu_column_info *col,
+                                  int validate_crc, int32_t *chunk_id, pqgpu_error *err);
+int pqgpu_batch_add_indexed_file_chunk(pqgpu_batch *b, const pqgpu_page_index *ix, int32_t ix_chunk,
+                                       const pqgpu_file *f, int col, int validate_crc, int32_t *chunk_id,
+                                       pqgpu_error *err);
 
 /* Copy staged page bytes and descriptors to HBM (hipMemcpyAsync from
  * pinned memory) and allocate the outputs. */
@@ -269,6 +326,10 @@ int pqgpu_batch_kernel_bytes(const pqgpu_batch *b, int slot, int64_t *bytes);
  * callers that hold device pointers of a chunk result, e.g. when gathering
  * a row-group shard into one column: hipMemcpy, hipMemcpyDefault. */
 int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_error *err);
+/* Device memory on the library's runtime (hipMalloc, 256-byte aligned), e.g. for
+ * file bytes made resident for pqgpu_page_index_build (copy them with pqgpu_copy). */
+int pqgpu_dev_alloc(pqgpu_ctx *ctx, size_t bytes, void **out, pqgpu_error *err);
+void pqgpu_dev_free(pqgpu_ctx *ctx, void *p);
 
 /* ---- streaming row-group pipeline -------------------------------------
  * FileReader.readRowGroupData (chunk_reader.go:375-404) called for row group
@@ -282,7 +343,9 @@ typedef struct {
   int32_t depth;         /* row groups in flight (batches); >= 2 double-buffers, default 3 */
   int32_t threads;       /* host planner threads; 0 = depth */
   int32_t validate_crc;  /* WithCRC32Validation (file_reader.go:134-139) */
-  int32_t pad;
+  int32_t device_index;  /* 1: each row group's byte range is copied to the device once and its page
+                            headers walked (and checksummed) there (pqgpu_page_index_build);
+                            UNCOMPRESSED page bodies then reach the decoder device to device */
 } pqgpu_pipeline_opts;
 typedef struct {
   int64_t row_groups;      /* row groups returned so far */
@@ -296,6 +359,7 @@ typedef struct {
   double upload_ms;        /* host side of pqgpu_batch_upload (descriptors, pinned copy), summed */
   double h2d_ms;           /* GPU: upload enqueue .. done, summed over row groups */
   double decode_ms;        /* GPU: decode launches .. done, summed over row groups */
+  double index_ms;         /* device_index: byte-range copy + device page walk, summed (part of plan_ms) */
 } pqgpu_pipeline_stats;
 /* rgs / cols may be NULL for all row groups / all columns. */
 int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const int32_t *rgs, int32_t n_rgs, const int32_t *cols,

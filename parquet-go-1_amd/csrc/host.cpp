@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <functional>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -445,6 +446,11 @@ struct pqgpu_batch {
   bool dev_snappy = !(getenv("PQ_HOST_SNAPPY") && atoi(getenv("PQ_HOST_SNAPPY")) != 0);
   std::vector<DevSnappy> snappy;
   std::vector<uint8_t> pagebuf;  // the planner's copy of a device-decompressed page's head
+  // UNCOMPRESSED pages of chunks added from an on-device page index: the body is copied device to
+  // device from the resident file bytes (k_page_gather, at upload) instead of through the stage.
+  struct HostGather { uint64_t src, len; uint32_t page; };
+  std::vector<HostGather> gathers;
+  uint64_t o_gather = 0;
   uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
@@ -532,6 +538,7 @@ static int chunk_fail(pqgpu_batch *b, HostChunk &hc, int32_t id, int code, int p
   b->pages.resize(hc.first_page);
   while (!b->ba_delta.empty() && b->ba_delta.back().page >= hc.first_page) b->ba_delta.pop_back();
   while (!b->snappy.empty() && b->snappy.back().page >= hc.first_page) b->snappy.pop_back();
+  while (!b->gathers.empty() && b->gathers.back().page >= hc.first_page) b->gathers.pop_back();
   hc.num_pages = 0;
   return code;
 }
@@ -552,9 +559,13 @@ struct SnappyDefer { const uint8_t *blk = nullptr; int64_t len = 0, dlen = 0; };
 // With `defer` a SNAPPY block whose preamble gives the expected size is not decompressed here
 // (k_snappy does it; a corrupt body is found there); anything else decodes on the host, whose
 // error is the reference's.
+// With a page-index entry `ixe` (the on-device walk of this header) the CRC32 verdict comes from
+// k_page_crc, and with `direct` an UNCOMPRESSED block is not copied: *direct points at it in the
+// caller's file bytes (its body reaches the device through k_page_gather).
 static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *count, int32_t csize, int32_t usize,
                       int validate_crc, const PageHeader &ph, int32_t codec, std::vector<uint8_t> *out,
-                      int64_t skip_levels, std::string *msg, SnappyDefer *defer = nullptr) {
+                      int64_t skip_levels, std::string *msg, SnappyDefer *defer = nullptr,
+                      const PageIxEntry *ixe = nullptr, const uint8_t **direct = nullptr) {
   if (csize < 0 || usize < 0) { *msg = "invalid page data size"; return PQ_ERR_INVALID; }
   int64_t avail = *off >= flen ? 0 : flen - *off;
   int64_t take = std::min<int64_t>(csize, avail);
@@ -562,8 +573,14 @@ static int read_block(const uint8_t *file, int64_t flen, int64_t *off, int64_t *
   *off += take;
   *count += take;
   if (validate_crc && ph.has_crc) {
-    uint32_t sum = (uint32_t)crc32(0L, blk, (uInt)take);
-    if (sum != (uint32_t)ph.crc) { *msg = "CRC32 check failed"; return PQ_ERR_CRC; }
+    bool ok;
+    if (ixe && (ixe->flags & IXF_CRC_CHECKED)) ok = (ixe->flags & IXF_CRC_OK) != 0;
+    else ok = (uint32_t)crc32(0L, blk, (uInt)take) == (uint32_t)ph.crc;
+    if (!ok) { *msg = "CRC32 check failed"; return PQ_ERR_CRC; }
+  }
+  if (direct && codec == 0 && take == csize && usize == csize && skip_levels <= take) {
+    *direct = blk;
+    return PQ_OK;
   }
   // V2: the level bytes are copied raw, only the values part goes through the codec (page_v2.go:112-127)
   if (skip_levels > 0) {
@@ -712,8 +729,66 @@ static int init_values(const uint8_t *page, int64_t plen, int64_t vstart, uint8_
   return PQ_OK;
 }
 
+// A chunk's entries of an on-device page index (pagewalk.hip) and where its pages are resident.
+struct IxChunkView {
+  const PageIxEntry *e;  // page order
+  uint32_t n;
+  uint64_t dev;          // device address of file byte `file_off`
+  int64_t file_off;
+};
+
+static void ix_header(const PageIxEntry &x, PageHeader *ph) {
+  *ph = PageHeader();
+  ph->type = x.type;
+  ph->usize = x.usize;
+  ph->csize = x.csize;
+  ph->crc = x.crc;
+  ph->has_crc = x.flags & IXF_CRC;
+  ph->has_dph = x.flags & IXF_DPH;
+  ph->has_dict = x.flags & IXF_DICT;
+  ph->has_dph2 = x.flags & IXF_DPH2;
+  ph->dph = DataPageHeader{x.dph[0], x.dph[1], x.dph[2], x.dph[3]};
+  ph->dict = DictPageHeader{x.dict[0], x.dict[1]};
+  ph->dph2.num_values = x.dph2[0];
+  ph->dph2.num_nulls = x.dph2[1];
+  ph->dph2.num_rows = x.dph2[2];
+  ph->dph2.encoding = x.dph2[3];
+  ph->dph2.def_len = x.dph2[4];
+  ph->dph2.rep_len = x.dph2[5];
+  ph->dph2.is_compressed = x.flags & IXF_COMPRESSED;
+}
+
+// ---------------------------------------------------------------------------
+// On-device page index (pagewalk.hip)
+// ---------------------------------------------------------------------------
+struct pqgpu_page_index {
+  uint64_t dev = 0;        // device address of file byte `file_off`
+  int64_t file_off = 0, len = 0;
+  int validate_crc = 0;
+  std::vector<pqgpu_chunk_meta> metas;
+  std::vector<PageIxChunk> chunks;
+  std::vector<PageIxEntry> entries;  // grouped by chunk, page order
+  std::vector<uint32_t> first;       // [nchunks + 1] each chunk's entries
+  double walk_ms = 0;                // walk (+ checksums) on the device, incl. the table read-back
+};
+
+static void to_public(const PageIxEntry &x, pqgpu_page_header *o) {
+  memset(o, 0, sizeof(*o));
+  o->header_offset = x.hdr_off;
+  o->header_len = x.hdr_len;
+  o->type = x.type;
+  o->uncompressed_page_size = x.usize;
+  o->compressed_page_size = x.csize;
+  o->crc = x.crc;
+  o->flags = (int32_t)x.flags;
+  for (int k = 0; k < 4; k++) o->data_page[k] = x.dph[k];
+  for (int k = 0; k < 2; k++) o->dictionary_page[k] = x.dict[k];
+  for (int k = 0; k < 6; k++) o->data_page_v2[k] = x.dph2[k];
+}
+
 static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, const pqgpu_column_info *col,
-                          const pqgpu_chunk_meta *meta, int validate_crc, int32_t *chunk_id, pqgpu_error *err) {
+                          const pqgpu_chunk_meta *meta, int validate_crc, int32_t *chunk_id, pqgpu_error *err,
+                          const IxChunkView *ix = nullptr) {
   auto t0 = std::chrono::steady_clock::now();
   int32_t id = (int32_t)b->chunks.size();
   if (chunk_id) *chunk_id = id;
@@ -739,10 +814,20 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
   std::string msg;
   std::vector<uint8_t> block;
   double decomp_ms = 0;
+  uint32_t ixk = 0;  // next page-index entry
   while (meta->total_compressed_size - count > 0) {
     PageHeader ph;
     int64_t consumed = 0;
-    bool ok = off < flen && ParsePageHeader(file + off, flen - off, &ph, &consumed);
+    const PageIxEntry *ixe = nullptr;  // this header as the device walk decoded it
+    bool ok;
+    if (ix && ixk < ix->n && ix->e[ixk].hdr_off == off) {
+      ixe = &ix->e[ixk++];
+      ix_header(*ixe, &ph);
+      consumed = ixe->hdr_len;
+      ok = true;
+    } else {
+      ok = off < flen && ParsePageHeader(file + off, flen - off, &ph, &consumed);
+    }
     off += consumed;
     count += consumed;
     if (!ok) return chunk_fail(b, hc, id, PQ_ERR_THRIFT, -1, "thrift: invalid page header", err);
@@ -757,7 +842,8 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
                           "only Encoding_PLAIN and Encoding_PLAIN_DICTIONARY is supported for dict values encoder", err);
       block.clear();
       auto d0 = std::chrono::steady_clock::now();
-      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg);
+      int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg,
+                         nullptr, ixe);
       decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
       if (e) return chunk_fail(b, hc, id, e, -1, msg, err);
       hc.has_dict = true;
@@ -814,7 +900,10 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
     // plus the decoded head in pagebuf, extended on demand
     const uint8_t *pg = nullptr;
     int64_t plen = 0, raw_len = 0;
+    const uint8_t *direct = nullptr;  // resident UNCOMPRESSED block (page index): read in place
+    const uint8_t **want_direct = ixe ? &direct : nullptr;
     auto bind_page = [&]() {
+      if (direct) { pg = direct; plen = ph.csize; return; }
       if (!sd.blk) { pg = block.data(); plen = (int64_t)block.size(); return; }
       raw_len = (int64_t)block.size();
       plen = raw_len + sd.dlen;
@@ -850,7 +939,7 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       if (ph.dph.num_values < 0) return chunk_fail(b, hc, id, PQ_ERR_INVALID, pi, "negative NumValues in DATA_PAGE", err);
       auto d0 = std::chrono::steady_clock::now();
       int e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, 0, &msg,
-                         can_defer ? &sd : nullptr);
+                         can_defer ? &sd : nullptr, ixe, want_direct);
       if (!e) bind_page();
       decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
       if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
@@ -894,7 +983,7 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       int64_t levels = (int64_t)ph.dph2.rep_len + ph.dph2.def_len;
       auto d0 = std::chrono::steady_clock::now();
       e = read_block(file, flen, &off, &count, ph.csize, ph.usize, validate_crc, ph, meta->codec, &block, levels, &msg,
-                     can_defer ? &sd : nullptr);
+                     can_defer ? &sd : nullptr, ixe, want_direct);
       if (!e) bind_page();
       decomp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
       if (e) return chunk_fail(b, hc, id, e, pi, msg, err);
@@ -926,6 +1015,11 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
     if (sd.blk) {  // staged by stage_snappy(); k_snappy writes the page
       pd.flags |= PF_DEV_SNAPPY;
       pd.data = b->snappy.size() - 1;  // job index until upload
+    } else if (direct) {  // resident: k_page_gather copies the block at upload
+      pd.flags |= PF_DEV_GATHER;
+      pd.data = b->gathers.size();  // gather-job index until upload
+      b->gathers.push_back(pqgpu_batch::HostGather{ix->dev + (uint64_t)((direct - file) - ix->file_off),
+                                                    (uint64_t)plen, (uint32_t)b->pages.size()});
     } else {
       pd.data = stage_append(b, block.data(), (int64_t)block.size());  // stage offset until upload
     }
@@ -1259,6 +1353,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_dbg = take(64 * 8);
   b->o_ba_delta = take(b->ba_delta.size() * sizeof(BaDelta));
   b->o_snappy = take(b->snappy.size() * sizeof(SnappyJob));
+  b->o_gather = take(b->gathers.size() * sizeof(GatherJob));
   b->o_dblk = take(b->dblk_total * sizeof(DeltaBlk));
   b->o_dblk_sum = take(b->dblk_total * 8);
   b->o_dblk_base = take((uint64_t)np * 8);
@@ -1300,7 +1395,15 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     dec_off[k] = dec;
     dec = align_up(dec + align_up((uint64_t)b->snappy[k].raw_len + b->snappy[k].dlen, 16) + 64, 256);
   }
-  const size_t dsz = (size_t)(dec_base + dec);
+  // then the resident UNCOMPRESSED pages k_page_gather copies in (same layout)
+  const uint64_t gat_base = align_up(dec_base + dec, 256);
+  std::vector<uint64_t> gat_off(b->gathers.size());
+  uint64_t gat = 0;
+  for (size_t k = 0; k < b->gathers.size(); k++) {
+    gat_off[k] = gat;
+    gat = align_up(gat + align_up(b->gathers[k].len, 16) + 64, 256);
+  }
+  const size_t dsz = (size_t)(gat_base + gat);
   if (dsz > b->d_stage_cap) {
     if (b->d_stage) (void)hipFree(b->d_stage);
     b->d_stage = nullptr;
@@ -1391,9 +1494,20 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                         (uint64_t)(b->d_stage + dec_base + dec_off[k]), j.comp_len - j.vlen, j.raw_len, j.dlen,
                         pd.chunk, pd.page_in_chunk, 0};
   }
+  std::vector<GatherJob> gjobs(b->gathers.size());
+  for (size_t k = 0; k < gjobs.size(); k++)
+    gjobs[k] = GatherJob{b->gathers[k].src, (uint64_t)(b->d_stage + gat_base + gat_off[k]), b->gathers[k].len};
   std::vector<PageDesc> pages = b->pages;
-  for (auto &pd : pages) pd.data = (pd.flags & PF_DEV_SNAPPY) ? jobs[pd.data].dst : (uint64_t)(b->d_stage + pd.data);
+  for (auto &pd : pages)
+    pd.data = (pd.flags & PF_DEV_SNAPPY)   ? jobs[pd.data].dst
+              : (pd.flags & PF_DEV_GATHER) ? gjobs[pd.data].dst
+                                           : (uint64_t)(b->d_stage + pd.data);
   HIPCHECK(hipMemcpyAsync(A + b->o_snappy, jobs.data(), jobs.size() * sizeof(SnappyJob), hipMemcpyHostToDevice, s), err);
+  if (!gjobs.empty()) {
+    HIPCHECK(hipMemcpyAsync(A + b->o_gather, gjobs.data(), gjobs.size() * sizeof(GatherJob), hipMemcpyHostToDevice, s),
+             err);
+    HIPCHECK(launch_page_gather((const GatherJob *)(A + b->o_gather), (uint32_t)gjobs.size(), s), err);
+  }
   auto up = [&](uint64_t o, const void *src, size_t n) -> hipError_t {
     if (!n) return hipSuccess;
     return hipMemcpyAsync(A + o, src, n, hipMemcpyHostToDevice, s);
@@ -1896,6 +2010,8 @@ int pqgpu_file_open(const uint8_t *buf, size_t len, pqgpu_file **out, pqgpu_erro
 }
 
 void pqgpu_file_close(pqgpu_file *f) { delete f; }
+const uint8_t *pqgpu_file_bytes(const pqgpu_file *f) { return f ? f->buf : nullptr; }
+size_t pqgpu_file_len(const pqgpu_file *f) { return f ? (size_t)f->len : 0; }
 int pqgpu_file_num_row_groups(const pqgpu_file *f) { return (int)f->meta.row_groups.size(); }
 int pqgpu_file_num_columns(const pqgpu_file *f) { return (int)f->meta.leaves.size(); }
 int64_t pqgpu_file_row_group_num_rows(const pqgpu_file *f, int rg) {
@@ -1993,6 +2109,7 @@ int pqgpu_batch_reset(pqgpu_batch *b) {
   b->pages.clear();
   b->ba_delta.clear();
   b->snappy.clear();
+  b->gathers.clear();
   b->stage.clear();
   b->uploaded = b->decoded = false;
   b->force_serial = spec_disabled();
@@ -2032,6 +2149,177 @@ int pqgpu_batch_add_file_chunk(pqgpu_batch *b, const pqgpu_file *f, int rg, int 
   // the chunk's staged bytes are about its compressed size (SNAPPY data pages stay compressed)
   b->stage.reserve(b->stage.size() + (size_t)std::max<int64_t>(cm.total_compressed_size, 0) + 4096);
   return add_chunk_impl(b, f->buf, f->len, &ci, &cm, validate_crc, chunk_id, err);
+}
+
+int pqgpu_parse_page_header(const uint8_t *buf, size_t len, pqgpu_page_header *out, int64_t *consumed) {
+  PageHeader ph;
+  int64_t c = 0;
+  const bool ok = buf && ParsePageHeader(buf, (int64_t)len, &ph, &c);
+  if (consumed) *consumed = c;
+  if (!ok) return PQ_ERR_THRIFT;
+  PageIxEntry x{};
+  x.hdr_len = (int32_t)c;
+  x.type = ph.type; x.usize = ph.usize; x.csize = ph.csize; x.crc = ph.crc;
+  x.flags = (ph.has_crc ? IXF_CRC : 0) | (ph.has_dph ? IXF_DPH : 0) | (ph.has_dict ? IXF_DICT : 0) |
+            (ph.has_dph2 ? IXF_DPH2 : 0) | (ph.dph2.is_compressed ? IXF_COMPRESSED : 0);
+  x.dph[0] = ph.dph.num_values; x.dph[1] = ph.dph.encoding; x.dph[2] = ph.dph.def_enc; x.dph[3] = ph.dph.rep_enc;
+  x.dict[0] = ph.dict.num_values; x.dict[1] = ph.dict.encoding;
+  x.dph2[0] = ph.dph2.num_values; x.dph2[1] = ph.dph2.num_nulls; x.dph2[2] = ph.dph2.num_rows;
+  x.dph2[3] = ph.dph2.encoding; x.dph2[4] = ph.dph2.def_len; x.dph2[5] = ph.dph2.rep_len;
+  if (out) to_public(x, out);
+  return PQ_OK;
+}
+
+int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_offset, int64_t len,
+                           const pqgpu_chunk_meta *metas, int32_t n_chunks, int32_t validate_crc, void *stream,
+                           pqgpu_page_index **out, pqgpu_error *err) {
+  clear_err(err);
+  if (!ctx || !out || (n_chunks > 0 && (!metas || !dev_bytes)) || n_chunks < 0 || len < 0 ||
+      ((uintptr_t)dev_bytes & 15)) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "page index: bad argument (dev_bytes must be 16-byte aligned)");
+    return PQ_ERR_ARG;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHECK(hipSetDevice(ctx->device), err);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  auto ix = std::make_unique<pqgpu_page_index>();
+  ix->dev = (uint64_t)(uintptr_t)dev_bytes;
+  ix->file_off = file_offset;
+  ix->len = len;
+  ix->validate_crc = validate_crc;
+  ix->metas.assign(metas, metas + n_chunks);
+  ix->chunks.resize(n_chunks);
+  uint64_t cap = 4096;
+  for (int32_t c = 0; c < n_chunks; c++) {
+    const pqgpu_chunk_meta &m = metas[c];
+    PageIxChunk &k = ix->chunks[c];
+    memset(&k, 0, sizeof(k));
+    k.start = m.dictionary_page_offset >= 0 ? m.dictionary_page_offset : m.data_page_offset;
+    k.data_off = m.data_page_offset;
+    k.dict_off = m.dictionary_page_offset;
+    k.total = m.has_file_path ? 0 : m.total_compressed_size;  // a chunk in another file: host error path
+    cap += 64 + (uint64_t)std::max<int64_t>(k.total, 0) / 4096;
+  }
+  if (n_chunks == 0) { *out = ix.release(); return PQ_OK; }
+  // table capacity: a page per 4 KiB plus 64 per chunk; a walk that outgrows it is rerun larger.
+  // The chunk table and the results travel through pinned host memory (DMA copies): a small
+  // pageable H2D copy may be written by the CPU through the BAR and not yet be visible to a kernel
+  // launched right behind it on another queue.
+  struct Pinned {
+    void *p = nullptr;
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+  } hc_tab;
+  const size_t ch_bytes = (size_t)n_chunks * sizeof(PageIxChunk);
+  HIPCHECK(hipHostMalloc(&hc_tab.p, ch_bytes + 64, hipHostMallocDefault), err);
+  uint32_t *h_n = (uint32_t *)((uint8_t *)hc_tab.p + ch_bytes);
+  uint32_t n = 0;
+  for (int attempt = 0;; attempt++) {
+    cap = std::min<uint64_t>(cap, 1u << 26);
+    memcpy(hc_tab.p, ix->chunks.data(), ch_bytes);
+    void *d = nullptr;
+    const size_t bytes = 256 + ch_bytes + cap * sizeof(PageIxEntry);
+    HIPCHECK(hipMallocAsync(&d, bytes, s), err);
+    uint8_t *D = (uint8_t *)d;
+    uint32_t *d_n = (uint32_t *)D;
+    PageIxChunk *d_ch = (PageIxChunk *)(D + 256);
+    PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + ch_bytes);
+    hipError_t he = hipMemsetAsync(d_n, 0, 4, s);
+    if (he == hipSuccess) he = hipMemcpyAsync(d_ch, hc_tab.p, ch_bytes, hipMemcpyHostToDevice, s);
+    if (he == hipSuccess)
+      he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, d_ch, (uint32_t)n_chunks, d_tab, d_n,
+                            (uint32_t)cap, validate_crc, s);
+    if (he == hipSuccess) he = hipMemcpyAsync(h_n, d_n, 4, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    n = *h_n;
+    const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < 3;
+    if (he == hipSuccess && !grow) {
+      const size_t eb = (size_t)std::min<uint64_t>(n, cap) * sizeof(PageIxEntry);
+      Pinned he_tab;
+      he = hipHostMalloc(&he_tab.p, eb + ch_bytes + 64, hipHostMallocDefault);
+      if (he == hipSuccess) he = hipMemcpyAsync(he_tab.p, d_tab, eb, hipMemcpyDeviceToHost, s);
+      if (he == hipSuccess)
+        he = hipMemcpyAsync((uint8_t *)he_tab.p + eb, d_ch, ch_bytes, hipMemcpyDeviceToHost, s);
+      if (he == hipSuccess) he = hipStreamSynchronize(s);
+      if (he == hipSuccess) {
+        ix->entries.resize(eb / sizeof(PageIxEntry));
+        memcpy(ix->entries.data(), he_tab.p, eb);
+        memcpy(ix->chunks.data(), (uint8_t *)he_tab.p + eb, ch_bytes);
+      }
+    }
+    (void)hipFreeAsync(d, s);
+    HIPCHECK(he, err);
+    if (!grow) break;
+    cap = (uint64_t)n * 2 + 4096;
+  }
+  if (getenv("PQ_IX_DEBUG")) {
+    fprintf(stderr, "[ix] n=%u cap=%llu\n", n, (unsigned long long)cap);
+    for (int32_t c = 0; c < n_chunks; c++)
+      fprintf(stderr, "[ix] chunk %d start %lld total %lld status %u npages %u fail %u\n", c,
+              (long long)ix->chunks[c].start, (long long)ix->chunks[c].total, ix->chunks[c].status,
+              ix->chunks[c].npages, ix->chunks[c].fail_page);
+    for (const auto &x : ix->entries)
+      fprintf(stderr, "[ix]   e chunk %u seq %u off %lld type %d cs %d\n", x.chunk, x.seq, (long long)x.hdr_off, x.type, x.csize);
+  }
+  // group by chunk in page order (a chunk's entries were reserved in increasing order)
+  std::vector<PageIxEntry> &e = ix->entries;
+  std::stable_sort(e.begin(), e.end(), [](const PageIxEntry &a, const PageIxEntry &b) {
+    return a.chunk != b.chunk ? a.chunk < b.chunk : a.seq < b.seq;
+  });
+  ix->first.assign(n_chunks + 1, 0);
+  for (const auto &x : e) ix->first[x.chunk + 1]++;
+  for (int32_t c = 0; c < n_chunks; c++) ix->first[c + 1] += ix->first[c];
+  for (int32_t c = 0; c < n_chunks; c++)  // a chunk that fell back mid-walk keeps no entries
+    if (ix->chunks[c].status != IX_OK || ix->first[c + 1] - ix->first[c] != ix->chunks[c].npages)
+      ix->chunks[c].status = IX_FALLBACK;
+  ix->walk_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = ix.release();
+  return PQ_OK;
+}
+
+int pqgpu_page_index_chunk(const pqgpu_page_index *ix, int32_t chunk, int32_t *num_pages, int32_t *status) {
+  if (!ix || chunk < 0 || chunk >= (int32_t)ix->chunks.size()) return PQ_ERR_ARG;
+  const bool ok = ix->chunks[chunk].status == IX_OK;
+  if (num_pages) *num_pages = ok ? (int32_t)(ix->first[chunk + 1] - ix->first[chunk]) : 0;
+  if (status) *status = ok ? PQGPU_IX_OK : PQGPU_IX_FALLBACK;
+  return PQ_OK;
+}
+
+int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, pqgpu_page_header *out) {
+  int32_t np = 0, st = 0;
+  if (pqgpu_page_index_chunk(ix, chunk, &np, &st) || k < 0 || k >= np || !out) return PQ_ERR_ARG;
+  to_public(ix->entries[ix->first[chunk] + k], out);
+  return PQ_OK;
+}
+
+double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix) { return ix ? ix->walk_ms : 0.0; }
+
+void pqgpu_page_index_destroy(pqgpu_page_index *ix) { delete ix; }
+
+int pqgpu_batch_add_indexed_chunk(pqgpu_batch *b, const pqgpu_page_index *ix, int32_t ix_chunk,
+                                  const uint8_t *file_bytes, size_t file_len, const pqgpu_column_info *col,
+                                  int validate_crc, int32_t *chunk_id, pqgpu_error *err) {
+  if (!b || !ix || !file_bytes || !col || ix_chunk < 0 || ix_chunk >= (int32_t)ix->chunks.size()) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "null argument or chunk out of range");
+    return PQ_ERR_ARG;
+  }
+  const pqgpu_chunk_meta &cm = ix->metas[ix_chunk];
+  b->stage.reserve(b->stage.size() + 4096);
+  if (ix->chunks[ix_chunk].status != IX_OK)  // the walk did not take it: the host walks the chunk
+    return add_chunk_impl(b, file_bytes, (int64_t)file_len, col, &cm, validate_crc, chunk_id, err);
+  IxChunkView v{ix->entries.data() + ix->first[ix_chunk], ix->first[ix_chunk + 1] - ix->first[ix_chunk], ix->dev,
+                ix->file_off};
+  return add_chunk_impl(b, file_bytes, (int64_t)file_len, col, &cm, validate_crc, chunk_id, err, &v);
+}
+
+int pqgpu_batch_add_indexed_file_chunk(pqgpu_batch *b, const pqgpu_page_index *ix, int32_t ix_chunk,
+                                       const pqgpu_file *f, int col, int validate_crc, int32_t *chunk_id,
+                                       pqgpu_error *err) {
+  pqgpu_column_info ci;
+  if (!f || pqgpu_file_column(f, col, &ci)) {
+    set_err(err, PQ_ERR_ARG, -1, -1, "column out of range");
+    return PQ_ERR_ARG;
+  }
+  return pqgpu_batch_add_indexed_chunk(b, ix, ix_chunk, f->buf, f->len, &ci, validate_crc, chunk_id, err);
 }
 
 #define NEED_CTX(b, err)                                                              \
@@ -2183,6 +2471,21 @@ int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t id, void *values, int32
   HIPCHECK(cp(validity, r.validity, (size_t)((r.num_slots + 31) / 32) * 4), err);
   HIPCHECK(cp(list_offsets, r.list_offsets, r.list_offsets ? (size_t)(r.num_records + 1) * 4 : 0), err);
   return e;
+}
+
+int pqgpu_dev_alloc(pqgpu_ctx *ctx, size_t bytes, void **out, pqgpu_error *err) {
+  clear_err(err);
+  if (!ctx || !out) { set_err(err, PQ_ERR_ARG, -1, -1, "null argument"); return PQ_ERR_ARG; }
+  *out = nullptr;
+  HIPCHECK(hipSetDevice(ctx->device), err);
+  HIPCHECK(hipMalloc(out, std::max<size_t>(bytes, 1)), err);
+  return PQ_OK;
+}
+
+void pqgpu_dev_free(pqgpu_ctx *ctx, void *p) {
+  if (!ctx || !p) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipFree(p);
 }
 
 int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_error *err) {

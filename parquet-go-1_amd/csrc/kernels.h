@@ -99,6 +99,12 @@ hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t 
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // walk + sums + prefix
+// on-device page index (pagewalk.hip): header walk of every chunk (+ CRC32 of every checksummed
+// block), and the upload-time gather of resident UNCOMPRESSED page bodies
+hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, PageIxChunk *chunks, uint32_t nchunks,
+                            PageIxEntry *table, uint32_t *table_n, uint32_t table_cap, int validate_crc,
+                            hipStream_t s);
+hipError_t launch_page_gather(const GatherJob *jobs, uint32_t njobs, hipStream_t s);
 
 // Names of the kernels, for the timing hook.
 extern const char *kValuesKernelName;

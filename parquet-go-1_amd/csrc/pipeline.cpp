@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -41,6 +42,9 @@ struct Slot {
   int64_t index = -1;  // row-group position in the pipeline's list
   int rc = PQ_OK;      // first launch error (upload / decode)
   pqgpu_error err{};
+  // device_index: the row group's byte range, staged in pinned memory and resident on the device
+  void *h_raw = nullptr, *d_raw = nullptr;
+  size_t raw_cap = 0;
 };
 
 void set_err(pqgpu_error *e, int code, const char *msg) {
@@ -57,7 +61,7 @@ struct pqgpu_pipeline {
   pqgpu_ctx *ctx = nullptr;
   const pqgpu_file *f = nullptr;
   std::vector<int32_t> rgs, cols;
-  int validate_crc = 0;
+  int validate_crc = 0, device_index = 0;
   std::vector<Slot> slots;
   std::vector<std::thread> workers;
   std::mutex m;
@@ -67,6 +71,42 @@ struct pqgpu_pipeline {
   clk::time_point t0;
   pqgpu_pipeline_stats st{};
 };
+
+// device_index: copy the selected chunks' byte range of row group `rg` to the slot's device buffer
+// (through its pinned staging buffer) and walk their page headers there. nullptr: walk on the host.
+static pqgpu_page_index *index_row_group(pqgpu_pipeline *p, Slot *sl, int32_t rg) {
+  std::vector<pqgpu_chunk_meta> metas(p->cols.size());
+  int64_t lo = INT64_MAX, hi = 0;
+  const int64_t flen = (int64_t)pqgpu_file_len(p->f);
+  for (size_t k = 0; k < p->cols.size(); k++) {
+    pqgpu_error e;
+    if (pqgpu_file_chunk_meta(p->f, rg, p->cols[k], &metas[k], &e)) return nullptr;  // the host path reports it
+    const pqgpu_chunk_meta &m = metas[k];
+    const int64_t st = m.dictionary_page_offset >= 0 ? m.dictionary_page_offset : m.data_page_offset;
+    lo = std::min(lo, std::max<int64_t>(st, 0));
+    hi = std::max(hi, std::min(flen, st + std::max<int64_t>(m.total_compressed_size, 0)));
+  }
+  if (lo >= hi) return nullptr;
+  const size_t n = (size_t)(hi - lo);
+  if (n + 64 > sl->raw_cap) {
+    if (sl->h_raw) (void)hipHostFree(sl->h_raw);
+    if (sl->d_raw) (void)hipFree(sl->d_raw);
+    sl->h_raw = sl->d_raw = nullptr;
+    sl->raw_cap = 0;
+    const size_t cap = n + n / 8 + 4096;
+    if (hipHostMalloc(&sl->h_raw, cap, hipHostMallocDefault) != hipSuccess || hipMalloc(&sl->d_raw, cap) != hipSuccess)
+      return nullptr;
+    sl->raw_cap = cap;
+  }
+  memcpy(sl->h_raw, pqgpu_file_bytes(p->f) + lo, n);
+  if (hipMemcpyAsync(sl->d_raw, sl->h_raw, n, hipMemcpyHostToDevice, sl->s) != hipSuccess) return nullptr;
+  pqgpu_page_index *ix = nullptr;
+  pqgpu_error e;
+  if (pqgpu_page_index_build(p->ctx, sl->d_raw, lo, (int64_t)n, metas.data(), (int32_t)metas.size(), p->validate_crc,
+                             sl->s, &ix, &e))
+    return nullptr;
+  return ix;
+}
 
 static void worker(pqgpu_pipeline *p) {
   (void)hipSetDevice(p->ctx->device);
@@ -90,16 +130,23 @@ static void worker(pqgpu_pipeline *p) {
     pqgpu_batch_reset(sl->b);
     sl->rc = PQ_OK;
     memset(&sl->err, 0, sizeof(sl->err));
-    for (int32_t c : p->cols) {
+    const int32_t rg = p->rgs[(size_t)i];
+    pqgpu_page_index *ix = p->device_index ? index_row_group(p, sl, rg) : nullptr;
+    const double ixms = ix ? ms_since(tp) : 0.0;
+    for (size_t k = 0; k < p->cols.size(); k++) {
       int32_t id;
       pqgpu_error e;
-      (void)pqgpu_batch_add_file_chunk(sl->b, p->f, p->rgs[(size_t)i], c, p->validate_crc, &id, &e);  // errors stay per chunk
+      if (ix)  // page headers (and checksums) walked on the device; chunks it did not take fall back
+        (void)pqgpu_batch_add_indexed_file_chunk(sl->b, ix, (int32_t)k, p->f, p->cols[k], p->validate_crc, &id, &e);
+      else
+        (void)pqgpu_batch_add_file_chunk(sl->b, p->f, rg, p->cols[k], p->validate_crc, &id, &e);  // errors stay per chunk
     }
     const double plan = ms_since(tp);
     const auto tu = clk::now();
     (void)hipEventRecord(sl->e0, sl->s);
-    int rc = pqgpu_batch_upload(sl->b, sl->s, &sl->err);
+    int rc = pqgpu_batch_upload(sl->b, sl->s, &sl->err);  // gathers resident pages; returns when done
     const double up = ms_since(tu);
+    pqgpu_page_index_destroy(ix);
     (void)hipEventRecord(sl->e1, sl->s);
     if (!rc) rc = pqgpu_batch_decode(sl->b, sl->s, &sl->err);
     (void)hipEventRecord(sl->e2, sl->s);
@@ -108,6 +155,7 @@ static void worker(pqgpu_pipeline *p) {
       sl->rc = rc;
       sl->state = LAUNCHED;
       p->st.plan_ms += plan;
+      p->st.index_ms += ixms;
       p->st.upload_ms += up;
     }
     p->cv.notify_all();
@@ -128,6 +176,8 @@ static void destroy(pqgpu_pipeline *p) {
     if (sl.e0) (void)hipEventDestroy(sl.e0);
     if (sl.e1) (void)hipEventDestroy(sl.e1);
     if (sl.e2) (void)hipEventDestroy(sl.e2);
+    if (sl.h_raw) (void)hipHostFree(sl.h_raw);
+    if (sl.d_raw) (void)hipFree(sl.d_raw);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
   delete p;
@@ -154,6 +204,7 @@ extern "C" int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const 
   const int depth = opts && opts->depth > 0 ? opts->depth : 3;
   const int threads = opts && opts->threads > 0 ? opts->threads : depth;
   p->validate_crc = opts ? opts->validate_crc : 0;
+  p->device_index = opts ? opts->device_index : 0;
   if (hipSetDevice(ctx->device) != hipSuccess) { delete p; set_err(err, PQ_ERR_HIP, "hipSetDevice failed"); return PQ_ERR_HIP; }
   p->slots.resize((size_t)depth);
   for (auto &sl : p->slots) {

@@ -46,6 +46,7 @@ enum : uint16_t {
   PF_DELTA_SLOW = 16,// DELTA page outside the tiled pipeline's shapes (miniblock not a multiple of 8
                      // values, block size not dividing kDeltaTileVals, > 8 miniblocks): exact scalar path
   PF_DEV_SNAPPY = 32,// host only: `data` is an offset into the device decompression region (k_snappy)
+  PF_DEV_GATHER = 64,// host only: `data` is a gather-job index (page body copied from resident file bytes)
 };
 
 // Error staging key (64 bit, smaller = reported first):
@@ -187,6 +188,42 @@ struct SnappyJob {       // 48 B
 };
 constexpr uint32_t kSnappyRing = 16384;  // LDS window of the most recent output bytes per page
 enum : uint32_t { ST_DECOMP = 4 };       // err_key stage of a device decompression error
+
+// On-device page index (pagewalk.hip): readPages' header loop
+// (chunk_reader.go:182-263) over column-chunk bytes resident in HBM, the Thrift compact decode of
+// every PageHeader (readThrift helpers.go:103-109) and the CRC32 check of readPageBlock
+// (chunk_reader.go:173-177). The walk covers the valid case only: anything the walk cannot take
+// (a Thrift error, a negative size, a page reaching past the buffer, a full table) marks the chunk
+// IX_FALLBACK and the host planner walks that chunk itself, so every error keeps the host's
+// (i.e. the reference's) class, message and position.
+enum : uint32_t { IX_OK = 0, IX_FALLBACK = 1 };
+struct PageIxChunk {     // 48 B: walk input (start .. total) and result (status, npages)
+  int64_t start;         // file offset of the first header (dictionary page offset, else data page offset)
+  int64_t data_off;      // DataPageOffset: the seek target after a dictionary page (chunk_reader.go:220-226)
+  int64_t dict_off;      // DictionaryPageOffset, -1 when unset
+  int64_t total;         // TotalCompressedSize: the loop bound (chunk_reader.go:190)
+  uint32_t status;       // IX_OK / IX_FALLBACK
+  uint32_t npages;       // entries the walk wrote for this chunk
+  uint32_t fail_page;    // IX_FALLBACK: the page the walk stopped at
+  uint32_t pad;
+};
+// Entry flags
+enum : uint32_t { IXF_CRC = 1, IXF_DPH = 2, IXF_DICT = 4, IXF_DPH2 = 8, IXF_COMPRESSED = 16,
+                  IXF_CRC_CHECKED = 32, IXF_CRC_OK = 64 };
+struct PageIxEntry {     // 96 B: one PageHeader (format.h) and where it lies
+  int64_t hdr_off;       // file offset of the header
+  int32_t hdr_len;       // Thrift bytes consumed
+  int32_t type, usize, csize, crc;
+  uint32_t flags;        // IXF_*
+  int32_t dph[4];        // DataPageHeader: num_values, encoding, def_enc, rep_enc
+  int32_t dict[2];       // DictionaryPageHeader: num_values, encoding
+  int32_t dph2[6];       // DataPageHeaderV2: num_values, num_nulls, num_rows, encoding, def_len, rep_len
+  uint32_t chunk, seq;   // walk input chunk, page position in its chunk (dictionary page included)
+  uint32_t pad[2];
+};
+// Device-to-device copy of an UNCOMPRESSED page body from the resident file bytes into the
+// batch's page region (16-B aligned, 64 zero bytes after it), done once at upload.
+struct GatherJob { uint64_t src, dst, len; };
 
 struct WorkItem {        // 16 B
   uint32_t page;         // global page index

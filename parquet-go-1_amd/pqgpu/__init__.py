@@ -81,16 +81,33 @@ class BatchStats(ctypes.Structure):
                 ("snappy_pages", ctypes.c_int64), ("snappy_kernel_bytes", ctypes.c_int64)]
 
 
+class PageHeader(ctypes.Structure):
+    """pqgpu_page_header: one PageHeader as the on-device walk (or the host) decoded it."""
+    _fields_ = [("header_offset", ctypes.c_int64), ("header_len", ctypes.c_int32), ("type", ctypes.c_int32),
+                ("uncompressed_page_size", ctypes.c_int32), ("compressed_page_size", ctypes.c_int32),
+                ("crc", ctypes.c_int32), ("flags", ctypes.c_int32), ("data_page", ctypes.c_int32 * 4),
+                ("dictionary_page", ctypes.c_int32 * 2), ("data_page_v2", ctypes.c_int32 * 6)]
+
+    def key(self):
+        """Every decoded field (flags without the CRC verdict bits), for comparisons."""
+        return (self.header_len, self.type, self.uncompressed_page_size, self.compressed_page_size, self.crc,
+                self.flags & 31, tuple(self.data_page), tuple(self.dictionary_page), tuple(self.data_page_v2))
+
+
+PH_CRC, PH_CRC_CHECKED, PH_CRC_OK = 1, 32, 64
+IX_OK, IX_FALLBACK = 0, 1
+
+
 class PipelineOpts(ctypes.Structure):
     _fields_ = [("depth", ctypes.c_int32), ("threads", ctypes.c_int32), ("validate_crc", ctypes.c_int32),
-                ("pad", ctypes.c_int32)]
+                ("device_index", ctypes.c_int32)]
 
 
 class PipelineStats(ctypes.Structure):
     _fields_ = [("row_groups", ctypes.c_int64), ("rows", ctypes.c_int64), ("chunks", ctypes.c_int64),
                 ("failed_chunks", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
                 ("wall_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
-                ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double)]
+                ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("index_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -98,7 +115,7 @@ class PipelineStats(ctypes.Structure):
 
 _LIB = None
 TIMER_SLOTS = 16  # PQGPU_TIMER_SLOTS
-ABI_VERSION = 4  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+ABI_VERSION = 5  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -108,7 +125,9 @@ _EXPORTS = [
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
     "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
     "pqgpu_copy", "pqgpu_pipeline_create", "pqgpu_pipeline_next", "pqgpu_pipeline_release", "pqgpu_pipeline_stats_get",
-    "pqgpu_pipeline_destroy", "pqgpu_batch_copy_nested",
+    "pqgpu_pipeline_destroy", "pqgpu_batch_copy_nested", "pqgpu_page_index_build", "pqgpu_page_index_chunk",
+    "pqgpu_page_index_page", "pqgpu_page_index_walk_ms", "pqgpu_page_index_destroy", "pqgpu_parse_page_header",
+    "pqgpu_batch_add_indexed_chunk", "pqgpu_batch_add_indexed_file_chunk", "pqgpu_dev_alloc", "pqgpu_dev_free",
 ]
 
 
@@ -165,6 +184,21 @@ def lib():
         "pqgpu_pipeline_release": ([P, P], ctypes.c_int),
         "pqgpu_pipeline_stats_get": ([P, ctypes.POINTER(PipelineStats)], ctypes.c_int),
         "pqgpu_pipeline_destroy": ([P], None),
+        "pqgpu_page_index_build": ([P, P, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ChunkMeta), ctypes.c_int32,
+                                    ctypes.c_int32, P, ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_page_index_chunk": ([P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)],
+                                   ctypes.c_int),
+        "pqgpu_page_index_page": ([P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(PageHeader)], ctypes.c_int),
+        "pqgpu_page_index_walk_ms": ([P], ctypes.c_double),
+        "pqgpu_page_index_destroy": ([P], None),
+        "pqgpu_parse_page_header": ([P, ctypes.c_size_t, ctypes.POINTER(PageHeader), ctypes.POINTER(ctypes.c_int64)],
+                                    ctypes.c_int),
+        "pqgpu_batch_add_indexed_chunk": ([P, P, ctypes.c_int32, P, ctypes.c_size_t, ctypes.POINTER(ColumnInfo),
+                                           ctypes.c_int, ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
+        "pqgpu_batch_add_indexed_file_chunk": ([P, P, ctypes.c_int32, P, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
+        "pqgpu_dev_alloc": ([P, ctypes.c_size_t, ctypes.POINTER(P), E], ctypes.c_int),
+        "pqgpu_dev_free": ([P, P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -268,6 +302,11 @@ class File:
             raise IndexError(col)
         return ci
 
+    def chunk_meta(self, rg, col):
+        m, err = ChunkMeta(), Error()
+        _check(lib().pqgpu_file_chunk_meta(self._h, rg, col, ctypes.byref(m), ctypes.byref(err)), err)
+        return m
+
     def column_paths(self):
         return [self.column(i).path.decode() for i in range(self.num_columns)]
 
@@ -343,6 +382,17 @@ class Batch:
         err = Error()
         rc = lib().pqgpu_batch_add_file_chunk(self._h, f._h, rg, col, int(validate_crc), ctypes.byref(cid),
                                               ctypes.byref(err))
+        self._files.append(f)
+        self._infos.append(f.column(col))
+        return cid.value, (DecodeError(err) if rc else None)
+
+    def add_indexed_chunk(self, ix, k, f, col, validate_crc=False):
+        """add_file_chunk for chunk k of a PageIndex (page headers and CRC verdicts from the device
+        walk, UNCOMPRESSED page bodies gathered from the resident bytes at upload)."""
+        cid = ctypes.c_int32(-1)
+        err = Error()
+        rc = lib().pqgpu_batch_add_indexed_file_chunk(self._h, ix._h, k, f._h, col, int(validate_crc),
+                                                      ctypes.byref(cid), ctypes.byref(err))
         self._files.append(f)
         self._infos.append(f.column(col))
         return cid.value, (DecodeError(err) if rc else None)
@@ -496,13 +546,14 @@ class Pipeline:
     (row_group, batch, error or None) in row-group order; a yielded batch is released when the
     iteration moves on. Chunk ids in a batch follow `cols`."""
 
-    def __init__(self, ctx, f, row_groups=None, cols=None, depth=3, threads=0, validate_crc=False):
+    def __init__(self, ctx, f, row_groups=None, cols=None, depth=3, threads=0, validate_crc=False,
+                 device_index=False):
         self.ctx, self.f = ctx, f
         self.cols = list(range(f.num_columns)) if cols is None else list(cols)
         self._infos = [f.column(c) for c in self.cols]
         rgs = None if row_groups is None else (ctypes.c_int32 * len(row_groups))(*row_groups)
         cs = (ctypes.c_int32 * len(self.cols))(*self.cols)
-        opts = PipelineOpts(depth, threads, int(validate_crc), 0)
+        opts = PipelineOpts(depth, threads, int(validate_crc), int(device_index))
         self._h = ctypes.c_void_p()
         err = Error()
         _check(lib().pqgpu_pipeline_create(ctx._h, f._h, rgs, len(row_groups) if row_groups is not None else 0, cs,
@@ -537,6 +588,98 @@ class Pipeline:
             self._release()
             lib().pqgpu_pipeline_destroy(self._h)
             self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBuffer:
+    """Device memory on libpqgpu's runtime holding `data` (pqgpu_dev_alloc + pqgpu_copy)."""
+
+    def __init__(self, ctx, data, pad=64):
+        self.ctx, self.size = ctx, len(data)
+        self.ptr = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_dev_alloc(ctx._h, self.size + pad, ctypes.byref(self.ptr), ctypes.byref(err)), err)
+        if self.size:
+            src = ctypes.create_string_buffer(bytes(data), self.size)
+            copy(ctx, self.ptr.value, ctypes.addressof(src), self.size)
+
+    def close(self):
+        if self.ptr and self.ptr.value:
+            lib().pqgpu_dev_free(self.ctx._h, self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def parse_page_header(buf):
+    """The host's PageHeader decode: (PageHeader, consumed) or (None, consumed) on a Thrift error."""
+    h, n = PageHeader(), ctypes.c_int64()
+    src = ctypes.create_string_buffer(bytes(buf), len(buf))
+    rc = lib().pqgpu_parse_page_header(ctypes.addressof(src), len(buf), ctypes.byref(h), ctypes.byref(n))
+    return (None if rc else h), n.value
+
+
+class PageIndex:
+    """pqgpu_page_index: the page headers of column chunks walked on the GPU over resident file bytes
+    (readPages' header loop, chunk_reader.go:182-263, and readPageBlock's CRC32 check, :173-177)."""
+
+    def __init__(self, ctx, dev_ptr, file_offset, length, metas, validate_crc=False, keep=None):
+        self.ctx, self._keep = ctx, keep
+        self.metas = list(metas)
+        arr = (ChunkMeta * max(len(self.metas), 1))(*self.metas)
+        self._h = ctypes.c_void_p()
+        err = Error()
+        _check(lib().pqgpu_page_index_build(ctx._h, ctypes.c_void_p(dev_ptr), file_offset, length, arr,
+                                            len(self.metas), int(validate_crc), None, ctypes.byref(self._h),
+                                            ctypes.byref(err)), err)
+
+    @classmethod
+    def for_chunks(cls, ctx, f, chunks, validate_crc=False, whole_file=False):
+        """Index the (row group, column) chunks of File f: their byte range (or the whole file) is
+        copied to the device once."""
+        metas = [f.chunk_meta(rg, c) for rg, c in chunks]
+        if whole_file or not metas:
+            lo, hi = 0, len(f.data)
+        else:
+            st = [m.dictionary_page_offset if m.dictionary_page_offset >= 0 else m.data_page_offset for m in metas]
+            lo = max(0, min(st))
+            hi = min(len(f.data), max(s + max(m.total_compressed_size, 0) for s, m in zip(st, metas)))
+            hi = max(hi, lo)
+        buf = DeviceBuffer(ctx, f.data[lo:hi])
+        return cls(ctx, buf.ptr.value, lo, hi - lo, metas, validate_crc, keep=buf)
+
+    def chunk(self, k):
+        n, st = ctypes.c_int32(), ctypes.c_int32()
+        if lib().pqgpu_page_index_chunk(self._h, k, ctypes.byref(n), ctypes.byref(st)):
+            raise IndexError(k)
+        return n.value, st.value
+
+    def page(self, k, i):
+        h = PageHeader()
+        if lib().pqgpu_page_index_page(self._h, k, i, ctypes.byref(h)):
+            raise IndexError((k, i))
+        return h
+
+    @property
+    def walk_ms(self):
+        return lib().pqgpu_page_index_walk_ms(self._h)
+
+    def close(self):
+        if self._h:
+            lib().pqgpu_page_index_destroy(self._h)
+            self._h = ctypes.c_void_p()
+        if self._keep is not None:
+            self._keep.close()
+            self._keep = None
 
     def __del__(self):
         try:

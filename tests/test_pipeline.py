@@ -104,13 +104,16 @@ def _files_for_pipeline():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("depth,threads", [(1, 1), (2, 2), (4, 3)])
+@pytest.mark.parametrize("depth,threads,device_index", [(1, 1, False), (2, 2, False), (4, 3, False), (2, 2, True),
+                                                        (3, 3, True)])
 @pytest.mark.parametrize("name", _files_for_pipeline())
-def test_gpu_pipeline_parity(gpu_ctx, name, depth, threads):
+def test_gpu_pipeline_parity(gpu_ctx, name, depth, threads, device_index):
+    """device_index: each row group's byte range is made resident and its page headers walked on the
+    GPU (pagewalk.hip); the results must not change."""
     data = pqtest.load(name)
     orc = {(rg, col): r for rg, col, r in pqtest.oracle_decode(data)}
     f = pqgpu.File(data)
-    p = pqgpu.Pipeline(gpu_ctx, f, depth=depth, threads=threads)
+    p = pqgpu.Pipeline(gpu_ctx, f, depth=depth, threads=threads, device_index=device_index)
     seen = []
     for rg, b, err in p:
         seen.append(rg)
@@ -125,6 +128,7 @@ def test_gpu_pipeline_parity(gpu_ctx, name, depth, threads):
     assert seen == list(range(f.num_row_groups))
     st = p.stats()
     assert st["row_groups"] == f.num_row_groups and st["chunks"] == f.num_row_groups * f.num_columns
+    assert (st["index_ms"] > 0) == device_index
     p.close()
 
 
@@ -172,7 +176,7 @@ def test_gpu_pipeline_cfg5_replica(gpu_ctx):
     data, _ = W.gen_cfg5(rows=3 * 20000, rg_rows=20000)
     orc = {(rg, col): r for rg, col, r in pqtest.oracle_decode(data)}
     f = pqgpu.File(data)
-    p = pqgpu.Pipeline(gpu_ctx, f, depth=2, threads=2)
+    p = pqgpu.Pipeline(gpu_ctx, f, depth=2, threads=2, device_index=True)
     n = 0
     for rg, b, err in p:
         assert err is None

@@ -486,3 +486,17 @@ def write_file_schema(schema, leaves, row_groups, codec=0):
                    (4, LIST, (STRUCT, rgs)), (6, BIN, "rawpq reference-style writer")])
     out += fmd + struct.pack("<I", len(fmd)) + b"PAR1"
     return bytes(out)
+
+
+def crc_probe_chunk(pages):
+    """A bare chunk of DATA_PAGE (V1) pages with given bodies and stored checksums [(body, crc)], for
+    the device CRC32 check: (bytes, [pqgpu.ChunkMeta]) with the chunk at offset 0."""
+    import pqgpu
+    out = bytearray()
+    for body, c in pages:
+        c &= 0xFFFFFFFF
+        dph = [(1, I32, 0), (2, I32, ENC["PLAIN"]), (3, I32, ENC["RLE"]), (4, I32, ENC["RLE"])]
+        out += tstruct([(1, I32, 0), (2, I32, len(body)), (3, I32, len(body)),
+                        (4, I32, c - (1 << 32) if c >= 1 << 31 else c), (5, STRUCT, dph)]) + body
+    m = pqgpu.ChunkMeta(TYPES["INT32"], 0, 0, len(out), 0, -1, 0, 0)
+    return bytes(out), [m]
