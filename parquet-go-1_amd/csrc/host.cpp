@@ -2497,6 +2497,7 @@ int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_e
   if (!bytes) return PQ_OK;
   HIPCHECK(hipSetDevice(ctx->device), err);
   HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDefault), err);
+  HIPCHECK(hipDeviceSynchronize(), err);  // visible to kernels on every stream of the device
   return PQ_OK;
 }
 

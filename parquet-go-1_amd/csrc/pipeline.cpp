@@ -62,6 +62,7 @@ struct pqgpu_pipeline {
   const pqgpu_file *f = nullptr;
   std::vector<int32_t> rgs, cols;
   int validate_crc = 0, device_index = 0;
+  bool registered = false;  // device_index: the file buffer is page-locked (H2D straight from it)
   std::vector<Slot> slots;
   std::vector<std::thread> workers;
   std::mutex m;
@@ -94,12 +95,17 @@ static pqgpu_page_index *index_row_group(pqgpu_pipeline *p, Slot *sl, int32_t rg
     sl->h_raw = sl->d_raw = nullptr;
     sl->raw_cap = 0;
     const size_t cap = n + n / 8 + 4096;
-    if (hipHostMalloc(&sl->h_raw, cap, hipHostMallocDefault) != hipSuccess || hipMalloc(&sl->d_raw, cap) != hipSuccess)
+    if ((!p->registered && hipHostMalloc(&sl->h_raw, cap, hipHostMallocDefault) != hipSuccess) ||
+        hipMalloc(&sl->d_raw, cap) != hipSuccess)
       return nullptr;
     sl->raw_cap = cap;
   }
-  memcpy(sl->h_raw, pqgpu_file_bytes(p->f) + lo, n);
-  if (hipMemcpyAsync(sl->d_raw, sl->h_raw, n, hipMemcpyHostToDevice, sl->s) != hipSuccess) return nullptr;
+  const uint8_t *src = pqgpu_file_bytes(p->f) + lo;
+  if (!p->registered) {  // stage through the slot's pinned buffer
+    memcpy(sl->h_raw, src, n);
+    src = (const uint8_t *)sl->h_raw;
+  }
+  if (hipMemcpyAsync(sl->d_raw, src, n, hipMemcpyHostToDevice, sl->s) != hipSuccess) return nullptr;
   pqgpu_page_index *ix = nullptr;
   pqgpu_error e;
   if (pqgpu_page_index_build(p->ctx, sl->d_raw, lo, (int64_t)n, metas.data(), (int32_t)metas.size(), p->validate_crc,
@@ -180,6 +186,7 @@ static void destroy(pqgpu_pipeline *p) {
     if (sl.d_raw) (void)hipFree(sl.d_raw);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
+  if (p->registered) (void)hipHostUnregister((void *)pqgpu_file_bytes(p->f));
   delete p;
 }
 
@@ -205,6 +212,11 @@ extern "C" int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const 
   const int threads = opts && opts->threads > 0 ? opts->threads : depth;
   p->validate_crc = opts ? opts->validate_crc : 0;
   p->device_index = opts ? opts->device_index : 0;
+  // device_index copies whole row-group ranges H2D: page-lock the file buffer once so they go
+  // straight from it (a buffer that cannot be registered, e.g. already pinned, is staged instead)
+  if (p->device_index && pqgpu_file_len(f) > 0 && hipSetDevice(ctx->device) == hipSuccess)
+    p->registered = hipHostRegister((void *)pqgpu_file_bytes(f), pqgpu_file_len(f), hipHostRegisterDefault) == hipSuccess;
+  if (p->device_index && !p->registered) (void)hipGetLastError();
   if (hipSetDevice(ctx->device) != hipSuccess) { delete p; set_err(err, PQ_ERR_HIP, "hipSetDevice failed"); return PQ_ERR_HIP; }
   p->slots.resize((size_t)depth);
   for (auto &sl : p->slots) {

@@ -599,14 +599,17 @@ class Pipeline:
 class DeviceBuffer:
     """Device memory on libpqgpu's runtime holding `data` (pqgpu_dev_alloc + pqgpu_copy)."""
 
-    def __init__(self, ctx, data, pad=64):
-        self.ctx, self.size = ctx, len(data)
+    def __init__(self, ctx, data=None, pad=64, src_addr=None, size=None):
+        """`data` (bytes-like), or `size` bytes at host address `src_addr` (no intermediate copy)."""
+        self.ctx, self.size = ctx, (len(data) if src_addr is None else size)
         self.ptr = ctypes.c_void_p()
         err = Error()
         _check(lib().pqgpu_dev_alloc(ctx._h, self.size + pad, ctypes.byref(self.ptr), ctypes.byref(err)), err)
         if self.size:
-            src = ctypes.create_string_buffer(bytes(data), self.size)
-            copy(ctx, self.ptr.value, ctypes.addressof(src), self.size)
+            if src_addr is None:
+                src = ctypes.create_string_buffer(bytes(data), self.size)
+                src_addr = ctypes.addressof(src)
+            copy(ctx, self.ptr.value, src_addr, self.size)
 
     def close(self):
         if self.ptr and self.ptr.value:
@@ -654,7 +657,7 @@ class PageIndex:
             lo = max(0, min(st))
             hi = min(len(f.data), max(s + max(m.total_compressed_size, 0) for s, m in zip(st, metas)))
             hi = max(hi, lo)
-        buf = DeviceBuffer(ctx, f.data[lo:hi])
+        buf = DeviceBuffer(ctx, src_addr=ctypes.addressof(f._buf) + lo, size=hi - lo)
         return cls(ctx, buf.ptr.value, lo, hi - lo, metas, validate_crc, keep=buf)
 
     def chunk(self, k):
