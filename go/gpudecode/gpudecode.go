@@ -169,6 +169,95 @@ func (b *Batch) AddFileChunk(f *File, rg, col int, validateCRC bool) (int32, err
 	return int32(id), err
 }
 
+// PageIndex is the on-device page index of some column chunks of a file
+// (pqgpu_page_index_build): readPages' header loop (chunk_reader.go:182-263) and
+// readPageBlock's CRC32 check (:173-177) run on the GPU over the chunks' bytes,
+// copied to the device once. Chunks the walk cannot take fall back to the host
+// walk inside AddIndexedChunk, so errors are the reference's either way.
+type PageIndex struct {
+	ix  *C.pqgpu_page_index
+	ctx *Context
+	dev unsafe.Pointer
+}
+
+// IndexRowGroup copies the byte range of the chunks (rg, cols...) of f to the
+// device and walks their page headers there (validateCRC: checksum every block).
+func IndexRowGroup(ctx *Context, f *File, rg int, cols []int, validateCRC bool) (*PageIndex, error) {
+	var e C.pqgpu_error
+	metas := make([]C.pqgpu_chunk_meta, len(cols))
+	lo, hi := int64(-1), int64(0)
+	for k, c := range cols {
+		if err := toErr(C.pqgpu_file_chunk_meta(f.f, C.int(rg), C.int(c), &metas[k], &e), &e); err != nil {
+			return nil, err
+		}
+		st := int64(metas[k].data_page_offset)
+		if metas[k].dictionary_page_offset >= 0 {
+			st = int64(metas[k].dictionary_page_offset)
+		}
+		if st < 0 {
+			st = 0
+		}
+		end := st + int64(metas[k].total_compressed_size)
+		if end > int64(f.n) {
+			end = int64(f.n)
+		}
+		if lo < 0 || st < lo {
+			lo = st
+		}
+		if end > hi {
+			hi = end
+		}
+	}
+	if lo < 0 || hi < lo {
+		lo, hi = 0, 0
+	}
+	var dev unsafe.Pointer
+	if err := toErr(C.pqgpu_dev_alloc(ctx.c, C.size_t(hi-lo+64), &dev, &e), &e); err != nil {
+		return nil, err
+	}
+	if hi > lo {
+		if err := toErr(C.pqgpu_copy(ctx.c, dev, unsafe.Pointer(uintptr(f.buf)+uintptr(lo)), C.size_t(hi-lo), &e), &e); err != nil {
+			C.pqgpu_dev_free(ctx.c, dev)
+			return nil, err
+		}
+	}
+	crc := C.int32_t(0)
+	if validateCRC {
+		crc = 1
+	}
+	var ix *C.pqgpu_page_index
+	var mp *C.pqgpu_chunk_meta
+	if len(metas) > 0 {
+		mp = &metas[0]
+	}
+	if err := toErr(C.pqgpu_page_index_build(ctx.c, dev, C.int64_t(lo), C.int64_t(hi-lo), mp, C.int32_t(len(metas)), crc,
+		nil, &ix, &e), &e); err != nil {
+		C.pqgpu_dev_free(ctx.c, dev)
+		return nil, err
+	}
+	return &PageIndex{ix: ix, ctx: ctx, dev: dev}, nil
+}
+
+// Close frees the index and its device copy of the bytes (after the batches that
+// added its chunks were uploaded: Decode uploads first).
+func (p *PageIndex) Close() {
+	C.pqgpu_page_index_destroy(p.ix)
+	C.pqgpu_dev_free(p.ctx.c, p.dev)
+	p.ix, p.dev = nil, nil
+}
+
+// AddIndexedChunk is AddFileChunk for chunk k of the index (column cols[k]).
+func (b *Batch) AddIndexedChunk(p *PageIndex, k int, f *File, col int, validateCRC bool) (int32, error) {
+	var e C.pqgpu_error
+	var id C.int32_t
+	crc := C.int(0)
+	if validateCRC {
+		crc = 1
+	}
+	err := toErr(C.pqgpu_batch_add_indexed_file_chunk(b.b, p.ix, C.int32_t(k), f.f, C.int(col), crc, &id, &e), &e)
+	return int32(id), err
+}
+
 // ColumnInfo is a leaf column's schema facts (readColumnSchema schema.go:893-924).
 type ColumnInfo struct {
 	PhysicalType, TypeLength, MaxDef, MaxRep, Repetition int

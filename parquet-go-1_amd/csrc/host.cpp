@@ -451,6 +451,9 @@ struct pqgpu_batch {
   struct HostGather { uint64_t src, len; uint32_t page; };
   std::vector<HostGather> gathers;
   uint64_t o_gather = 0;
+  // PLAIN BYTE_ARRAY pages (plainba.hip): page list, first segment per page, segment -> page
+  std::vector<uint32_t> pba_pages, pba_seg0, pba_seg_page;
+  uint64_t l_pba_pages = 0, l_pba_seg0 = 0, l_pba_seg_page = 0, o_pba_segs = 0, o_pba_limit = 0;
   uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
@@ -1066,6 +1069,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->level_pages_bw1.clear();
   b->ba_delta_scratch.assign(b->ba_delta.size(), 0);
   b->delta_pages.clear();
+  b->pba_pages.clear();
+  b->pba_seg0.clear();
+  b->pba_seg_page.clear();
   b->dblk_base.assign(np, 0);
   b->dblk_total = 0;
   b->scan_pages.clear();
@@ -1235,7 +1241,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           }
           break;
         case VK_PLAIN_BA:
-          if (ns_p) b->items.push_back(WorkItem{p, 0, ns_p, WI_PLAIN_BA, {0, 0, 0}});
+          if (ns_p) {  // plainba.hip: 256-byte segments of the values section
+            const uint32_t li = (uint32_t)b->pba_pages.size();
+            b->pba_pages.push_back(p);
+            b->pba_seg0.push_back((uint32_t)b->pba_seg_page.size());
+            const uint32_t nseg = std::max<uint32_t>(1, (pd.val_len + kPbaSegHost - 1) / kPbaSegHost);
+            b->pba_seg_page.insert(b->pba_seg_page.end(), nseg, li);
+          }
           break;
         case VK_DLBA: case VK_DBA: {
           BaDelta &bd = b->ba_delta[pd.ba_delta];
@@ -1354,6 +1366,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_ba_delta = take(b->ba_delta.size() * sizeof(BaDelta));
   b->o_snappy = take(b->snappy.size() * sizeof(SnappyJob));
   b->o_gather = take(b->gathers.size() * sizeof(GatherJob));
+  b->pba_seg0.push_back((uint32_t)b->pba_seg_page.size());  // [n_pages + 1]
+  b->l_pba_pages = take(b->pba_pages.size() * 4);
+  b->l_pba_seg0 = take(b->pba_seg0.size() * 4);
+  b->l_pba_seg_page = take(b->pba_seg_page.size() * 4);
+  b->o_pba_segs = take(b->pba_seg_page.size() * 16);
+  b->o_pba_limit = take(b->pba_pages.size() * 4);
   b->o_dblk = take(b->dblk_total * sizeof(DeltaBlk));
   b->o_dblk_sum = take(b->dblk_total * 8);
   b->o_dblk_base = take((uint64_t)np * 8);
@@ -1542,6 +1560,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
   HIPCHECK(up(b->l_delta, b->delta_pages.data(), b->delta_pages.size() * 4), err);
+  HIPCHECK(up(b->l_pba_pages, b->pba_pages.data(), b->pba_pages.size() * 4), err);
+  HIPCHECK(up(b->l_pba_seg0, b->pba_seg0.data(), b->pba_seg0.size() * 4), err);
+  HIPCHECK(up(b->l_pba_seg_page, b->pba_seg_page.data(), b->pba_seg_page.size() * 4), err);
   // the host copies above read from std::vector memory: wait before those vectors change
   HIPCHECK(hipStreamSynchronize(s), err);
   b->stats.num_chunks = nc;
@@ -1597,6 +1618,19 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.npages = (uint32_t)b->pages.size();
   d.nchunks = (uint32_t)b->chunks.size();
   return d;
+}
+
+static PbaLists pba_lists(pqgpu_batch *b) {
+  uint8_t *A = b->d_arena;
+  PbaLists l;
+  l.pages = (const uint32_t *)(A + b->l_pba_pages);
+  l.n_pages = (uint32_t)b->pba_pages.size();
+  l.seg0 = (const uint32_t *)(A + b->l_pba_seg0);
+  l.seg_page = (const uint32_t *)(A + b->l_pba_seg_page);
+  l.segs = (uint4 *)(A + b->o_pba_segs);
+  l.limit = (uint32_t *)(A + b->o_pba_limit);
+  l.n_segs = (uint32_t)b->pba_seg_page.size();
+  return l;
 }
 
 static LaunchLists launch_lists(pqgpu_batch *b) {
@@ -1667,6 +1701,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(hipMemsetAsync(A + b->f_begin, 0xff, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
+  const PbaLists pl = pba_lists(b);
   // SNAPPY pages first: every later kernel reads page data
   if (!b->snappy.empty())
     HIPCHECK(timed(b, 11, s, b->snappy.size(), [&] {
@@ -1690,6 +1725,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
     HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
     HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
+    HIPCHECK(launch_plain_ba(d, pl, v), err);
     HIPCHECK(launch_ba_delta(d, l, v), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
@@ -1710,6 +1746,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       // are dispatched first and the bandwidth-bound tiles fill the CUs around them
       HIPCHECK(timed(b, 9, s, l.n_items, [&] { return launch_values(d, l, s); }), err);
     }
+    HIPCHECK(launch_plain_ba(d, pl, s), err);  // PLAIN BYTE_ARRAY: length chains -> values
     HIPCHECK(launch_ba_delta(d, l, s), err);  // DELTA_LENGTH / DELTA_BYTE_ARRAY: lengths -> values
   }
   if (!b->ba_chunks.empty()) {

@@ -99,6 +99,17 @@ hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t 
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // walk + sums + prefix
+// PLAIN BYTE_ARRAY pages (plainba.hip): speculative segment walks, verified per page
+struct PbaLists {
+  const uint32_t *pages; uint32_t n_pages;  // PLAIN BYTE_ARRAY pages with values
+  const uint32_t *seg0;                     // [n_pages + 1] first segment of each page
+  const uint32_t *seg_page;                 // [n_segs] the page-list index of each segment
+  uint4 *segs;                              // [n_segs] entry, exit, values, error -> first value
+  uint32_t *limit;                          // [n_pages] values written per page
+  uint32_t n_segs;
+};
+constexpr uint32_t kPbaSegHost = 256;  // plainba.hip kPbaSeg
+hipError_t launch_plain_ba(const BatchDev &b, const PbaLists &l, hipStream_t s);
 // on-device page index (pagewalk.hip): header walk of every chunk (+ CRC32 of every checksummed
 // block), and the upload-time gather of resident UNCOMPRESSED page bodies
 hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, PageIxChunk *chunks, uint32_t nchunks,

@@ -437,8 +437,6 @@ constexpr uint32_t kNoEntry = 0xffffffffu;
 constexpr uint32_t kLvRunShift = 48;  // generic widths: run counts in the P5 scan's high bits
 constexpr uint64_t kLvValMask = (1ull << kLvRunShift) - 1;
 constexpr uint32_t kLvTileBuf = 64;
-constexpr uint32_t kLvSerialHops = 48;    // P0: hops one lane takes before the chunk goes to list ranking
-constexpr uint32_t kLvSerialBackoff = 4;  // chunks P0 is not tried after it ran out of hops  // fill-tile starts buffered per chunk (more go out directly)
 constexpr uint32_t kLfTile = kLfTileHost;  // values per k_level_fill tile (aligned on the chunk's slots)
 // Fill tiles of a page: the kLfTile-slot blocks of the chunk that hold any of its slots.
 DEV uint32_t lf_tiles(uint64_t slot_base, uint32_t ns) {
@@ -1408,7 +1406,6 @@ DEV bool delta_hdr(const uint8_t *s, const uint8_t *gs, uint32_t n, uint32_t pos
 // ---------------------------------------------------------------------------
 constexpr uint32_t kDwWin = 16384;                     // walk window bytes
 constexpr uint32_t kDwWinLoad = kDwWin + 64;           // + overlap for a header straddling the end
-constexpr uint32_t kDwVec = (kDwWinLoad / 16 + 255) / 256;  // uint4 per thread per window
 
 struct DeltaWalkLDS {
   uint32_t win[kDwWinLoad / 4 + 4];
@@ -2334,32 +2331,6 @@ DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn) {
   }
 }
 
-// PLAIN BYTE_ARRAY (type_bytearray.go:24-55): u32 length prefix chain, walked by
-// one lane; records the source address and length of every value.
-DEV void do_plain_ba(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
-  if (threadIdx.x != 0) return;
-  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
-  const uint32_t n = pd.val_len;
-  const uint64_t vb = b.page_vbase[wi.page];
-  const int32_t fixed = cd.type == T_FLBA ? cd.type_length : 0;
-  uint32_t p = 0;
-  for (uint32_t v = 0; v < nn; v++) {
-    int64_t l = fixed;
-    if (fixed == 0) {
-      if (p >= n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_EOF); return; }
-      if (p + 4 > n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_UNEXPECTED_EOF); return; }
-      l = (int32_t)ld32(s + p);
-      p += 4;
-      if (l < 0) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_INVALID); return; }
-    }
-    if (l > 0 && p >= n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_EOF); return; }
-    if ((uint64_t)p + (uint64_t)l > n) { report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, v, PQ_ERR_UNEXPECTED_EOF); return; }
-    (gp_u64<uint64_t>(cd.ba_index))[vb + v] = (uint64_t)(s + p);
-    (gp_u64<int32_t>(cd.offsets))[vb + v + 1] = (int32_t)l;
-    p += (uint32_t)l;
-  }
-}
-
 __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
   __shared__ ValuesLDS lds;
@@ -2374,7 +2345,6 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
-    case WI_PLAIN_BA: do_plain_ba(b, wi, pd, cd, nn); break;
     case WI_DLENS: {  // a DELTA lengths stream of a DELTA_LENGTH / DELTA_BYTE_ARRAY page
       const BaDelta &bd = b.ba_delta[pd.ba_delta];
       const BaDeltaStream &st = bd.st[wi.v0];
