@@ -2703,9 +2703,130 @@ DEV void snappy_copy(SnappyOut &o, uint32_t P, uint32_t off, uint32_t len) {
   if (i < len) o.ring[(P + i) & kRingMask] = (uint8_t)v;
 }
 
+// The elements of one 64-byte stream window whose output lies within reach, executed together
+// (`batch`: chain lanes; every literal among them lies inside the window, so its bytes are in the
+// lanes' `w` registers). Output byte j of the batch (page position P + j) gets a state: a resolved
+// byte (literals; copy sources before the batch, read from the ring or, past it, from HBM) or a
+// pointer to the earlier batch byte it copies (copy source inside the batch; an overlapping copy
+// points into its own output). Pointer jumping resolves every byte in O(log T) rounds, then the
+// batch lands in the ring at once — instead of executing one element after another, each waiting
+// for the previous one's LDS writes. Returns false on a corrupt element (bounds as
+// decode_other.go:63-95: literal past the stream or the decoded length, copy offset 0 or past
+// the output start, copy past the decoded length).
+constexpr uint32_t kSnappyBatch = 1536;  // bytes: elements starting in 64 stream bytes write at most
+                                         // 22 copies x 64 = 1408 (2-byte-offset copies, 3 bytes each)
+constexpr uint32_t kSnRes = 0x8000u;     // state: resolved | byte, else the batch index it copies
+DEV bool snappy_batch(SnappyOut &o, uint16_t *st, uint64_t batch, uint32_t P, uint32_t op, uint32_t dlen, uint32_t n,
+                      uint32_t pos, uint32_t t, uint32_t hdr, uint32_t val, uint32_t clen, uint32_t w, uint32_t &T) {
+  const uint32_t lane = lane_id();
+  const bool in = (batch >> lane) & 1ull;
+  const uint32_t len = in ? (t == 0 ? val + 1 : clen) : 0u;  // literals in a batch are short: no overflow
+  const uint32_t O = wave_excl_scan(len);
+  T = sgpr(rdlane(O + len, 63));
+  const uint32_t rel = lane + hdr;  // literal start within the window
+  bool bad = false;
+  if (in) {
+    if (pos + rel > n) bad = true;
+    else if (t == 0) bad = (uint64_t)len > (uint64_t)(dlen - (op + O)) || pos + rel + len > n;
+    else bad = val == 0 || op + O < val || len > dlen - (op + O);
+  }
+  if (__ballot(bad) || T > kSnappyBatch) return false;
+  snappy_room(o, P, T);
+  // Byte-parallel fill: batch byte j belongs to the last lane e whose output start O_e <= j (a
+  // lane outside the batch has the start of the next batch lane, so that lane is a batch lane),
+  // found by binary search over the lanes' O (ds_bpermute); 4 bytes per lane in flight.
+  const uint32_t pk2 = t | (rel << 2);
+  bool far = false;  // some copy source is older than the ring
+  auto bperm = [](uint32_t l, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l & 63) * 4), (int)v);
+  };
+  for (uint32_t j0 = 0; j0 < T; j0 += 256) {
+    uint32_t e[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) e[k] = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t c = e[k] + step;
+        const uint32_t oc = bperm(c, O);
+        if (c < 64 && oc <= j0 + 64 * k + lane) e[k] = c;
+      }
+    }
+    uint32_t Oe[4], ve[4], pe[4], lb[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      Oe[k] = bperm(e[k], O);
+      ve[k] = bperm(e[k], val);
+      pe[k] = bperm(e[k], pk2);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t j = j0 + 64 * k + lane;
+      lb[k] = bperm((pe[k] >> 2) + (j - Oe[k]), w) & 0xffu;  // the literal's byte (literals lie in the window)
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t j = j0 + 64 * k + lane;
+      if (j < T) {
+        uint32_t sv;
+        if ((pe[k] & 3) == 0) {
+          sv = kSnRes | lb[k];
+        } else if (j >= ve[k]) {
+          sv = j - ve[k];  // an earlier byte of this batch
+        } else if (ve[k] + T <= kSnappyRing) {
+          sv = kSnRes | o.ring[(P + j - ve[k]) & kRingMask];  // page byte before the batch, in the ring
+        } else {
+          sv = kSnRes;
+          far = true;  // resolved below from HBM
+        }
+        st[j] = (uint16_t)sv;
+      }
+    }
+  }
+  if (__ballot(far)) {  // sources flushed long ago: read the page in HBM (L1 bypassed)
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t i = 0;; i++) {
+      const bool act = in && t != 0 && i < len && O + i < val && val + T > kSnappyRing;
+      if (!__ballot(act)) break;
+      if (act) {
+        const uint32_t q = P + O + i - val;
+        const uint32_t *wp = (const uint32_t *)(o.dst + (q & ~3u));
+        st[O + i] = (uint16_t)(kSnRes | ((__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (q & 3))) & 0xffu));
+      }
+    }
+  }
+  wave_lds_sync();
+  for (;;) {  // pointer jumping: 8 bytes per lane per group, their LDS reads issued together
+    bool open = false;
+    for (uint32_t j0 = 0; j0 < T; j0 += 512) {
+      uint32_t v[8], u[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t j = j0 + 64 * k + lane;
+        v[k] = j < T ? st[j] : kSnRes;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) u[k] = (v[k] & kSnRes) ? v[k] : st[v[k]];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        if (!(v[k] & kSnRes)) {
+          st[j0 + 64 * k + lane] = (uint16_t)u[k];
+          open |= !(u[k] & kSnRes);
+        }
+      }
+    }
+    wave_lds_sync();
+    if (!__ballot(open)) break;
+  }
+  for (uint32_t j = lane; j < T; j += 64) o.ring[(P + j) & kRingMask] = (uint8_t)st[j];
+  wave_lds_sync();
+  return true;
+}
+
 // Wave 0 walks and executes the element chain; waves 1.. wait at barriers and join in the
 // body copies of long literals (snappy_literal) until wave 0 raises `stop`.
-DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, SnappyCmd &cmd) {
+DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, SnappyCmd &cmd, uint16_t *st) {
   const uint8_t *src = gp_u64<const uint8_t>(jb.src);
   const uint32_t n = sgpr(jb.src_len), raw = sgpr(jb.raw_len), dlen = sgpr(jb.dlen);
   const uint32_t lane = lane_id();
@@ -2725,6 +2846,8 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     return k < wlim ? srcw[k >> 2] : 0u;
   };
   uint32_t wb = 0, W0 = ldw(0), W1 = ldw(256);
+  PQ_STAMPS(sp, b.dbg);
+  sp.begin();
   while (pos < n) {
     // the element that would start at pos + lane: tag, header bytes, literal length - 1 or
     // copy offset, copy length (decode_other.go:20-96)
@@ -2764,41 +2887,50 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     const uint32_t pk = t | (hdr << 2) | (clen << 5);  // one readlane per element for type, header, length
     uint64_t chain = 0;
     uint32_t cur = 0;
+    sp.lap(0);
     while (cur < 64 && pos + cur < n) {
       chain |= 1ull << cur;
       cur += (uint32_t)__builtin_amdgcn_readlane((int)esz, (int)cur);
     }
-    while (chain) {
-      const uint32_t e = (uint32_t)__builtin_ctzll(chain);
-      chain &= chain - 1;
-      const uint32_t epk = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)e);
-      const uint32_t et = epk & 3, eh = (epk >> 2) & 7;
-      const uint32_t ev = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)e);
-      const uint32_t s = pos + e + eh;  // first byte after the header
-      if (s > n) { bad = true; break; }
-      if (et == 0) {
+    sp.lap(1);
+    sp.count(4);
+    sp.add(5, __popcll(chain));
+    // runs of short elements execute as batches; a literal reaching past the window (its bytes
+    // are not in the registers) executes on its own, with the long-literal copy when it is long
+    const bool lng = t == 0 && lane + hdr + (uint64_t)val + 1 > 64;
+    const uint64_t longs = __ballot(lng) & chain;
+    while (chain && !bad) {
+      const uint64_t upto = longs & chain;
+      const uint32_t fl = upto ? (uint32_t)__builtin_ctzll(upto) : 64u;
+      const uint64_t batch = fl < 64 ? chain & ((1ull << fl) - 1ull) : chain;
+      if (batch) {
+        uint32_t T;
+        if (!snappy_batch(o, st, batch, raw + op, op, dlen, n, pos, t, hdr, val, clen, w, T)) { bad = true; break; }
+        op += T;
+        sp.lap(2);
+        sp.add(6, T);
+        chain &= ~batch;
+      }
+      if (fl < 64) {
+        const uint32_t e = fl;
+        chain &= chain - 1;  // fl is now the lowest element
+        const uint32_t epk = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)e);
+        const uint32_t eh = (epk >> 2) & 7;
+        const uint32_t ev = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)e);
+        const uint32_t s = pos + e + eh;
+        if (s > n) { bad = true; break; }
         const uint64_t len = (uint64_t)ev + 1;
         if (len > dlen - op || len > n - s) { bad = true; break; }
-        const uint32_t rel = s - pos;  // literal start inside this window's 64 lanes
-        if (rel + len <= 64) {
-          // short literal: its bytes are byte 0 of lanes rel.. of this window (no memory load)
-          snappy_room(o, raw + op, 64);
-          const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rel + lane) * 4), (int)w);
-          if (lane < (uint32_t)len) o.ring[(raw + op + lane) & kRingMask] = (uint8_t)v;
-        } else {
-          snappy_literal(o, cmd, src + s, raw + op, (uint32_t)len);
-        }
+        snappy_literal(o, cmd, src + s, raw + op, (uint32_t)len);
         op += (uint32_t)len;
-      } else {
-        const uint32_t el = epk >> 5;
-        if (ev == 0 || op < ev || el > dlen - op) { bad = true; break; }
-        snappy_copy(o, raw + op, ev, el);
-        op += el;
+        sp.lap(3);
       }
     }
     if (bad) break;
     pos += cur;
   }
+  sp.lap(7);
+  sp.flush(48);
   if (bad || op != dlen) {
     if (lane == 0) report(b, jb.chunk, 0, jb.page_in_chunk, ST_DECOMP, 0, PQ_ERR_DECOMPRESS);
     return;
@@ -2815,10 +2947,11 @@ __global__ void __launch_bounds__(64 * kSnappyWaves) k_snappy(BatchDev b_in, con
   const BatchDev b = global_view(b_in);
   __shared__ __attribute__((aligned(16))) uint8_t ring[kSnappyRing];
   __shared__ SnappyCmd cmd;
+  __shared__ uint16_t st[kSnappyBatch];  // batch byte states (snappy_batch)
   const SnappyJob &jb = gp(jobs)[blockIdx.x];
   const uint32_t w = threadIdx.x / 64;
   if (w == 0) {
-    snappy_page(b, jb, ring, cmd);
+    snappy_page(b, jb, ring, cmd, st);
     if (lane_id() == 0) cmd.stop = 1;
     wg_barrier();
   } else {

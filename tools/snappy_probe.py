@@ -33,24 +33,29 @@ def make(kind):
     return bio.getvalue()
 
 
-ctx = pqgpu.Context(0)
-for kind in ("double_required", "double_optional", "int64_small"):
-    data = make(kind)
-    f = pqgpu.File(data)
-    b = pqgpu.Batch(ctx)
-    for rg in range(f.num_row_groups):
-        _, e = b.add_file_chunk(f, rg, 0)
-        assert e is None, e
-    b.upload()
-    b.decode()
-    assert b.sync() is None
-    b.kernel_timing(True)
-    for _ in range(10):
+def main():
+    ctx = pqgpu.Context(0)
+    for kind in ("double_required", "double_optional", "int64_small"):
+        data = make(kind)
+        f = pqgpu.File(data)
+        b = pqgpu.Batch(ctx)
+        for rg in range(f.num_row_groups):
+            _, e = b.add_file_chunk(f, rg, 0)
+            assert e is None, e
+        b.upload()
         b.decode()
-    b.sync()
-    kt = b.kernel_times()
-    st = b.stats()
-    print(json.dumps({"case": kind, "pages": int(st.snappy_pages), "file_MB": round(len(data) / 1e6, 1),
-                      "k_snappy_ms": round(kt["k_snappy"][0], 4),
-                      "k_snappy_GBps": round(st.snappy_kernel_bytes / kt["k_snappy"][0] / 1e6, 1)}), flush=True)
-    b.close()
+        assert b.sync() is None
+        b.kernel_timing(True)
+        for _ in range(10):
+            b.decode()
+        b.sync()
+        kt = b.kernel_times()
+        st = b.stats()
+        print(json.dumps({"case": kind, "pages": int(st.snappy_pages), "file_MB": round(len(data) / 1e6, 1),
+                          "k_snappy_ms": round(kt["k_snappy"][0], 4),
+                          "k_snappy_GBps": round(st.snappy_kernel_bytes / kt["k_snappy"][0] / 1e6, 1)}), flush=True)
+        b.close()
+
+
+if __name__ == "__main__":
+    main()
