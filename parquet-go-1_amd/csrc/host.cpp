@@ -370,7 +370,7 @@ struct KernelTimer {
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
-    "k_nest_count", "k_nest_emit", "k_level_fill"};
+    "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -481,6 +481,7 @@ struct pqgpu_batch {
   // is known up front; PQ_SPEC=0 keeps the serial order. cfg2: 0.559 vs 0.595 ms per step.
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
+  bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
@@ -1721,14 +1722,17 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
+    if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
+      HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
     HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
     HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
-    HIPCHECK(launch_plain_ba(d, pl, v), err);
-    HIPCHECK(launch_ba_delta(d, l, v), err);
+    HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
+    HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
-    HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    if (!b->levels_first)
+      HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
@@ -1746,8 +1750,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       // are dispatched first and the bandwidth-bound tiles fill the CUs around them
       HIPCHECK(timed(b, 9, s, l.n_items, [&] { return launch_values(d, l, s); }), err);
     }
-    HIPCHECK(launch_plain_ba(d, pl, s), err);  // PLAIN BYTE_ARRAY: length chains -> values
-    HIPCHECK(launch_ba_delta(d, l, s), err);  // DELTA_LENGTH / DELTA_BYTE_ARRAY: lengths -> values
+    HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
+    HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
   }
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
@@ -1784,13 +1788,13 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
     }
     HIPCHECK(timed(b, 6, s, l.n_ba_tiles, [&] { return launch_ba_emit(d, l, s); }), err);
-    HIPCHECK(launch_dba_gather(d, l, s), err);
+    HIPCHECK(timed(b, 19, s, l.n_ba_delta, [&] { return launch_dba_gather(d, l, s); }), err);
     if (b->any_ba_sync) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc copies above read host memory
   }
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)
   HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
-  HIPCHECK(launch_nest_scan(d, l, s), err);
+  HIPCHECK(timed(b, 16, s, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, s); }), err);
   HIPCHECK(timed(b, 14, s, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, s); }), err);
   b->decoded = true;
   return PQ_OK;

@@ -98,21 +98,38 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_
         part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
 }
 
-// One wave per chunk: lane j scans counter j over the chunk's tiles.
-__global__ void __launch_bounds__(64) k_nest_scan(BatchDev b_in, const uint32_t *chunks) {
+// One 256-thread workgroup per chunk: thread i takes a contiguous run of the chunk's tiles, sums
+// its counters, one workgroup scan per counter gives the run's bases, and a second pass over the
+// run writes every tile's base (a chunk of 4 M records has ~5,000 tiles: a serial scan of them
+// cost ~0.5 ms).
+__global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t *chunks) {
   const BatchDev b = global_view(b_in);
+  __shared__ uint64_t wsum[4];
   const uint32_t c = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[c];
-  const uint32_t j = threadIdx.x;
-  if (j >= kNestCnt) return;
   const uint32_t nt = (uint32_t)((cd.num_slots + kNestTile - 1) / kNestTile);
-  uint64_t acc = 0;
-  for (uint32_t k = 0; k < nt; k++) {
-    const uint64_t t = (uint64_t)cd.nest_tile0 + k;
-    b.nest_base[t * kNestCnt + j] = acc;
-    acc += b.nest_cnt[t * kNestCnt + j];
+  const uint32_t per = (nt + blockDim.x - 1) / blockDim.x;
+  const uint32_t k0 = min(nt, threadIdx.x * per), k1 = min(nt, k0 + per);
+  const uint32_t *cnt = b.nest_cnt + (uint64_t)cd.nest_tile0 * kNestCnt;
+  uint64_t *base = b.nest_base + (uint64_t)cd.nest_tile0 * kNestCnt;
+  uint64_t acc[kNestCnt];
+#pragma unroll
+  for (uint32_t j = 0; j < kNestCnt; j++) acc[j] = 0;
+  for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++) acc[j] += cnt[(uint64_t)k * kNestCnt + j];
+#pragma unroll
+  for (uint32_t j = 0; j < kNestCnt; j++) {
+    uint64_t tot;
+    acc[j] = block_excl_scan64(acc[j], wsum, &tot);
+    if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot;
   }
-  b.nest_tot[(uint64_t)c * kNestCnt + j] = acc;
+  for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++) {
+      base[(uint64_t)k * kNestCnt + j] = acc[j];
+      acc[j] += cnt[(uint64_t)k * kNestCnt + j];
+    }
 }
 
 // Bits of x at the positions set in m, packed towards bit 0 (Hacker's Delight 7-4, compress).
@@ -276,7 +293,7 @@ hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_
 }
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_chunks) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_scan, dim3(l.n_nest_chunks), dim3(64), 0, s, b, l.nest_chunks);
+  hipLaunchKernelGGL(k_nest_scan, dim3(l.n_nest_chunks), dim3(256), 0, s, b, l.nest_chunks);
   return hipGetLastError();
 }
 template <uint32_t R>
