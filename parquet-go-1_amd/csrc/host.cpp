@@ -2014,13 +2014,8 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   HIPCHECK(hipSetDevice(device), err);
   pqgpu_ctx *c = new pqgpu_ctx();
   c->device = device;
-  // PQ_STREAM_PRIO (experiment): 1 = the side stream (values beside the level kernels) gets the
-  // greatest priority, 2 = the main stream (levels) does
-  const int prio_mode = getenv("PQ_STREAM_PRIO") ? atoi(getenv("PQ_STREAM_PRIO")) : 0;
-  int lo_prio = 0, hi_prio = 0;
-  if (prio_mode) (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
-  e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_mode == 2 ? hi_prio : lo_prio);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio_mode == 1 ? hi_prio : lo_prio);
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

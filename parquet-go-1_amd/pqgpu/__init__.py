@@ -226,10 +226,16 @@ class DecodeError(Exception):
 # after its context or after the HIP runtime has shut down.
 _live_batches = weakref.WeakSet()
 _live_contexts = weakref.WeakSet()
+_live_pipelines = weakref.WeakSet()  # closed first: they own batches, streams and a page-locked file
+_live_indexes = weakref.WeakSet()    # page indexes and the device copies of file bytes they keep
 
 
 @atexit.register
 def _release_all():
+    for p in list(_live_pipelines):
+        p.close()
+    for x in list(_live_indexes):
+        x.close()
     for b in list(_live_batches):
         b.close()
     for c in list(_live_contexts):
@@ -560,6 +566,7 @@ class Pipeline:
                                            len(self.cols), ctypes.byref(opts), ctypes.byref(self._h),
                                            ctypes.byref(err)), err)
         self._out = None
+        _live_pipelines.add(self)
 
     def __iter__(self):
         while True:
@@ -603,6 +610,7 @@ class DeviceBuffer:
         """`data` (bytes-like), or `size` bytes at host address `src_addr` (no intermediate copy)."""
         self.ctx, self.size = ctx, (len(data) if src_addr is None else size)
         self.ptr = ctypes.c_void_p()
+        _live_indexes.add(self)
         err = Error()
         _check(lib().pqgpu_dev_alloc(ctx._h, self.size + pad, ctypes.byref(self.ptr), ctypes.byref(err)), err)
         if self.size:
@@ -644,6 +652,7 @@ class PageIndex:
         _check(lib().pqgpu_page_index_build(ctx._h, ctypes.c_void_p(dev_ptr), file_offset, length, arr,
                                             len(self.metas), int(validate_crc), None, ctypes.byref(self._h),
                                             ctypes.byref(err)), err)
+        _live_indexes.add(self)
 
     @classmethod
     def for_chunks(cls, ctx, f, chunks, validate_crc=False, whole_file=False):

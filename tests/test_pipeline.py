@@ -185,3 +185,30 @@ def test_gpu_pipeline_cfg5_replica(gpu_ctx):
         n += 1
     assert n == 3
     p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["crc_v1", "crc_v1_flipped"])
+def test_gpu_pipeline_device_index_crc(gpu_ctx, name):
+    """WithCRC32Validation through the device-index pipeline (checksums on the GPU): every chunk's
+    outcome equals the host-walk pipeline's (the flipped byte fails its page with PQ_ERR_CRC)."""
+    data = pqtest.load(name)
+    f = pqgpu.File(data)
+    out = {}
+    for dix in (False, True):
+        p = pqgpu.Pipeline(gpu_ctx, f, depth=2, threads=2, validate_crc=True, device_index=dix)
+        for rg, b, _err in p:  # (an assertion below leaves p to pqgpu's exit-time cleanup)
+            for col in range(f.num_columns):
+                e = b.status(col)
+                if e is not None:
+                    got = (e.code, e.page)
+                else:
+                    r = b.result(col)
+                    got = (r.num_slots, r.num_values, r.dLevels.tobytes(),
+                           r.payload if r.offsets is not None else np.asarray(r.values_raw).tobytes())
+                out.setdefault((rg, col), []).append(got)
+        p.close()
+    for k, (host, dev) in out.items():
+        assert host == dev, (name, k)
+    if name == "crc_v1_flipped":
+        assert any(isinstance(v[0], tuple) and v[0][0] == pqgpu.PQ_ERR_CRC for v in out.values())
