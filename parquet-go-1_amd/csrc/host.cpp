@@ -397,7 +397,7 @@ struct StageBuf {
     size_t c = std::max<size_t>(want, cap ? cap * 2 : (size_t)1 << 20);
     uint8_t *q = nullptr;
     if (pinned) {
-      if (hipHostMalloc((void **)&q, c, hipHostMallocDefault) != hipSuccess) q = nullptr;
+      if (hipHostMalloc((void **)&q, c, hipHostMallocCoherent) != hipSuccess) q = nullptr;
     } else {
       q = (uint8_t *)malloc(c);
     }
@@ -2031,6 +2031,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
+  c->pin_release();
   delete c;
 }
 
@@ -2243,53 +2244,54 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
   }
   if (n_chunks == 0) { *out = ix.release(); return PQ_OK; }
   // table capacity: a page per 4 KiB plus 64 per chunk; a walk that outgrows it is rerun larger.
-  // The chunk table and the results travel through pinned host memory (DMA copies): a small
-  // pageable H2D copy may be written by the CPU through the BAR and not yet be visible to a kernel
-  // launched right behind it on another queue.
+  // One launch sequence and one synchronisation per build: the chunk table rides in the kernel
+  // arguments, and k_page_export writes the entry count, the per-chunk results and the table
+  // straight into page-locked host memory (reused from the context's pool).
   struct Pinned {
+    pqgpu_ctx *c;
     void *p = nullptr;
-    ~Pinned() { if (p) (void)hipHostFree(p); }
-  } hc_tab;
-  const size_t ch_bytes = (size_t)n_chunks * sizeof(PageIxChunk);
-  HIPCHECK(hipHostMalloc(&hc_tab.p, ch_bytes + 64, hipHostMallocDefault), err);
-  uint32_t *h_n = (uint32_t *)((uint8_t *)hc_tab.p + ch_bytes);
+    size_t cap = 0;
+    explicit Pinned(pqgpu_ctx *x) : c(x) {}
+    ~Pinned() { c->pin_put(p, cap); }
+  };
+  const size_t res_bytes = align_up((uint64_t)n_chunks * sizeof(uint4), 256);
+  const uint64_t tab_off = ix_out_table_off((uint32_t)n_chunks);
   uint32_t n = 0;
   for (int attempt = 0;; attempt++) {
     cap = std::min<uint64_t>(cap, 1u << 26);
-    memcpy(hc_tab.p, ix->chunks.data(), ch_bytes);
     void *d = nullptr;
-    const size_t bytes = 256 + ch_bytes + cap * sizeof(PageIxEntry);
+    const size_t bytes = 256 + res_bytes + cap * sizeof(PageIxEntry);
+    Pinned h_out(ctx);
+    h_out.p = ctx->pin_get(tab_off + cap * sizeof(PageIxEntry) + 64, &h_out.cap);
+    if (!h_out.p) HIPCHECK(hipErrorOutOfMemory, err);
+    uint8_t *o_dev = nullptr;
+    HIPCHECK(hipHostGetDevicePointer((void **)&o_dev, h_out.p, 0), err);
     HIPCHECK(hipMallocAsync(&d, bytes, s), err);
     uint8_t *D = (uint8_t *)d;
     uint32_t *d_n = (uint32_t *)D;
-    PageIxChunk *d_ch = (PageIxChunk *)(D + 256);
-    PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + ch_bytes);
-    hipError_t he = hipMemsetAsync(d_n, 0, 4, s);
-    if (he == hipSuccess) he = hipMemcpyAsync(d_ch, hc_tab.p, ch_bytes, hipMemcpyHostToDevice, s);
-    if (he == hipSuccess)
-      he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, d_ch, (uint32_t)n_chunks, d_tab, d_n,
-                            (uint32_t)cap, validate_crc, s);
-    if (he == hipSuccess) he = hipMemcpyAsync(h_n, d_n, 4, hipMemcpyDeviceToHost, s);
+    uint4 *d_res = (uint4 *)(D + 256);
+    PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + res_bytes);
+    hipError_t he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, ix->chunks.data(), (uint32_t)n_chunks, d_res,
+                            d_tab, d_n, (uint32_t)cap, validate_crc, s);
+    if (he == hipSuccess) he = launch_page_export(d_n, d_tab, (uint32_t)cap, d_res, (uint32_t)n_chunks, o_dev, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
-    n = *h_n;
-    const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < 3;
-    if (he == hipSuccess && !grow) {
-      const size_t eb = (size_t)std::min<uint64_t>(n, cap) * sizeof(PageIxEntry);
-      Pinned he_tab;
-      he = hipHostMalloc(&he_tab.p, eb + ch_bytes + 64, hipHostMallocDefault);
-      if (he == hipSuccess) he = hipMemcpyAsync(he_tab.p, d_tab, eb, hipMemcpyDeviceToHost, s);
-      if (he == hipSuccess)
-        he = hipMemcpyAsync((uint8_t *)he_tab.p + eb, d_ch, ch_bytes, hipMemcpyDeviceToHost, s);
-      if (he == hipSuccess) he = hipStreamSynchronize(s);
-      if (he == hipSuccess) {
-        ix->entries.resize(eb / sizeof(PageIxEntry));
-        memcpy(ix->entries.data(), he_tab.p, eb);
-        memcpy(ix->chunks.data(), (uint8_t *)he_tab.p + eb, ch_bytes);
-      }
-    }
     (void)hipFreeAsync(d, s);
     HIPCHECK(he, err);
-    if (!grow) break;
+    const uint8_t *O = (const uint8_t *)h_out.p;
+    n = *(const uint32_t *)O;
+    const bool grow = n > cap && cap < (1u << 26) && attempt < 3;
+    if (!grow) {
+      const size_t eb = (size_t)std::min<uint64_t>(n, cap) * sizeof(PageIxEntry);
+      ix->entries.resize(eb / sizeof(PageIxEntry));
+      memcpy(ix->entries.data(), O + tab_off, eb);
+      const uint4 *r = (const uint4 *)(O + kIxOutRes);
+      for (int32_t c = 0; c < n_chunks; c++) {
+        ix->chunks[c].status = r[c].x;
+        ix->chunks[c].npages = r[c].y;
+        ix->chunks[c].fail_page = r[c].z;
+      }
+      break;
+    }
     cap = (uint64_t)n * 2 + 4096;
   }
   if (getenv("PQ_IX_DEBUG")) {

@@ -26,13 +26,18 @@
 //                  region (16-B aligned destination, funnel-shifted 16-B stores) with 64 zero
 //                  bytes after it, the layout every decode kernel reads.
 #include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "dev_util.h"
+#include "kernels.h"
 
 namespace pq {
 
 constexpr uint32_t kIxDepth = 24;  // Thrift nesting the walk follows (the host allows 64: deeper -> host)
 constexpr uint32_t kCrcPoly = 0xedb88320u;
+static_assert(kIxArgChunks * sizeof(PageIxChunk) + 64 <= 4096, "chunk table must fit the kernel arguments");
 
 // ---------------------------------------------------------------------------
 // Thrift compact decode from a wave-wide register window
@@ -192,6 +197,15 @@ DEV void tskip_field(TWin &t, int32_t ty, TFrame *stk) {
   if (ty != TC_TRUE && ty != TC_FALSE) tskip(t, ty, 1, stk);
 }
 
+// arr[k] = v with constant indices only, so the header stays in registers (a dynamically indexed
+// member array would put the whole entry in scratch memory)
+template <int N>
+DEV void set_field(int32_t (&arr)[N], int32_t k, int32_t v) {
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if (k == j) arr[j] = v;
+}
+
 // ParsePageHeader (format.cpp; the generated PageHeader.Read with its required-field checks)
 DEV bool parse_page_header(TWin &t, PageIxEntry &h, TFrame *stk) {
   int32_t last = 0, id, ty;
@@ -211,7 +225,7 @@ DEV bool parse_page_header(TWin &t, PageIxEntry &h, TFrame *stk) {
       int32_t l2 = 0, i2, t2;
       uint32_t set = 0;
       while (tfield(t, l2, i2, t2)) {
-        if (i2 >= 1 && i2 <= 4 && t2 == TC_I32) { h.dph[i2 - 1] = ti32(t); set |= 1u << i2; }
+        if (i2 >= 1 && i2 <= 4 && t2 == TC_I32) { set_field(h.dph, i2 - 1, ti32(t)); set |= 1u << i2; }
         else tskip_field(t, t2, stk);
       }
       if (!t.err && set != 0x1e) t.err = true;
@@ -220,7 +234,7 @@ DEV bool parse_page_header(TWin &t, PageIxEntry &h, TFrame *stk) {
       int32_t l2 = 0, i2, t2;
       uint32_t set = 0;
       while (tfield(t, l2, i2, t2)) {
-        if (i2 >= 1 && i2 <= 2 && t2 == TC_I32) { h.dict[i2 - 1] = ti32(t); set |= 1u << i2; }
+        if (i2 >= 1 && i2 <= 2 && t2 == TC_I32) { set_field(h.dict, i2 - 1, ti32(t)); set |= 1u << i2; }
         else tskip_field(t, t2, stk);
       }
       if (!t.err && set != 0x6) t.err = true;
@@ -233,7 +247,7 @@ DEV bool parse_page_header(TWin &t, PageIxEntry &h, TFrame *stk) {
           const int32_t v = ti32(t);
           set |= 1u << i2;
           // PageHeader field order 1..6: num_values, num_nulls, num_rows, encoding, def_len, rep_len
-          h.dph2[i2 - 1] = v;
+          set_field(h.dph2, i2 - 1, v);
         } else if (i2 == 7 && (t2 == TC_TRUE || t2 == TC_FALSE)) {
           h.flags = t2 == TC_TRUE ? (h.flags | IXF_COMPRESSED) : (h.flags & ~IXF_COMPRESSED);
         } else tskip_field(t, t2, stk);
@@ -246,15 +260,19 @@ DEV bool parse_page_header(TWin &t, PageIxEntry &h, TFrame *stk) {
 }
 
 // One wavefront per chunk: the header chain of readPages.
+// The chunk table travels in the kernel arguments (kIxArgChunks per launch); results go to `res`.
+struct IxChunkArgs {
+  PageIxChunk c[kIxArgChunks];
+};
+
 __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t len, int64_t file_off,
-                                                  PageIxChunk *chunks_in, PageIxEntry *table_in, uint32_t *table_n,
-                                                  uint32_t table_cap) {
+                                                  const IxChunkArgs args, uint32_t chunk0, uint4 *res_in,
+                                                  PageIxEntry *table_in, uint32_t *table_n, uint32_t table_cap) {
   __shared__ TFrame stk[kIxDepth];
   const uint8_t *buf = gp(buf_in);
-  PageIxChunk *chunks = gp(chunks_in);
   PageIxEntry *table = gp(table_in);
-  const uint32_t c = blockIdx.x, lane = lane_id();
-  const PageIxChunk ch = chunks[c];
+  const uint32_t c = chunk0 + blockIdx.x, lane = lane_id();
+  const PageIxChunk ch = args.c[blockIdx.x];
   TWin t;
   t.buf = buf;
   t.len = len;
@@ -311,11 +329,7 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     }
   }
   if (status == IX_OK && seq > flushed && !flush(seq - flushed)) status = IX_FALLBACK;
-  if (lane == 0) {
-    chunks[c].status = status;
-    chunks[c].npages = status == IX_OK ? seq : 0;
-    chunks[c].fail_page = seq;
-  }
+  if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -425,14 +439,55 @@ __global__ void __launch_bounds__(256) k_page_gather(const GatherJob *jobs_in, u
   }
 }
 
-hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, PageIxChunk *chunks, uint32_t nchunks,
-                            PageIxEntry *table, uint32_t *table_n, uint32_t table_cap, int validate_crc,
-                            hipStream_t s) {
+// Before the walk: the entry counter to zero, every chunk's result to IX_FALLBACK (a chunk whose
+// walk never reports stays with the host)
+__global__ void __launch_bounds__(256) k_page_walk_init(uint32_t *table_n, uint4 *res, uint32_t nchunks) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) *gp(table_n) = 0;
+  if (t < nchunks) gp(res)[t] = make_uint4(IX_FALLBACK, 0u, 0u, 0u);
+}
+
+hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, const PageIxChunk *chunks,
+                            uint32_t nchunks, uint4 *res, PageIxEntry *table, uint32_t *table_n, uint32_t table_cap,
+                            int validate_crc, hipStream_t s) {
   if (!nchunks) return hipSuccess;
-  hipLaunchKernelGGL(k_page_walk, dim3(nchunks), dim3(64), 0, s, buf, len, file_off, chunks, table, table_n, table_cap);
+  hipLaunchKernelGGL(k_page_walk_init, dim3((nchunks + 255) / 256), dim3(256), 0, s, table_n, res, nchunks);
+  for (uint32_t c0 = 0; c0 < nchunks; c0 += kIxArgChunks) {
+    const uint32_t n = std::min<uint32_t>(kIxArgChunks, nchunks - c0);
+    IxChunkArgs a;
+    memset(&a, 0, sizeof(a));
+    memcpy(a.c, chunks + c0, n * sizeof(PageIxChunk));
+    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap);
+  }
   if (validate_crc)
     hipLaunchKernelGGL(k_page_crc, dim3(2048), dim3(kCrcThreads), 0, s, buf, len, file_off, table,
                        (const uint32_t *)table_n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Results to the host: the entry count, the per-chunk results and the table, written by the GPU
+// straight into page-locked host memory (no D2H copy reads the device-side table)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_page_export(const uint32_t *table_n_in, const PageIxEntry *table_in,
+                                                     uint32_t table_cap, const uint4 *res_in, uint32_t nchunks,
+                                                     uint8_t *out) {
+  const uint32_t n = *gp(table_n_in);
+  const uint32_t ne = min(n, table_cap);
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  uint4 *o = (uint4 *)gp(out);
+  if (tid == 0) o[0] = make_uint4(n, 0u, 0u, 0u);
+  const uint4 *res = gp(res_in);
+  for (uint32_t c = tid; c < nchunks; c += nth) o[kIxOutRes / 16 + c] = res[c];
+  const uint4 *t = (const uint4 *)gp(table_in);
+  uint4 *ot = o + ix_out_table_off(nchunks) / 16;
+  const uint64_t words = (uint64_t)ne * (sizeof(PageIxEntry) / 16);
+  for (uint64_t k = tid; k < words; k += nth) ot[k] = t[k];
+}
+
+hipError_t launch_page_export(const uint32_t *table_n, const PageIxEntry *table, uint32_t table_cap, const uint4 *res,
+                              uint32_t nchunks, uint8_t *host_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_page_export, dim3(64), dim3(256), 0, s, table_n, table, table_cap, res, nchunks, host_out);
   return hipGetLastError();
 }
 
