@@ -11,41 +11,42 @@ struct pqgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
-  // page-locked staging kept between calls (small DMA tables of the page index build):
-  // hipHostMalloc costs far more than the copies it serves
-  std::mutex pin_m;
-  std::vector<std::pair<void *, size_t>> pin_free;
+  // Device scratch of the page index builds, kept between calls (hipMalloc'd: kernel stores into
+  // stream-ordered hipMallocAsync memory from workgroups off the first XCD were observed never to
+  // reach a later device-to-host copy of it)
+  std::mutex scratch_m;
+  std::vector<std::pair<void *, size_t>> scratch_free;
 
-  void *pin_get(size_t want, size_t *cap) {
+  void *scratch_get(size_t want, size_t *cap) {
     {
-      std::lock_guard<std::mutex> lk(pin_m);
-      for (size_t k = 0; k < pin_free.size(); k++)
-        if (pin_free[k].second >= want) {
-          void *p = pin_free[k].first;
-          *cap = pin_free[k].second;
-          pin_free.erase(pin_free.begin() + (long)k);
+      std::lock_guard<std::mutex> lk(scratch_m);
+      for (size_t k = 0; k < scratch_free.size(); k++)
+        if (scratch_free[k].second >= want) {
+          void *p = scratch_free[k].first;
+          *cap = scratch_free[k].second;
+          scratch_free.erase(scratch_free.begin() + (long)k);
           return p;
         }
     }
-    size_t c = 4096;
+    size_t c = 1 << 16;
     while (c < want) c *= 2;
     void *p = nullptr;
-    if (hipHostMalloc(&p, c, hipHostMallocCoherent) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) return nullptr;
     *cap = c;
     return p;
   }
-  void pin_put(void *p, size_t cap) {
+  void scratch_put(void *p, size_t cap) {
     if (!p) return;
-    std::lock_guard<std::mutex> lk(pin_m);
-    if (pin_free.size() < 16) {
-      pin_free.emplace_back(p, cap);
+    std::lock_guard<std::mutex> lk(scratch_m);
+    if (scratch_free.size() < 16) {
+      scratch_free.emplace_back(p, cap);
       return;
     }
-    (void)hipHostFree(p);
+    (void)hipFree(p);
   }
-  void pin_release() {
-    std::lock_guard<std::mutex> lk(pin_m);
-    for (auto &b : pin_free) (void)hipHostFree(b.first);
-    pin_free.clear();
+  void scratch_release() {
+    std::lock_guard<std::mutex> lk(scratch_m);
+    for (auto &b : scratch_free) (void)hipFree(b.first);
+    scratch_free.clear();
   }
 };

@@ -2031,7 +2031,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
-  c->pin_release();
+  c->scratch_release();
   delete c;
 }
 
@@ -2244,54 +2244,54 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
   }
   if (n_chunks == 0) { *out = ix.release(); return PQ_OK; }
   // table capacity: a page per 4 KiB plus 64 per chunk; a walk that outgrows it is rerun larger.
-  // One launch sequence and one synchronisation per build: the chunk table rides in the kernel
-  // arguments, and k_page_export writes the entry count, the per-chunk results and the table
-  // straight into page-locked host memory (reused from the context's pool).
-  struct Pinned {
-    pqgpu_ctx *c;
-    void *p = nullptr;
-    size_t cap = 0;
-    explicit Pinned(pqgpu_ctx *x) : c(x) {}
-    ~Pinned() { c->pin_put(p, cap); }
-  };
+  // The chunk table rides in the kernel arguments; the count, the per-chunk results and the table
+  // come back by device-to-host copies after the stream has drained, from hipMalloc'd scratch.
   const size_t res_bytes = align_up((uint64_t)n_chunks * sizeof(uint4), 256);
-  const uint64_t tab_off = ix_out_table_off((uint32_t)n_chunks);
   uint32_t n = 0;
   for (int attempt = 0;; attempt++) {
     cap = std::min<uint64_t>(cap, 1u << 26);
-    void *d = nullptr;
+    size_t dcap = 0;
     const size_t bytes = 256 + res_bytes + cap * sizeof(PageIxEntry);
-    Pinned h_out(ctx);
-    h_out.p = ctx->pin_get(tab_off + cap * sizeof(PageIxEntry) + 64, &h_out.cap);
-    if (!h_out.p) HIPCHECK(hipErrorOutOfMemory, err);
-    uint8_t *o_dev = nullptr;
-    HIPCHECK(hipHostGetDevicePointer((void **)&o_dev, h_out.p, 0), err);
-    HIPCHECK(hipMallocAsync(&d, bytes, s), err);
+    void *d = ctx->scratch_get(bytes, &dcap);
+    if (!d) HIPCHECK(hipErrorOutOfMemory, err);
     uint8_t *D = (uint8_t *)d;
     uint32_t *d_n = (uint32_t *)D;
     uint4 *d_res = (uint4 *)(D + 256);
     PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + res_bytes);
-    hipError_t he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, ix->chunks.data(), (uint32_t)n_chunks, d_res,
-                            d_tab, d_n, (uint32_t)cap, validate_crc, s);
-    if (he == hipSuccess) he = launch_page_export(d_n, d_tab, (uint32_t)cap, d_res, (uint32_t)n_chunks, o_dev, s);
+    hipError_t he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, ix->chunks.data(), (uint32_t)n_chunks,
+                                     d_res, d_tab, d_n, (uint32_t)cap, validate_crc, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
-    (void)hipFreeAsync(d, s);
-    HIPCHECK(he, err);
-    const uint8_t *O = (const uint8_t *)h_out.p;
-    n = *(const uint32_t *)O;
-    const bool grow = n > cap && cap < (1u << 26) && attempt < 3;
-    if (!grow) {
-      const size_t eb = (size_t)std::min<uint64_t>(n, cap) * sizeof(PageIxEntry);
-      ix->entries.resize(eb / sizeof(PageIxEntry));
-      memcpy(ix->entries.data(), O + tab_off, eb);
-      const uint4 *r = (const uint4 *)(O + kIxOutRes);
-      for (int32_t c = 0; c < n_chunks; c++) {
-        ix->chunks[c].status = r[c].x;
-        ix->chunks[c].npages = r[c].y;
-        ix->chunks[c].fail_page = r[c].z;
-      }
-      break;
+    // every chunk's walk must have reported before the count and the table are read (a safety net:
+    // with hipMallocAsync scratch, results of workgroups off the first XCD never arrived)
+    std::vector<uint4> r((size_t)n_chunks);
+    int polls = 0;
+    for (; he == hipSuccess; polls++) {
+      he = hipMemcpy(r.data(), d_res, (size_t)n_chunks * sizeof(uint4), hipMemcpyDeviceToHost);
+      bool all = true;
+      for (int32_t c = 0; c < n_chunks && all; c++) all = r[c].w == kIxDone;
+      if (all || polls >= 200) break;
+      he = hipDeviceSynchronize();
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+    if (polls && getenv("PQ_IX_DEBUG")) fprintf(stderr, "[ix] results complete after %d polls\n", polls);
+    if (he == hipSuccess) he = hipMemcpy(&n, d_n, 4, hipMemcpyDeviceToHost);
+    const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < 3;
+    if (he == hipSuccess && !grow) {
+      const size_t ne = (size_t)std::min<uint64_t>(n, cap);
+      ix->entries.resize(ne);
+      if (ne) he = hipMemcpy(ix->entries.data(), d_tab, ne * sizeof(PageIxEntry), hipMemcpyDeviceToHost);
+      if (he == hipSuccess)
+        for (int32_t c = 0; c < n_chunks; c++) {
+          const bool rep = r[c].w == kIxDone;  // a chunk that never reported stays with the host
+          ix->chunks[c].status = rep ? r[c].x : IX_FALLBACK;
+          ix->chunks[c].npages = rep ? r[c].y : 0;
+          ix->chunks[c].fail_page = r[c].z;
+        }
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(s);  // the scratch is free for the next build
+    ctx->scratch_put(d, dcap);
+    HIPCHECK(he, err);
+    if (!grow) break;
     cap = (uint64_t)n * 2 + 4096;
   }
   if (getenv("PQ_IX_DEBUG")) {

@@ -115,18 +115,11 @@ hipError_t launch_plain_ba(const BatchDev &b, const PbaLists &l, hipStream_t s);
 // The chunk table is host memory: it reaches the walk in the kernel arguments, kIxArgChunks chunks
 // per launch (never through a DMA copy the walk would read); res[c] = (status, npages, fail_page, 0).
 constexpr uint32_t kIxArgChunks = 64;
+constexpr uint32_t kIxDone = 0x600d0001u;  // res[c].w once chunk c's walk has reported
 hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, const PageIxChunk *chunks,
                             uint32_t nchunks, uint4 *res, PageIxEntry *table, uint32_t *table_n, uint32_t table_cap,
                             int validate_crc, hipStream_t s);
 hipError_t launch_page_gather(const GatherJob *jobs, uint32_t njobs, hipStream_t s);
-// The walk's results written by the GPU into page-locked host memory `host_out`: the entry count
-// at 0, res[c] at kIxOutRes, the min(count, cap) entries at ix_out_table_off(nchunks).
-constexpr uint32_t kIxOutRes = 256;
-constexpr uint64_t ix_out_table_off(uint32_t nchunks) {
-  return (kIxOutRes + (uint64_t)nchunks * 16 + 255) / 256 * 256;
-}
-hipError_t launch_page_export(const uint32_t *table_n, const PageIxEntry *table, uint32_t table_cap, const uint4 *res,
-                              uint32_t nchunks, uint8_t *host_out, hipStream_t s);
 
 // Names of the kernels, for the timing hook.
 extern const char *kValuesKernelName;

@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     }
   }
   if (status == IX_OK && seq > flushed && !flush(seq - flushed)) status = IX_FALLBACK;
-  if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, 0u);
+  if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, kIxDone);
 }
 
 // ---------------------------------------------------------------------------
@@ -462,32 +462,6 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
   if (validate_crc)
     hipLaunchKernelGGL(k_page_crc, dim3(2048), dim3(kCrcThreads), 0, s, buf, len, file_off, table,
                        (const uint32_t *)table_n);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Results to the host: the entry count, the per-chunk results and the table, written by the GPU
-// straight into page-locked host memory (no D2H copy reads the device-side table)
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_page_export(const uint32_t *table_n_in, const PageIxEntry *table_in,
-                                                     uint32_t table_cap, const uint4 *res_in, uint32_t nchunks,
-                                                     uint8_t *out) {
-  const uint32_t n = *gp(table_n_in);
-  const uint32_t ne = min(n, table_cap);
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-  uint4 *o = (uint4 *)gp(out);
-  if (tid == 0) o[0] = make_uint4(n, 0u, 0u, 0u);
-  const uint4 *res = gp(res_in);
-  for (uint32_t c = tid; c < nchunks; c += nth) o[kIxOutRes / 16 + c] = res[c];
-  const uint4 *t = (const uint4 *)gp(table_in);
-  uint4 *ot = o + ix_out_table_off(nchunks) / 16;
-  const uint64_t words = (uint64_t)ne * (sizeof(PageIxEntry) / 16);
-  for (uint64_t k = tid; k < words; k += nth) ot[k] = t[k];
-}
-
-hipError_t launch_page_export(const uint32_t *table_n, const PageIxEntry *table, uint32_t table_cap, const uint4 *res,
-                              uint32_t nchunks, uint8_t *host_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_page_export, dim3(64), dim3(256), 0, s, table_n, table, table_cap, res, nchunks, host_out);
   return hipGetLastError();
 }
 
