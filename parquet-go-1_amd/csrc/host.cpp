@@ -439,6 +439,8 @@ struct pqgpu_batch {
   // until upload, which places their output in a region after the stage.
   struct DevSnappy {
     uint64_t comp_off, raw_off;  // stage offsets: the block (then >= 128 zero bytes), the raw prefix
+    int64_t comp_gather = -1;    // page index: the gather job that copies the resident block
+                                 // device to device at upload (not staged on the host)
     uint32_t comp_len, vlen;     // block bytes, preamble bytes
     uint32_t raw_len, dlen;      // V2 level bytes, decoded length
     uint32_t page;               // global page index
@@ -739,6 +741,7 @@ struct IxChunkView {
   uint32_t n;
   uint64_t dev;          // device address of file byte `file_off`
   int64_t file_off;
+  int64_t len;           // resident bytes
 };
 
 static void ix_header(const PageIxEntry &x, PageHeader *ph) {
@@ -922,12 +925,21 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
       pqgpu_batch::DevSnappy j;
       j.raw_off = stage_append(b, block.data(), (int64_t)block.size());
       j.raw_len = (uint32_t)block.size();
-      j.comp_off = stage_append(b, sd.blk, sd.len);
       j.comp_len = (uint32_t)sd.len;
       j.vlen = (uint32_t)(sp.src - sd.blk);
       j.dlen = (uint32_t)sd.dlen;
       j.page = (uint32_t)b->pages.size();
-      b->stage.resize(b->stage.size() + 128, 0);  // k_snappy reads up to 70 bytes past the block
+      const int64_t at = (int64_t)(sd.blk - file) - (ix ? ix->file_off : 0);
+      if (ix && at >= 0 && at + sd.len <= ix->len) {
+        // page index: the block is already in HBM; k_page_gather copies it into the batch at
+        // upload (the resident bytes are needed only until then), with zero bytes after it
+        j.comp_off = 0;
+        j.comp_gather = (int64_t)b->gathers.size();
+        b->gathers.push_back(pqgpu_batch::HostGather{ix->dev + (uint64_t)at, (uint64_t)sd.len, j.page});
+      } else {
+        j.comp_off = stage_append(b, sd.blk, sd.len);
+        b->stage.resize(b->stage.size() + 128, 0);  // k_snappy reads up to 70 bytes past the block
+      }
       b->snappy.push_back(j);
     };
     auto corrupt_fail = [&]() {
@@ -1505,17 +1517,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.offsets = hc.o_offsets ? dp(hc.o_offsets) : 0;
     cd.ba_index = hc.o_ba_index ? dp(hc.o_ba_index) : 0;
   }
+  std::vector<GatherJob> gjobs(b->gathers.size());
+  for (size_t k = 0; k < gjobs.size(); k++)
+    gjobs[k] = GatherJob{b->gathers[k].src, (uint64_t)(b->d_stage + gat_base + gat_off[k]), b->gathers[k].len};
   std::vector<SnappyJob> jobs(b->snappy.size());
   for (size_t k = 0; k < jobs.size(); k++) {
     const pqgpu_batch::DevSnappy &j = b->snappy[k];
     const PageDesc &pd = b->pages[j.page];
-    jobs[k] = SnappyJob{(uint64_t)(b->d_stage + j.comp_off + j.vlen), (uint64_t)(b->d_stage + j.raw_off),
-                        (uint64_t)(b->d_stage + dec_base + dec_off[k]), j.comp_len - j.vlen, j.raw_len, j.dlen,
-                        pd.chunk, pd.page_in_chunk, 0};
+    const uint64_t comp = j.comp_gather >= 0 ? gjobs[(size_t)j.comp_gather].dst : (uint64_t)(b->d_stage + j.comp_off);
+    jobs[k] = SnappyJob{comp + j.vlen, (uint64_t)(b->d_stage + j.raw_off), (uint64_t)(b->d_stage + dec_base + dec_off[k]),
+                        j.comp_len - j.vlen, j.raw_len, j.dlen, pd.chunk, pd.page_in_chunk, 0};
   }
-  std::vector<GatherJob> gjobs(b->gathers.size());
-  for (size_t k = 0; k < gjobs.size(); k++)
-    gjobs[k] = GatherJob{b->gathers[k].src, (uint64_t)(b->d_stage + gat_base + gat_off[k]), b->gathers[k].len};
   std::vector<PageDesc> pages = b->pages;
   for (auto &pd : pages)
     pd.data = (pd.flags & PF_DEV_SNAPPY)   ? jobs[pd.data].dst
@@ -2350,7 +2362,7 @@ int pqgpu_batch_add_indexed_chunk(pqgpu_batch *b, const pqgpu_page_index *ix, in
   if (ix->chunks[ix_chunk].status != IX_OK)  // the walk did not take it: the host walks the chunk
     return add_chunk_impl(b, file_bytes, (int64_t)file_len, col, &cm, validate_crc, chunk_id, err);
   IxChunkView v{ix->entries.data() + ix->first[ix_chunk], ix->first[ix_chunk + 1] - ix->first[ix_chunk], ix->dev,
-                ix->file_off};
+                ix->file_off, ix->len};
   return add_chunk_impl(b, file_bytes, (int64_t)file_len, col, &cm, validate_crc, chunk_id, err, &v);
 }
 

@@ -2840,10 +2840,14 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
   // to 4 B). W1 is loaded one window ahead, so the walk does not wait on HBM every 64 bytes.
   const uint32_t sa0 = (uint32_t)((uintptr_t)src & 3);
   const uint32_t *srcw = (const uint32_t *)(src - sa0);
-  const uint32_t wlim = n + sa0 + 64;  // dwords below this are inside the block's zero padding
+  // bytes past the block read as zero whatever follows it (a staged block is followed by zero
+  // padding; a resident one, page index, by the next page): the partial last dword is masked
+  const uint32_t wlim = n + sa0;
   auto ldw = [&](uint32_t at) -> uint32_t {  // the dword at aligned offset at + 4 * lane
     const uint32_t k = at + 4 * lane;
-    return k < wlim ? srcw[k >> 2] : 0u;
+    if (k >= wlim) return 0u;
+    const uint32_t w = srcw[k >> 2];
+    return k + 4 <= wlim ? w : w & ((1u << (8 * (wlim - k))) - 1u);
   };
   uint32_t wb = 0, W0 = ldw(0), W1 = ldw(256);
   PQ_STAMPS(sp, b.dbg);
