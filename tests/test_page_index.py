@@ -262,6 +262,33 @@ def test_partial_residency_falls_back(gpu_ctx):
     b.close()
 
 
+@pytest.mark.parametrize("name", ["cfg5_small", "cfg2_snappy_v1", "dba_v1_snappy"])
+def test_indexed_snappy_decoded_twice_after_release(gpu_ctx, name):
+    """SNAPPY blocks of indexed chunks are gathered from the resident bytes at upload; the index and
+    its device buffer are released before the first decode, and a second decode of the same batch
+    (the bench's pattern) still equals the oracle."""
+    data = pqtest.load(name)
+    f = pqgpu.File(data)
+    chunks = _all_chunks(f)
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, chunks, whole_file=True)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = []
+    for k, (rg, c) in enumerate(chunks):
+        cid, e = b.add_indexed_chunk(ix, k, f, c)
+        ids.append(cid)
+    b.upload()
+    ix.close()
+    orc = pqtest.oracle_decode(data)
+    for rep in range(2):
+        b.decode()
+        b.sync()
+        for (rg, c, r), cid in zip(orc, ids):
+            if isinstance(r, O.OracleError):
+                continue
+            pqtest.assert_chunk_equal(b.result(cid), r, f"{name} pass {rep} rg{rg} c{c}")
+    b.close()
+
+
 def test_must_not_crash_indexed(gpu_ctx):
     """The reference's fuzz regression images through the indexed path: the oracle's outcome."""
     d = os.path.join(pqtest.GOLDEN, "must_not_crash")
