@@ -2194,35 +2194,43 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
       } else if (__ballot(valid && d0 + 8 <= stop) == ~0ull) {
         // the wave's 64 groups are 512 consecutive values: transpose through LDS so that every
         // store instruction writes 1 KiB contiguous (16 B per lane) instead of 64 B-strided pieces
+        // Piece e (16 B) of the wave's output is held by lane e / vw as its piece e % vw; it sits in
+        // LDS slot xsw(e): the piece index within the lane is XOR-swizzled with lane bits so that
+        // the 16-B writes of 16 (int64) / 8 (int32) consecutive lanes cover all 64 banks (lanes
+        // 64 B / 32 B apart would otherwise meet in the same banks, 4- / 2-way).
         uint4 *xw = L.xpose[wv];
         const uint32_t vw = is64 ? 4u : 2u;  // uint4 per lane
+        auto xsw = [&](uint32_t e) -> uint32_t {
+          return is64 ? (e & ~3u) | ((e ^ (e >> 4)) & 3u) : (e & ~1u) | ((e ^ (e >> 4)) & 1u);
+        };
         if (is64) {
 #pragma unroll
           for (int q = 0; q < 4; q++)
-            xw[lane * 4 + q] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
-                                          (uint32_t)(out[2 * q + 1] >> 32));
+            xw[xsw(lane * 4 + q)] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
+                                               (uint32_t)(out[2 * q + 1] >> 32));
         } else {
-          xw[lane * 2] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
-          xw[lane * 2 + 1] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
+          xw[xsw(lane * 2)] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
+          xw[xsw(lane * 2 + 1)] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
         }
         asm volatile("" ::: "memory");  // same wave: LDS executes its accesses in order
         const uint32_t wd0 = rdlane(d0, 0);
         uint8_t *dst0 = ds.out + (uint64_t)wd0 * (is64 ? 8 : 4);
         if (al16) {
           uint4 *dst = (uint4 *)dst0;
-          for (uint32_t q = 0; q < vw; q++) dst[q * 64 + lane] = xw[q * 64 + lane];
+          for (uint32_t q = 0; q < vw; q++) dst[q * 64 + lane] = xw[xsw(q * 64 + lane)];
         } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
           const uint32_t bytes = vw * 1024, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
           const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;
           const uint32_t *xs = (const uint32_t *)xw;
+          auto xd = [&](uint32_t D) -> uint32_t { return xs[xsw(D >> 2) * 4 + (D & 3)]; };  // dword D
           uint4 *body = (uint4 *)(dst0 + adj);
           for (uint32_t j = lane; j < nbody; j += 64) {
             const uint32_t o = a4 + 4 * j;
-            body[j] = make_uint4(xs[o], xs[o + 1], xs[o + 2], xs[o + 3]);
+            body[j] = make_uint4(xd(o), xd(o + 1), xd(o + 2), xd(o + 3));
           }
           const uint32_t nt = (bytes - adj - 16 * nbody) >> 2;
-          if (lane < a4) ((uint32_t *)dst0)[lane] = xs[lane];
-          if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xs[a4 + 4 * nbody + lane];
+          if (lane < a4) ((uint32_t *)dst0)[lane] = xd(lane);
+          if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xd(a4 + 4 * nbody + lane);
         }
       } else if (valid) {
         if (d0 + 8 <= stop && al16) {
