@@ -45,20 +45,21 @@ static_assert(kIxArgChunks * sizeof(PageIxChunk) + 64 <= 4096, "chunk table must
 enum { TC_STOP = 0, TC_TRUE = 1, TC_FALSE = 2, TC_BYTE = 3, TC_I16 = 4, TC_I32 = 5, TC_I64 = 6, TC_DOUBLE = 7,
        TC_BINARY = 8, TC_LIST = 9, TC_SET = 10, TC_MAP = 11, TC_STRUCT = 12 };
 
-// Cursor over the resident bytes [0, len) of `buf`; lane l's `w` holds bytes [base + 4l, +4).
-// Every member is wave-uniform.
+// Cursor over the bytes [0, len) of `buf` (one chunk's span of the resident bytes, so positions
+// are 32-bit: the cursor checks compile to scalar compares); lane l's `w` holds bytes
+// [base + 4l, +4). Every member is wave-uniform.
 struct TWin {
   const uint8_t *buf;
-  int64_t len;
-  int64_t base;
+  uint32_t len;
+  uint32_t base;
   uint32_t w;
-  int64_t i;    // next byte (buffer-relative)
+  uint32_t i;   // next byte (span-relative)
   bool err;
 };
 
-DEV void twin_load(TWin &t, int64_t at) {
-  t.base = at & ~(int64_t)3;
-  const int64_t p = t.base + 4 * (int64_t)lane_id();
+DEV void twin_load(TWin &t, uint32_t at) {
+  t.base = at & ~3u;
+  const uint64_t p = (uint64_t)t.base + 4 * lane_id();
   uint32_t w = 0;
   if (p + 4 <= t.len) {
     w = *(const uint32_t *)(t.buf + p);
@@ -71,8 +72,8 @@ DEV void twin_load(TWin &t, int64_t at) {
 
 DEV bool tbyte(TWin &t, uint32_t &b) {
   if (t.err || t.i >= t.len) { t.err = true; return false; }
-  if (t.i < t.base || t.i >= t.base + 256) twin_load(t, t.i);
-  const uint32_t r = (uint32_t)(t.i - t.base);
+  if (t.i - t.base >= 256u) twin_load(t, t.i);  // unsigned: also when i < base
+  const uint32_t r = t.i - t.base;
   b = (rdlane(t.w, r >> 2) >> (8 * (r & 3))) & 0xffu;
   t.i++;
   return true;
@@ -137,7 +138,7 @@ DEV void tskip(TWin &t, int32_t ty, uint32_t depth, TFrame *stk) {
         case TC_BINARY: {
           const int32_t n = (int32_t)tuvarint(t);
           if (t.err) break;
-          if (n < 0 || (int64_t)n > t.len - t.i) { t.err = true; break; }
+          if (n < 0 || (uint32_t)n > t.len - t.i) { t.err = true; break; }
           t.i += n;
           break;
         }
@@ -273,10 +274,14 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
   PageIxEntry *table = gp(table_in);
   const uint32_t c = chunk0 + blockIdx.x, lane = lane_id();
   const PageIxChunk ch = args.c[blockIdx.x];
+  // the chunk's span of the resident bytes: from its first header (or its data pages, when they
+  // come first) to the end, at most 4 GiB - 1 (a walk that needs more falls back)
+  const int64_t first = (ch.data_off >= 0 ? min(ch.start, ch.data_off) : ch.start) - file_off;
+  const int64_t cb = first < 0 ? 0 : min(first, len);
   TWin t;
-  t.buf = buf;
-  t.len = len;
-  t.base = -4096;
+  t.buf = buf + cb;
+  t.len = (uint32_t)min(len - cb, (int64_t)0xffffffffll);
+  t.base = 0xfffff000u;  // no window yet
   t.w = 0;
   t.err = false;
   int64_t off = ch.start, count = 0;
@@ -292,13 +297,13 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     return true;
   };
   while (ch.total - count > 0) {
-    const int64_t rel = off - file_off;
-    if (rel < 0 || rel >= len) { status = IX_FALLBACK; break; }
+    const int64_t rel = off - file_off - cb;
+    if (rel < 0 || rel >= (int64_t)t.len) { status = IX_FALLBACK; break; }
     PageIxEntry h;
-    t.i = rel;
+    t.i = (uint32_t)rel;
     t.err = false;
     if (!parse_page_header(t, h, stk)) { status = IX_FALLBACK; break; }
-    const int64_t hl = t.i - rel;
+    const int64_t hl = (int64_t)(t.i - (uint32_t)rel);
     off += hl;
     count += hl;
     // readPageBlock: the whole block must be resident (a short block is the host's error)
