@@ -2781,7 +2781,10 @@ DEV bool snappy_batch(SnappyOut &o, uint16_t *st, uint64_t batch, uint32_t P, ui
         if ((pe[k] & 3) == 0) {
           sv = kSnRes | lb[k];
         } else if (j >= ve[k]) {
-          sv = j - ve[k];  // an earlier byte of this batch
+          // an earlier byte of this batch; inside an overlapping copy (offset < its length) byte j
+          // repeats byte Oe - d + (j - Oe) mod d, before the element: one hop instead of a chain
+          const uint32_t d = ve[k], r = j - Oe[k];
+          sv = (r >= d && Oe[k] >= d) ? Oe[k] - d + r % d : j - d;
         } else if (ve[k] + T <= kSnappyRing) {
           sv = kSnRes | o.ring[(P + j - ve[k]) & kRingMask];  // page byte before the batch, in the ring
         } else {
