@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 5
+#define PQGPU_ABI_VERSION 6
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -247,6 +247,12 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
 int pqgpu_page_index_chunk(const pqgpu_page_index *ix, int32_t chunk, int32_t *num_pages, int32_t *status);
 int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, pqgpu_page_header *out);
 double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix);
+/* How the build went: result read-backs beyond the first (some chunk's completion marker, a
+ * per-build generation, was not yet visible), chunks that never reported (walked by the host),
+ * chunks that fell back for any reason, and 1 when the header table overflowed its largest size
+ * (every chunk then falls back). */
+int pqgpu_page_index_stats(const pqgpu_page_index *ix, int32_t *polls, int32_t *unreported, int32_t *fallback_chunks,
+                           int32_t *overflowed);
 void pqgpu_page_index_destroy(pqgpu_page_index *ix);
 /* The host's PageHeader decode (the same fields), for comparison. */
 int pqgpu_parse_page_header(const uint8_t *buf, size_t len, pqgpu_page_header *out, int64_t *consumed);
@@ -315,7 +321,7 @@ int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
 int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
 /* The same for every timed launch slot (0 <= slot < PQGPU_TIMER_SLOTS); PQ_ERR_ARG past the end. */
-#define PQGPU_TIMER_SLOTS 20
+#define PQGPU_TIMER_SLOTS 21
 int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
                             size_t name_len);
 /* Algorithmic bytes (sections read + outputs written, counted once) of one launch

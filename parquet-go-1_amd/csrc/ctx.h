@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -11,10 +12,17 @@ struct pqgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
+  hipStream_t copy = nullptr;  // PLAIN / BOOLEAN copies (k_values_copy) beside both
   // Device scratch of the page index builds, kept between calls (hipMalloc'd: kernel stores into
   // stream-ordered hipMallocAsync memory from workgroups off the first XCD were observed never to
   // reach a later device-to-host copy of it)
   std::mutex scratch_m;
+  std::atomic<uint32_t> ix_gen{0};  // page index builds: completion-marker generation (never 0)
+  uint32_t next_ix_gen() {
+    uint32_t g;
+    do g = ++ix_gen; while (g == 0);
+    return g;
+  }
   std::vector<std::pair<void *, size_t>> scratch_free;
 
   void *scratch_get(size_t want, size_t *cap) {

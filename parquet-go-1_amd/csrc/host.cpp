@@ -370,7 +370,8 @@ struct KernelTimer {
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
-    "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather"};
+    "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
+    "k_values_copy"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -484,7 +485,10 @@ struct pqgpu_batch {
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // PQ_COPY_FUSED=1: PLAIN / BOOLEAN copies inside k_values (the round-2 single grid), for comparison
+  bool copy_fused = getenv("PQ_COPY_FUSED") && atoi(getenv("PQ_COPY_FUSED")) != 0;
+  uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr;
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
   uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
@@ -777,6 +781,9 @@ struct pqgpu_page_index {
   std::vector<PageIxEntry> entries;  // grouped by chunk, page order
   std::vector<uint32_t> first;       // [nchunks + 1] each chunk's entries
   double walk_ms = 0;                // walk (+ checksums) on the device, incl. the table read-back
+  int32_t polls = 0;                 // result read-backs beyond the first (a chunk's marker was missing)
+  int32_t unreported = 0;            // chunks whose walk never reported (kept with the host walk)
+  int32_t overflowed = 0;            // 1: the table could not hold every header (every chunk falls back)
 };
 
 static void to_public(const PageIxEntry &x, pqgpu_page_header *o) {
@@ -1344,14 +1351,21 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_end = a;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the bandwidth-bound tiles
-  auto rank = [](uint8_t k) { return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : 2; };
+  // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (their own
+  // zero-LDS launch, k_values_copy, on the copy stream)
+  const bool fused = b->copy_fused;
+  auto rank = [fused](uint8_t k) {
+    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : (!fused && (k == WI_PLAIN || k == WI_BOOL)) ? 3 : 2;
+  };
   std::stable_sort(b->items.begin(), b->items.end(),
                    [&](const WorkItem &x, const WorkItem &y) { return rank(x.kind) < rank(y.kind); });
   b->n_delta_items = 0;
   b->n_delta_tiles = 0;
+  b->n_copy_items = 0;
   for (auto &it : b->items) {
     b->n_delta_items += it.kind == WI_DELTA || it.kind == WI_DELTA_TILE || it.kind == WI_DELTA_PAGE;
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
+    b->n_copy_items += rank(it.kind) == 3;
   }
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
@@ -1661,7 +1675,9 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.base_chunks = (const uint32_t *)(A + b->l_base);
   l.n_base_chunks = (uint32_t)b->base_chunks.size();
   l.items = (const WorkItem *)(A + b->o_items);
-  l.n_items = (uint32_t)b->items.size();
+  l.n_items = (uint32_t)b->items.size() - b->n_copy_items;
+  l.copy_items = l.items + l.n_items;
+  l.n_copy_items = b->n_copy_items;
   l.ba_chunks = (const uint32_t *)(A + b->l_ba);
   l.n_ba_chunks = (uint32_t)b->ba_chunks.size();
   l.n_ba_tiles = (uint32_t)b->ba_tile_page.size();
@@ -1726,6 +1742,18 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   l1.n_items = b->n_delta_items;
   l2.items = l.items + b->n_delta_items;
   l2.n_items = l.n_items - b->n_delta_items;
+  // PLAIN / BOOLEAN copies (k_values_copy) run on the copy stream beside everything else once
+  // their value bases are known: at the start in speculative mode, after k_bases otherwise.
+  hipStream_t cs = b->ctx->copy;
+  if (!b->ev_copy) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming), err);
+  if (!b->ev_copy_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy_join, hipEventDisableTiming), err);
+  auto fork_copies = [&]() -> hipError_t {
+    hipError_t e = hipEventRecord(b->ev_copy, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, b->ev_copy, 0);
+    if (e == hipSuccess) e = timed(b, 20, cs, l.n_copy_items, [&] { return launch_values_copy(d, l, cs); });
+    if (e == hipSuccess) e = hipEventRecord(b->ev_copy_join, cs);
+    return e;
+  };
   if (b->spec) {
     // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
     // side stream concurrently with the level decode; k_bases then checks the header counts
@@ -1740,6 +1768,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
     HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
     HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
+    HIPCHECK(fork_copies(), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
     HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
@@ -1748,10 +1777,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(fork_copies(), err);
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
     HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
     if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items as two launches (profiling)
@@ -1764,6 +1795,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
   }
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
@@ -1929,6 +1961,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         const PageDesc &pd = b->pages[p];
         lvl_bytes += pd.rep_len + pd.def_len;
         if (pd.vkind == VK_DELTA32 || pd.vkind == VK_DELTA64) dl_bytes += pd.val_len + (int64_t)nn[p] * w;
+        if (!b->copy_fused && (pd.vkind == VK_PLAIN_FIXED || pd.vkind == VK_PLAIN_INT96 || pd.vkind == VK_PLAIN_BOOL))
+          kb[20] += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_PLAIN_BOOL ? 1 : w);  // k_values_copy
         if (pd.vkind == VK_DICT || pd.vkind == VK_RLE_BOOL) kb[2] += pd.val_len;  // k_scan_runs: index streams
         if (w == 0 && pd.vkind == VK_DICT) {
           if (hc.ba_sync) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices (CF_BA_SYNC chunks)
@@ -1974,7 +2008,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   kb[0] = lvl_bytes;
   kb[1] = dl_bytes;
-  kb[9] = val_bytes;
+  kb[9] = val_bytes - kb[20];  // k_values: the LDS kinds (DELTA, dictionary tiles)
   kb[8] = val_bytes - dl_bytes;
   kb[11] = b->stats.snappy_kernel_bytes;
   memcpy(b->slot_bytes, kb, sizeof(kb));
@@ -2028,8 +2062,10 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   c->device = device;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
     set_err(err, PQ_ERR_HIP, -1, -1, hipGetErrorString(e));
     return PQ_ERR_HIP;
@@ -2043,6 +2079,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->copy) (void)hipStreamDestroy(c->copy);
   c->scratch_release();
   delete c;
 }
@@ -2143,9 +2180,12 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   (void)hipSetDevice(b->ctx->device);
   (void)hipStreamSynchronize(b->ctx->stream);
   (void)hipStreamSynchronize(b->ctx->side);
+  (void)hipStreamSynchronize(b->ctx->copy);
   free_payloads(b);
   if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+  if (b->ev_copy) (void)hipEventDestroy(b->ev_copy);
+  if (b->ev_copy_join) (void)hipEventDestroy(b->ev_copy_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);
@@ -2244,6 +2284,12 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
   ix->metas.assign(metas, metas + n_chunks);
   ix->chunks.resize(n_chunks);
   uint64_t cap = 4096;
+  // test knobs: PQ_IX_CAP forces the first table capacity (drives the grow path; PQ_IX_NOGROW=1
+  // the overflow path),
+  // PQ_IX_POOL=1 takes the scratch from the stream-ordered pool (the DESIGN.md §9 experiment)
+  const char *cap_env = getenv("PQ_IX_CAP");
+  const bool use_pool = getenv("PQ_IX_POOL") && atoi(getenv("PQ_IX_POOL")) == 1;
+  const bool no_grow = getenv("PQ_IX_NOGROW") && atoi(getenv("PQ_IX_NOGROW")) == 1;  // with PQ_IX_CAP
   for (int32_t c = 0; c < n_chunks; c++) {
     const pqgpu_chunk_meta &m = metas[c];
     PageIxChunk &k = ix->chunks[c];
@@ -2255,6 +2301,7 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     cap += 64 + (uint64_t)std::max<int64_t>(k.total, 0) / 4096;
   }
   if (n_chunks == 0) { *out = ix.release(); return PQ_OK; }
+  if (cap_env) cap = std::max<uint64_t>(1, strtoull(cap_env, nullptr, 10));
   // table capacity: a page per 4 KiB plus 64 per chunk; a walk that outgrows it is rerun larger.
   // The chunk table rides in the kernel arguments; the count, the per-chunk results and the table
   // come back by device-to-host copies after the stream has drained, from hipMalloc'd scratch.
@@ -2264,44 +2311,66 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     cap = std::min<uint64_t>(cap, 1u << 26);
     size_t dcap = 0;
     const size_t bytes = 256 + res_bytes + cap * sizeof(PageIxEntry);
-    void *d = ctx->scratch_get(bytes, &dcap);
+    void *d = nullptr;
+    if (use_pool) {
+      dcap = bytes;
+      if (hipMallocAsync(&d, bytes, s) != hipSuccess) d = nullptr;
+    } else {
+      d = ctx->scratch_get(bytes, &dcap);
+    }
     if (!d) HIPCHECK(hipErrorOutOfMemory, err);
     uint8_t *D = (uint8_t *)d;
     uint32_t *d_n = (uint32_t *)D;
     uint4 *d_res = (uint4 *)(D + 256);
     PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + res_bytes);
+    const uint32_t gen = ctx->next_ix_gen();
     hipError_t he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, ix->chunks.data(), (uint32_t)n_chunks,
-                                     d_res, d_tab, d_n, (uint32_t)cap, validate_crc, s);
+                                     d_res, d_tab, d_n, (uint32_t)cap, validate_crc, gen, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
-    // every chunk's walk must have reported before the count and the table are read (a safety net:
-    // with hipMallocAsync scratch, results of workgroups off the first XCD never arrived)
+    // Every chunk's walk must have reported (its result carries this build's generation) before the
+    // count and the table are read. A missing marker is re-read after another drain of the stream,
+    // a bounded number of times; the polls and the chunks that never reported are kept in the index
+    // (pqgpu_page_index_stats), and such a chunk is walked by the host.
     std::vector<uint4> r((size_t)n_chunks);
     int polls = 0;
-    for (; he == hipSuccess; polls++) {
-      he = hipMemcpy(r.data(), d_res, (size_t)n_chunks * sizeof(uint4), hipMemcpyDeviceToHost);
+    for (;; polls++) {
+      if (he == hipSuccess) he = hipMemcpyAsync(r.data(), d_res, (size_t)n_chunks * sizeof(uint4), hipMemcpyDeviceToHost, s);
+      if (he == hipSuccess) he = hipStreamSynchronize(s);
+      if (he != hipSuccess) break;
       bool all = true;
-      for (int32_t c = 0; c < n_chunks && all; c++) all = r[c].w == kIxDone;
-      if (all || polls >= 200) break;
-      he = hipDeviceSynchronize();
+      for (int32_t c = 0; c < n_chunks && all; c++) all = r[c].w == gen;
+      if (all || polls >= 20) break;
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+    ix->polls += polls;
     if (polls && getenv("PQ_IX_DEBUG")) fprintf(stderr, "[ix] results complete after %d polls\n", polls);
-    if (he == hipSuccess) he = hipMemcpy(&n, d_n, 4, hipMemcpyDeviceToHost);
-    const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < 3;
+    if (he == hipSuccess) he = hipMemcpyAsync(&n, d_n, 4, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < (no_grow ? 0 : 3);
     if (he == hipSuccess && !grow) {
-      const size_t ne = (size_t)std::min<uint64_t>(n, cap);
-      ix->entries.resize(ne);
-      if (ne) he = hipMemcpy(ix->entries.data(), d_tab, ne * sizeof(PageIxEntry), hipMemcpyDeviceToHost);
-      if (he == hipSuccess)
-        for (int32_t c = 0; c < n_chunks; c++) {
-          const bool rep = r[c].w == kIxDone;  // a chunk that never reported stays with the host
-          ix->chunks[c].status = rep ? r[c].x : IX_FALLBACK;
-          ix->chunks[c].npages = rep ? r[c].y : 0;
-          ix->chunks[c].fail_page = r[c].z;
-        }
+      ix->unreported = 0;
+      for (int32_t c = 0; c < n_chunks; c++) {
+        const bool rep = r[c].w == gen;  // a chunk that never reported stays with the host
+        ix->unreported += !rep;
+        ix->chunks[c].status = rep ? r[c].x : IX_FALLBACK;
+        ix->chunks[c].npages = rep ? r[c].y : 0;
+        ix->chunks[c].fail_page = r[c].z;
+      }
+      if (n > cap) {
+        // the table overflowed and cannot grow: slots reserved by failed flushes were never written,
+        // so no entry is trusted and every chunk is walked by the host
+        ix->overflowed = 1;
+        ix->entries.clear();
+        for (int32_t c = 0; c < n_chunks; c++) ix->chunks[c].status = IX_FALLBACK;
+      } else {
+        ix->entries.resize(n);
+        if (n) he = hipMemcpyAsync(ix->entries.data(), d_tab, (size_t)n * sizeof(PageIxEntry), hipMemcpyDeviceToHost, s);
+        if (he == hipSuccess) he = hipStreamSynchronize(s);
+      }
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);  // the scratch is free for the next build
-    ctx->scratch_put(d, dcap);
+    if (use_pool) (void)hipFreeAsync(d, s);
+    else ctx->scratch_put(d, dcap);
     HIPCHECK(he, err);
     if (!grow) break;
     cap = (uint64_t)n * 2 + 4096;
@@ -2315,6 +2384,10 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     for (const auto &x : ix->entries)
       fprintf(stderr, "[ix]   e chunk %u seq %u off %lld type %d cs %d\n", x.chunk, x.seq, (long long)x.hdr_off, x.type, x.csize);
   }
+  // entries of a chunk id outside the build cannot come from a completed walk: dropped
+  ix->entries.erase(std::remove_if(ix->entries.begin(), ix->entries.end(),
+                                   [&](const PageIxEntry &x) { return x.chunk >= (uint32_t)n_chunks; }),
+                    ix->entries.end());
   // group by chunk in page order (a chunk's entries were reserved in increasing order)
   std::vector<PageIxEntry> &e = ix->entries;
   std::stable_sort(e.begin(), e.end(), [](const PageIxEntry &a, const PageIxEntry &b) {
@@ -2347,6 +2420,18 @@ int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, 
 }
 
 double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix) { return ix ? ix->walk_ms : 0.0; }
+
+int pqgpu_page_index_stats(const pqgpu_page_index *ix, int32_t *polls, int32_t *unreported, int32_t *fallback_chunks,
+                           int32_t *overflowed) {
+  if (!ix) return PQ_ERR_ARG;
+  int32_t fb = 0;
+  for (const auto &k : ix->chunks) fb += k.status != IX_OK;
+  if (polls) *polls = ix->polls;
+  if (unreported) *unreported = ix->unreported;
+  if (fallback_chunks) *fallback_chunks = fb;
+  if (overflowed) *overflowed = ix->overflowed;
+  return PQ_OK;
+}
 
 void pqgpu_page_index_destroy(pqgpu_page_index *ix) { delete ix; }
 

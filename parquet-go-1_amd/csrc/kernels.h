@@ -65,7 +65,8 @@ struct LaunchLists {
   uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
-  const WorkItem *items; uint32_t n_items;               // values work items
+  const WorkItem *items; uint32_t n_items;               // values work items (LDS kinds: DELTA, dictionary)
+  const WorkItem *copy_items; uint32_t n_copy_items;     // PLAIN / BOOLEAN copies (k_values_copy, no LDS)
   const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with byte-array output
   uint32_t n_ba_tiles;
   uint32_t n_ba_class[3];  // k_ba_emit tiles per class (bytearray.hip ba_emit)                                   // byte-array tiles (BatchDev::ba_tile_page)
@@ -85,6 +86,7 @@ constexpr uint32_t kLfTileHost = 8192;  // k_level_fill tile (kernels.hip kLfTil
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // byte-array outputs (bytearray.hip): per-tile payload sums, per-chunk scan of the tile sums,
 // offsets + payload of every tile
 hipError_t launch_dict_slots(const BatchDev &b, const LaunchLists &l, hipStream_t s);
@@ -115,10 +117,11 @@ hipError_t launch_plain_ba(const BatchDev &b, const PbaLists &l, hipStream_t s);
 // The chunk table is host memory: it reaches the walk in the kernel arguments, kIxArgChunks chunks
 // per launch (never through a DMA copy the walk would read); res[c] = (status, npages, fail_page, 0).
 constexpr uint32_t kIxArgChunks = 64;
-constexpr uint32_t kIxDone = 0x600d0001u;  // res[c].w once chunk c's walk has reported
+// res[c].w = `gen` once chunk c's walk has reported: a per-build generation (never 0, the value
+// k_page_walk_init writes), so a marker left in reused scratch by an earlier build never passes.
 hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, const PageIxChunk *chunks,
                             uint32_t nchunks, uint4 *res, PageIxEntry *table, uint32_t *table_n, uint32_t table_cap,
-                            int validate_crc, hipStream_t s);
+                            int validate_crc, uint32_t gen, hipStream_t s);
 hipError_t launch_page_gather(const GatherJob *jobs, uint32_t njobs, hipStream_t s);
 
 // Names of the kernels, for the timing hook.

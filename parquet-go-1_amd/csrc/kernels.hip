@@ -640,8 +640,10 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     uint32_t nv[kLvPer];
     {
       uint32_t W[5];
-#pragma unroll
-      for (uint32_t q = 0; q < 5; q++) W[q] = L.stage[2 * tid + q];
+      {  // two 8-B reads and a dword (lanes 8 B apart: no two lanes of a read share a bank)
+        const uint2 A0 = *(const uint2 *)&L.stage[2 * tid], A1 = *(const uint2 *)&L.stage[2 * tid + 2];
+        W[0] = A0.x; W[1] = A0.y; W[2] = A1.x; W[3] = A1.y; W[4] = L.stage[2 * tid + 4];
+      }
       uint32_t jj[kLvPer];
 #pragma unroll
       for (uint32_t k = 0; k < kLvPer; k++) {
@@ -788,9 +790,12 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         break;
       }
       const FastHdr f = fast_hdr(L.stage, cs, p, n, bw, rs);
-      put((uint32_t)v, min(nv[k], rem), f.bp, f.value);
+      uint32_t nvk = 0;  // nv[k] by selects: a dynamic index would put nv[] in scratch memory
+#pragma unroll
+      for (uint32_t q = 0; q < kLvPer; q++) nvk = q == k ? nv[q] : nvk;
+      put((uint32_t)v, min(nvk, rem), f.bp, f.value);
       if (L.J0[i0 + k] == kLvExit) L.next_e = p + f.adv;  // the chain's last node
-      v += nv[k];
+      v += nvk;
     }
     st.lap(5);
     wg_barrier();
@@ -2339,6 +2344,18 @@ DEV void do_delta_slow(const BatchDev &b, const DeltaStream &ds, uint32_t nn) {
   }
 }
 
+// PLAIN / BOOLEAN copies: no LDS, so their workgroups fit on a CU beside the DELTA pages'
+// (39 KB of LDS each) and the level kernels' instead of queueing behind them.
+__global__ void __launch_bounds__(256) k_values_copy(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
+  const WorkItem wi = gp(items)[blockIdx.x];
+  const PageDesc &pd = b.pages[wi.page];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t nn = b.page_nn_v[wi.page];
+  if (wi.kind == WI_PLAIN) do_plain(b, wi, pd, cd, nn);
+  else do_bool(b, wi, pd, cd, nn);
+}
+
 __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
   __shared__ ValuesLDS lds;
@@ -2347,7 +2364,7 @@ __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *i
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t nn = b.page_nn_v[wi.page];
   switch (wi.kind) {
-    case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;
+    case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;  // (only when PQ_COPY_FUSED=1 puts them here)
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
     case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
@@ -3012,6 +3029,11 @@ hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_items) return hipSuccess;
   hipLaunchKernelGGL(k_values, dim3(l.n_items), dim3(256), 0, s, b, l.items);
+  return hipGetLastError();
+}
+hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_copy_items) return hipSuccess;
+  hipLaunchKernelGGL(k_values_copy, dim3(l.n_copy_items), dim3(256), 0, s, b, l.copy_items);
   return hipGetLastError();
 }
 hipError_t launch_delta_prep(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

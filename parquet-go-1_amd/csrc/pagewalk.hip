@@ -268,7 +268,8 @@ struct IxChunkArgs {
 
 __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t len, int64_t file_off,
                                                   const IxChunkArgs args, uint32_t chunk0, uint4 *res_in,
-                                                  PageIxEntry *table_in, uint32_t *table_n, uint32_t table_cap) {
+                                                  PageIxEntry *table_in, uint32_t *table_n, uint32_t table_cap,
+                                                  uint32_t gen) {
   __shared__ TFrame stk[kIxDepth];
   const uint8_t *buf = gp(buf_in);
   PageIxEntry *table = gp(table_in);
@@ -334,7 +335,7 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     }
   }
   if (status == IX_OK && seq > flushed && !flush(seq - flushed)) status = IX_FALLBACK;
-  if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, kIxDone);
+  if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, gen);
 }
 
 // ---------------------------------------------------------------------------
@@ -376,7 +377,8 @@ DEV uint32_t x8n_modp(uint64_t n) {  // x^(8n) mod P
 constexpr uint32_t kCrcThreads = 256;
 
 __global__ void __launch_bounds__(kCrcThreads) k_page_crc(const uint8_t *buf_in, int64_t len, int64_t file_off,
-                                                          PageIxEntry *table_in, const uint32_t *table_n_in) {
+                                                          PageIxEntry *table_in, const uint32_t *table_n_in,
+                                                          uint32_t table_cap) {
   __shared__ uint32_t T[4][256];
   __shared__ uint32_t wred[kCrcThreads / 64];
   const uint8_t *buf = gp(buf_in);
@@ -393,7 +395,11 @@ __global__ void __launch_bounds__(kCrcThreads) k_page_crc(const uint8_t *buf_in,
     T[j][tid] = (c >> 8) ^ T[0][c & 0xff];
     wg_barrier();
   }
+  // An overflowing walk (count > capacity) left reserved slots unwritten: the host reruns it with a
+  // larger table or keeps no entries, so no block of this table is checksummed. Otherwise every
+  // slot below the count was written by the walk.
   const uint32_t n_entries = *gp(table_n_in);
+  if (n_entries > table_cap) return;
   for (uint32_t e = blockIdx.x; e < n_entries; e += gridDim.x) {
     const PageIxEntry &h = table[e];
     const uint32_t fl = h.flags;
@@ -454,7 +460,7 @@ __global__ void __launch_bounds__(256) k_page_walk_init(uint32_t *table_n, uint4
 
 hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, const PageIxChunk *chunks,
                             uint32_t nchunks, uint4 *res, PageIxEntry *table, uint32_t *table_n, uint32_t table_cap,
-                            int validate_crc, hipStream_t s) {
+                            int validate_crc, uint32_t gen, hipStream_t s) {
   if (!nchunks) return hipSuccess;
   hipLaunchKernelGGL(k_page_walk_init, dim3((nchunks + 255) / 256), dim3(256), 0, s, table_n, res, nchunks);
   for (uint32_t c0 = 0; c0 < nchunks; c0 += kIxArgChunks) {
@@ -462,11 +468,11 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
     IxChunkArgs a;
     memset(&a, 0, sizeof(a));
     memcpy(a.c, chunks + c0, n * sizeof(PageIxChunk));
-    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap);
+    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap, gen);
   }
   if (validate_crc)
     hipLaunchKernelGGL(k_page_crc, dim3(2048), dim3(kCrcThreads), 0, s, buf, len, file_off, table,
-                       (const uint32_t *)table_n);
+                       (const uint32_t *)table_n, table_cap);
   return hipGetLastError();
 }
 

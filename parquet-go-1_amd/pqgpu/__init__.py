@@ -114,8 +114,8 @@ class PipelineStats(ctypes.Structure):
 
 
 _LIB = None
-TIMER_SLOTS = 20  # PQGPU_TIMER_SLOTS
-ABI_VERSION = 5  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+TIMER_SLOTS = 21  # PQGPU_TIMER_SLOTS
+ABI_VERSION = 6  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -126,7 +126,7 @@ _EXPORTS = [
     "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
     "pqgpu_copy", "pqgpu_pipeline_create", "pqgpu_pipeline_next", "pqgpu_pipeline_release", "pqgpu_pipeline_stats_get",
     "pqgpu_pipeline_destroy", "pqgpu_batch_copy_nested", "pqgpu_page_index_build", "pqgpu_page_index_chunk",
-    "pqgpu_page_index_page", "pqgpu_page_index_walk_ms", "pqgpu_page_index_destroy", "pqgpu_parse_page_header",
+    "pqgpu_page_index_page", "pqgpu_page_index_walk_ms", "pqgpu_page_index_stats", "pqgpu_page_index_destroy", "pqgpu_parse_page_header",
     "pqgpu_batch_add_indexed_chunk", "pqgpu_batch_add_indexed_file_chunk", "pqgpu_dev_alloc", "pqgpu_dev_free",
 ]
 
@@ -190,6 +190,7 @@ def lib():
                                    ctypes.c_int),
         "pqgpu_page_index_page": ([P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(PageHeader)], ctypes.c_int),
         "pqgpu_page_index_walk_ms": ([P], ctypes.c_double),
+        "pqgpu_page_index_stats": ([P] + [ctypes.POINTER(ctypes.c_int32)] * 4, ctypes.c_int),
         "pqgpu_page_index_destroy": ([P], None),
         "pqgpu_parse_page_header": ([P, ctypes.c_size_t, ctypes.POINTER(PageHeader), ctypes.POINTER(ctypes.c_int64)],
                                     ctypes.c_int),
@@ -400,6 +401,7 @@ class Batch:
         rc = lib().pqgpu_batch_add_indexed_file_chunk(self._h, ix._h, k, f._h, col, int(validate_crc),
                                                       ctypes.byref(cid), ctypes.byref(err))
         self._files.append(f)
+        self._files.append(ix)  # upload gathers page bodies from the index's device buffer
         self._infos.append(f.column(col))
         return cid.value, (DecodeError(err) if rc else None)
 
@@ -684,6 +686,12 @@ class PageIndex:
     @property
     def walk_ms(self):
         return lib().pqgpu_page_index_walk_ms(self._h)
+
+    def stats(self):
+        """{polls, unreported, fallback_chunks, overflowed} of the build (pqgpu_page_index_stats)."""
+        v = [ctypes.c_int32() for _ in range(4)]
+        lib().pqgpu_page_index_stats(self._h, *[ctypes.byref(x) for x in v])
+        return dict(zip(("polls", "unreported", "fallback_chunks", "overflowed"), (x.value for x in v)))
 
     def close(self):
         if self._h:

@@ -323,3 +323,40 @@ def test_corrupted_headers(gpu_ctx, seed):
         if not _oracle_ok(data):
             continue
         _check_against_oracle(f"seed{seed}.{trial}", data, _decode_indexed(gpu_ctx, data))
+
+
+@pytest.mark.parametrize("no_grow", [False, True])
+def test_table_overflow(gpu_ctx, monkeypatch, no_grow):
+    """A header table too small for the walk (PQ_IX_CAP forces the first capacity): the CRC pass
+    checksums nothing of an overflowed table, the build is rerun larger, or — when it may not grow
+    (PQ_IX_NOGROW) — keeps no entries and hands every chunk to the host walk. Results equal the
+    oracle's either way, with CRC validation on."""
+    data = pqtest.load("edge_tiny_pages")
+    f = pqgpu.File(data)
+    chunks = _all_chunks(f)
+    monkeypatch.setenv("PQ_IX_CAP", "8")
+    if no_grow:
+        monkeypatch.setenv("PQ_IX_NOGROW", "1")
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, chunks, validate_crc=True, whole_file=True)
+    st = ix.stats()
+    assert st["polls"] == 0 and st["unreported"] == 0, st
+    if no_grow:
+        assert st["overflowed"] == 1 and st["fallback_chunks"] == len(chunks), st
+        assert all(ix.chunk(k) == (0, pqgpu.IX_FALLBACK) for k in range(len(chunks)))
+    else:
+        assert st["overflowed"] == 0 and st["fallback_chunks"] == 0, st
+    ix.close()
+    _check_against_oracle("edge_tiny_pages", data, _decode_indexed(gpu_ctx, data, validate_crc=True))
+
+
+@pytest.mark.parametrize("name", ["cfg2_v2_small", "cfg5_small", "edge_tiny_pages"])
+def test_build_stats_clean(gpu_ctx, name):
+    """Every chunk's completion marker (a per-build generation) is visible at the first read-back:
+    no polls, no unreported chunk, across repeated builds that reuse the same scratch."""
+    data = pqtest.load(name)
+    f = pqgpu.File(data)
+    for _ in range(3):
+        ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, _all_chunks(f), whole_file=True)
+        st = ix.stats()
+        ix.close()
+        assert st == {"polls": 0, "unreported": 0, "fallback_chunks": 0, "overflowed": 0}, (name, st)
