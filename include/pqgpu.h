@@ -77,6 +77,16 @@ typedef struct {
    * element from it). Filled by pqgpu_file_column from the schema. */
   int32_t list_null_def[8];
   int32_t list_def[8];
+  /* OPTIONAL groups on the path, outermost first (num_groups <= PQGPU_MAX_NEST;
+   * the leaf itself is not one): the group's definition level (it is non-null
+   * from it), the REPEATED nodes above it (its entries are the records at 0,
+   * else the elements of list level group_depth - 1) and its position in the
+   * dotted path (0 = the top-level field). Filled by pqgpu_file_column. */
+  int32_t num_groups;
+  int32_t group_def[8];
+  int32_t group_depth[8];
+  int32_t group_node[8];
+  int32_t list_node[8];    /* path position of each REPEATED node (list level k) */
 } pqgpu_column_info;
 #define PQGPU_MAX_NEST 8
 
@@ -141,6 +151,19 @@ typedef struct {
   uint32_t *lvl_validity[8];
   int64_t num_elements;
   uint32_t *element_validity;
+  /* Struct validity of the OPTIONAL groups on the path (column info
+   * num_groups / group_*; produced with the nested arrays, and for leaves with
+   * max_rep == 0): group g has group_entries[g] entries — the records (for a
+   * max_rep == 0 leaf its slots), else the element entries of list level
+   * group_depth[g] - 1 — and bit e of group_validity[g] = the group of entry e
+   * is non-null. Column.getNextData (schema.go:216-260) makes a group nil
+   * unless a child is defined at or below the group's own level, i.e. bit =
+   * (def >= group_def[g]). A pointer may alias lvl_validity / element_validity /
+   * validity when the bitmaps are equal. */
+  int32_t num_groups;
+  int32_t pad1;
+  int64_t group_entries[8];
+  uint32_t *group_validity[8];
 } pqgpu_chunk_result;
 
 /* Per-batch statistics, for the roofline accounting. */
@@ -310,6 +333,19 @@ int pqgpu_batch_copy_chunk(const pqgpu_batch *b, int32_t chunk_id, void *values,
  * the element validity words, of a nested chunk to host buffers (any may be NULL). */
 int pqgpu_batch_copy_nested(const pqgpu_batch *b, int32_t chunk_id, int32_t level, int32_t *offsets,
                             uint32_t *validity, uint32_t *element_validity, pqgpu_error *err);
+/* Copy group g's struct validity words ((group_entries[g] + 31) / 32) to a host buffer. */
+int pqgpu_batch_copy_group(const pqgpu_batch *b, int32_t chunk_id, int32_t group, uint32_t *validity, pqgpu_error *err);
+/* Two leaves of one group — a MAP's key and value, or sibling fields of a
+ * struct (Column.getNextData reads every child of a group at the same
+ * position, schema.go:216-312): the nested arrays of their common ancestors
+ * (the list levels and OPTIONAL groups on the shared path prefix) must be
+ * identical. They are compared on the device; when equal, *equal = 1 and
+ * chunk_b's result carries chunk_a's arrays for those levels and groups (one
+ * shared offsets array per list level, one bitmap per group) until the next
+ * decode; otherwise *equal = 0 and nothing changes. Both chunks must have
+ * decoded without error; PQ_ERR_ARG when their paths share no ancestor
+ * structure consistently (e.g. leaves of different files). */
+int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t chunk_a, int32_t chunk_b, int32_t *equal, pqgpu_error *err);
 int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out);
 /* Diagnostics: 64 device counters filled by in-kernel phase stamps when the
  * environment has PQ_DEBUG_STAMPS=1 at upload time. */

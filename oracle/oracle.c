@@ -630,6 +630,7 @@ typedef struct {
 typedef struct {
   int32_t physical_type, type_length, max_def, max_rep, rep;
   char path[256];
+  int32_t path_len, node_rep[64];
 } leaf_col;
 
 struct or_file {
@@ -756,7 +757,7 @@ static int rd_file_meta(breader *r, or_file *f) {
 /* ------------------------------------------------------------------ */
 /* Schema -> leaf columns  schema.go:893-1079                          */
 /* ------------------------------------------------------------------ */
-static int add_leaf(or_file *f, const char *path, schema_el *e, int d, int r) {
+static int add_leaf(or_file *f, const char *path, schema_el *e, int d, int r, const int32_t *reps, int nreps) {
   leaf_col *nl = (leaf_col *)realloc(f->leaves, sizeof(leaf_col) * (size_t)(f->nleaves + 1));
   if (!nl) return OR_ERR_NOMEM;
   f->leaves = nl;
@@ -767,6 +768,9 @@ static int add_leaf(or_file *f, const char *path, schema_el *e, int d, int r) {
   c->max_rep = r;
   c->rep = e->rep;
   snprintf(c->path, sizeof(c->path), "%s", path);
+  c->path_len = nreps < 63 ? nreps + 1 : 64;
+  for (int k = 0; k < c->path_len - 1; k++) c->node_rep[k] = reps[k];
+  c->node_rep[c->path_len - 1] = e->rep;
   /* getValuesStore data_store.go:325-362 */
   if (e->type < 0 || e->type > 7) return OR_ERR_UNSUPPORTED;
   if (e->type == 7 && !e->has_type_length) return OR_ERR_INVALID;
@@ -774,7 +778,8 @@ static int add_leaf(or_file *f, const char *path, schema_el *e, int d, int r) {
 }
 
 /* readColumnSchema :893-924 */
-static int read_column_schema(or_file *f, int32_t base, int32_t idx, const char *path, int d, int r, int32_t *next) {
+static int read_column_schema(or_file *f, int32_t base, int32_t idx, const char *path, int d, int r, int32_t *next,
+                              const int32_t *reps, int nreps) {
   schema_el *s = &f->schema[base + idx];
   if (!s->name[0]) return OR_ERR_INVALID;
   if (!s->has_rep) return OR_ERR_INVALID;
@@ -782,7 +787,7 @@ static int read_column_schema(or_file *f, int32_t base, int32_t idx, const char 
   if (s->rep == 2) r++;
   char p[256];
   snprintf(p, sizeof(p), "%s%s%s", path, path[0] ? "." : "", s->name);
-  int e = add_leaf(f, p, s, d, r);
+  int e = add_leaf(f, p, s, d, r, reps, nreps);
   if (e) return e;
   *next = idx + 1;
   return OR_OK;
@@ -790,7 +795,7 @@ static int read_column_schema(or_file *f, int32_t base, int32_t idx, const char 
 
 /* readGroupSchema :926-990 */
 static int read_group_schema(or_file *f, int32_t base, int32_t n, int32_t idx, const char *path, int d, int r,
-                             int32_t *next, int depth) {
+                             int32_t *next, int depth, int32_t *reps) {
   if (depth > 1000) return OR_ERR_INVALID;
   if (n <= idx) return OR_ERR_INVALID;
   schema_el *s = &f->schema[base + idx];
@@ -801,14 +806,15 @@ static int read_group_schema(or_file *f, int32_t base, int32_t n, int32_t idx, c
   if ((int64_t)n <= (int64_t)idx + l) return OR_ERR_INVALID;
   if (s->has_rep && s->rep != 0) d++;
   if (s->has_rep && s->rep == 2) r++;
+  if (depth < 63) reps[depth] = s->has_rep ? s->rep : 0;  /* this group's node on its children's paths */
   char p[256];
   snprintf(p, sizeof(p), "%s%s%s", path, path[0] ? "." : "", s->name);
   idx++;
   for (int32_t i = 0; i < l; i++) {
     if (n <= idx) return OR_ERR_INVALID;
     int e;
-    if (!f->schema[base + idx].has_type) e = read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1);
-    else e = read_column_schema(f, base, idx, p, d, r, &idx);
+    if (!f->schema[base + idx].has_type) e = read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1, reps);
+    else e = read_column_schema(f, base, idx, p, d, r, &idx, reps, depth + 1 < 63 ? depth + 1 : 63);
     if (e) return e;
   }
   *next = idx;
@@ -819,10 +825,11 @@ static int read_group_schema(or_file *f, int32_t base, int32_t n, int32_t idx, c
 static int make_schema(or_file *f) {
   if (f->nschema < 1) return OR_ERR_INVALID;
   int32_t n = f->nschema - 1;
+  int32_t reps[64];
   for (int32_t idx = 0; idx < n;) {
     int e;
-    if (!f->schema[1 + idx].has_type) e = read_group_schema(f, 1, n, idx, "", 0, 0, &idx, 0);
-    else e = read_column_schema(f, 1, idx, "", 0, 0, &idx);
+    if (!f->schema[1 + idx].has_type) e = read_group_schema(f, 1, n, idx, "", 0, 0, &idx, 0, reps);
+    else e = read_column_schema(f, 1, idx, "", 0, 0, &idx, reps, 0);
     if (e) return e;
   }
   return OR_OK;
@@ -899,6 +906,8 @@ int or_file_column_info(const or_file *f, int col, or_column_info *out) {
   out->max_rep = c->max_rep;
   out->repetition = c->rep;
   snprintf(out->path, sizeof(out->path), "%s", c->path);
+  out->path_len = c->path_len;
+  for (int k = 0; k < 64; k++) out->node_rep[k] = k < c->path_len ? c->node_rep[k] : 0;
   return OR_OK;
 }
 

@@ -45,6 +45,8 @@ typedef struct {
   int32_t max_rep;
   int32_t repetition;    /* leaf FieldRepetitionType */
   char path[256];        /* dotted path */
+  int32_t path_len;      /* nodes on the path (groups, then the leaf) */
+  int32_t node_rep[64];  /* FieldRepetitionType of each node on the path (nested-array checks) */
 } or_column_info;
 
 typedef struct {

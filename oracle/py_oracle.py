@@ -20,7 +20,8 @@ TYPE_DTYPES = {0: np.uint8, 1: np.int32, 2: np.int64, 3: None, 4: np.uint32, 5: 
 class ColumnInfo(ctypes.Structure):
     _fields_ = [("physical_type", ctypes.c_int32), ("type_length", ctypes.c_int32),
                 ("max_def", ctypes.c_int32), ("max_rep", ctypes.c_int32),
-                ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 256)]
+                ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 256),
+                ("path_len", ctypes.c_int32), ("node_rep", ctypes.c_int32 * 64)]
 
 
 class ChunkResult(ctypes.Structure):

@@ -3,6 +3,9 @@
 #include "format.h"
 
 #include <string.h>
+
+#include <algorithm>
+#include <array>
 #include <zlib.h>
 
 #include "../../include/pqgpu.h"
@@ -252,10 +255,12 @@ static void read_row_group(ThriftReader &t, RowGroup *g, int64_t remaining) {
 }
 
 // schema.go:893-924 readColumnSchema
-// `lists`: (definition level before, at) of every REPEATED ancestor, outermost first
-using ListLevels = std::vector<std::pair<int32_t, int32_t>>;
+// `lists`: (definition level before, at) of every REPEATED ancestor, outermost first;
+// `groups`: (definition level, REPEATED ancestors above, path position) of every OPTIONAL group ancestor
+using ListLevels = std::vector<std::array<int32_t, 3>>;  // + the node's path position
+using GroupLevels = std::vector<std::array<int32_t, 3>>;
 static Status read_column_schema(FileMeta *f, size_t base, int32_t idx, const std::string &path, int d, int r,
-                                 int32_t *next, const ListLevels &lists) {
+                                 int32_t *next, const ListLevels &lists, const GroupLevels &groups) {
   const SchemaElement &s = f->schema[base + (size_t)idx];
   if (s.name.empty()) return Status::Err(PQ_ERR_INVALID, "name in schema is empty");
   if (!s.has_rep) return Status::Err(PQ_ERR_INVALID, "field RepetitionType is nil");
@@ -263,8 +268,10 @@ static Status read_column_schema(FileMeta *f, size_t base, int32_t idx, const st
   if (s.rep != 0) d++;
   if (s.rep == 2) r++;
   Leaf l;
-  for (const auto &x : lists) { l.list_null_def.push_back(x.first); l.list_def.push_back(x.second); }
-  if (s.rep == 2) { l.list_null_def.push_back(d0); l.list_def.push_back(d); }
+  const int32_t self = (int32_t)std::count(path.begin(), path.end(), '.') + (path.empty() ? 0 : 1);
+  for (const auto &x : lists) { l.list_null_def.push_back(x[0]); l.list_def.push_back(x[1]); l.list_node.push_back(x[2]); }
+  if (s.rep == 2) { l.list_null_def.push_back(d0); l.list_def.push_back(d); l.list_node.push_back(self); }
+  for (const auto &g : groups) { l.group_def.push_back(g[0]); l.group_depth.push_back(g[1]); l.group_node.push_back(g[2]); }
   l.type = s.type;
   l.type_length = s.has_type_length ? s.type_length : 0;
   l.max_def = d;
@@ -280,7 +287,7 @@ static Status read_column_schema(FileMeta *f, size_t base, int32_t idx, const st
 
 // schema.go:926-990 readGroupSchema
 static Status read_group_schema(FileMeta *f, size_t base, int32_t n, int32_t idx, const std::string &path, int d,
-                                int r, int32_t *next, int depth, const ListLevels &lists) {
+                                int r, int32_t *next, int depth, const ListLevels &lists, const GroupLevels &groups) {
   if (depth > 1000 || n <= idx) return Status::Err(PQ_ERR_INVALID, "schema index out of bound");
   const SchemaElement &s = f->schema[base + (size_t)idx];
   if (s.has_type) return Status::Err(PQ_ERR_INVALID, "field Type is not nil");
@@ -292,13 +299,15 @@ static Status read_group_schema(FileMeta *f, size_t base, int32_t n, int32_t idx
   if (s.has_rep && s.rep != 0) d++;
   if (s.has_rep && s.rep == 2) r++;
   ListLevels sub = lists;
-  if (s.has_rep && s.rep == 2) sub.emplace_back(d0, d);
+  if (s.has_rep && s.rep == 2) sub.push_back({d0, d, depth});
+  GroupLevels gsub = groups;
+  if (s.has_rep && s.rep == 1) gsub.push_back({d, r, depth});
   std::string p = path.empty() ? s.name : path + "." + s.name;
   idx++;
   for (int32_t k = 0; k < l; k++) {
     if (n <= idx) return Status::Err(PQ_ERR_INVALID, "schema index is out of bounds");
-    Status st = !f->schema[base + (size_t)idx].has_type ? read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1, sub)
-                                                        : read_column_schema(f, base, idx, p, d, r, &idx, sub);
+    Status st = !f->schema[base + (size_t)idx].has_type ? read_group_schema(f, base, n, idx, p, d, r, &idx, depth + 1, sub, gsub)
+                                                        : read_column_schema(f, base, idx, p, d, r, &idx, sub, gsub);
     if (!st.ok()) return st;
   }
   *next = idx;
@@ -335,8 +344,8 @@ Status OpenFile(const uint8_t *buf, int64_t len, FileMeta *out) {
   if (out->schema.empty()) return Status::Err(PQ_ERR_INVALID, "no schema element found");
   int32_t n = (int32_t)out->schema.size() - 1;
   for (int32_t idx = 0; idx < n;) {
-    Status st = !out->schema[1 + (size_t)idx].has_type ? read_group_schema(out, 1, n, idx, "", 0, 0, &idx, 0, {})
-                                                      : read_column_schema(out, 1, idx, "", 0, 0, &idx, {});
+    Status st = !out->schema[1 + (size_t)idx].has_type ? read_group_schema(out, 1, n, idx, "", 0, 0, &idx, 0, {}, {})
+                                                      : read_column_schema(out, 1, idx, "", 0, 0, &idx, {}, {});
     if (!st.ok()) return Status::Err(st.code, "creating schema failed: " + st.msg);
   }
   return Status::Ok();

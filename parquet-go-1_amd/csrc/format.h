@@ -83,7 +83,11 @@ struct Leaf {
   // per REPEATED node on the path, outermost first (max_rep entries): the definition level
   // before the node (a list at that level is non-null from here) and at the node (it has
   // an element from here)
-  std::vector<int32_t> list_null_def, list_def;
+  std::vector<int32_t> list_null_def, list_def, list_node;  // + the node's position on the dotted path
+  // per OPTIONAL group on the path, outermost first: its definition level (the group is non-null
+  // from here), the REPEATED nodes above it (its entries are those of that list depth) and its
+  // position on the dotted path
+  std::vector<int32_t> group_def, group_depth, group_node;
 };
 struct FileMeta {
   std::vector<SchemaElement> schema;

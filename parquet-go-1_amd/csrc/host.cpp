@@ -20,6 +20,8 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <tuple>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -238,6 +240,16 @@ struct HostChunk {
   uint32_t nest = 0, nest_tile0 = 0;
   uint64_t o_lvl_off[PQGPU_MAX_NEST] = {}, o_lvl_valid[PQGPU_MAX_NEST] = {}, o_elem_valid = 0;
   int64_t num_lists[PQGPU_MAX_NEST] = {}, num_elems = 0;
+  // struct validity of the OPTIONAL groups on the path (pqgpu_chunk_result group_*): own bitmap
+  // (grp_alias -1) or the same bits as list level k's validity (0..7), the element validity (8)
+  // or the chunk validity (9)
+  uint32_t ngroups = 0, grp_tile0 = 0;
+  int8_t grp_alias[PQGPU_MAX_NEST] = {};
+  uint64_t o_grp_valid[PQGPU_MAX_NEST] = {};
+  // pqgpu_batch_share_ancestors: list levels [0, share_lists) and groups [0, share_groups) are
+  // chunk share_from's (cleared by every decode)
+  int32_t share_from = -1;
+  uint32_t share_lists = 0, share_groups = 0;
   // byte-array dictionaries: (position, length) of every entry, from the host's walk of the
   // dictionary page (page_dict.go:35-72 + byteArrayPlainDecoder type_bytearray.go:24-55)
   std::vector<uint32_t> dict_ent;
@@ -465,6 +477,8 @@ struct pqgpu_batch {
   uint64_t dblk_total = 0;
   uint32_t n_delta_tiles = 0;
   std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_tiles, nest_chunks;
+  std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
+  uint64_t l_grp_tiles = 0;
   uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0;
   uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
   std::vector<uint64_t> run_base, tile_base;
@@ -1100,6 +1114,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->rec_pages.clear();
   b->nest_tiles.clear();
   b->nest_chunks.clear();
+  b->grp_tiles.clear();
   b->run_base.assign(np, 0);
   b->tile_base.assign(np, 0);
   b->lv_run_base.assign(2 * (size_t)np, 0);
@@ -1137,6 +1152,25 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     const uint64_t words = ((hc.num_slots + 31) / 32 + 2) * 4;
     for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) hc.o_lvl_valid[k] = k < hc.nest ? take(words) : 0;
     hc.o_elem_valid = hc.nest ? take(words) : 0;
+    // struct validity of the OPTIONAL groups (with the nested arrays, or for max_rep == 0 leaves);
+    // a group whose bits equal an existing bitmap's shares it
+    hc.ngroups = 0;
+    for (uint32_t g = 0; g < PQGPU_MAX_NEST; g++) hc.o_grp_valid[g] = 0;
+    const int R = hc.col.max_rep;
+    if (!hc.err.code && (R == 0 || hc.nest) && hc.col.num_groups > 0 && hc.col.num_groups <= PQGPU_MAX_NEST) {
+      bool ok = true;
+      for (int g = 0; g < hc.col.num_groups; g++)
+        ok &= hc.col.group_def[g] >= 1 && hc.col.group_def[g] <= hc.col.max_def && hc.col.group_depth[g] >= 0 &&
+              hc.col.group_depth[g] <= R && (R > 0 || hc.col.max_def > 1 || hc.col.group_def[g] == hc.col.max_def);
+      if (ok) hc.ngroups = (uint32_t)hc.col.num_groups;
+    }
+    for (uint32_t g = 0; g < hc.ngroups; g++) {
+      const int j = hc.col.group_depth[g], dg = hc.col.group_def[g];
+      hc.grp_alias[g] = -1;
+      if (j < R && dg == hc.col.list_null_def[j]) hc.grp_alias[g] = (int8_t)j;
+      else if (j == R && dg == hc.col.max_def) hc.grp_alias[g] = R ? 8 : 9;
+      if (hc.grp_alias[g] < 0) hc.o_grp_valid[g] = take(words);
+    }
   }
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
@@ -1162,6 +1196,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     hc.o_lists = hc.col.max_rep > 0 ? take((ns + 1) * 4) : 0;
     for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) hc.o_lvl_off[k] = k < hc.nest ? take((ns + 1) * 4) : 0;
     if (hc.nest) b->nest_chunks.push_back(c);
+    hc.grp_tile0 = (uint32_t)b->grp_tiles.size();
+    bool own_flat = false;
+    for (uint32_t g = 0; g < hc.ngroups; g++) own_flat |= hc.col.max_rep == 0 && hc.grp_alias[g] < 0;
+    if (own_flat)  // k_group_flat: one 256-thread workgroup per kGrpTile slots (32 per thread)
+      b->grp_tiles.insert(b->grp_tiles.end(), (size_t)((ns + kGrpTileHost - 1) / kGrpTileHost), c);
     hc.o_offsets = is_ba ? take((ns + 1) * 4) : 0;
     hc.o_ba_index = 0;
     b->base_chunks.push_back(c);
@@ -1412,6 +1451,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_rec = take(b->rec_pages.size() * 4);
   b->l_nest_tiles = take(b->nest_tiles.size() * 4);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
+  b->l_grp_tiles = take(b->grp_tiles.size() * 4);
   b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * kNestCnt * 4);
   b->o_nest_base = take((uint64_t)b->nest_tiles.size() * kNestCnt * 8);
   b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
@@ -1528,6 +1568,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       cd.lvl_validity[k] = hc.o_lvl_valid[k] ? dp(hc.o_lvl_valid[k]) : 0;
     }
     cd.elem_validity = hc.o_elem_valid ? dp(hc.o_elem_valid) : 0;
+    cd.ngroups = hc.ngroups;
+    cd.grp_tile0 = hc.grp_tile0;
+    for (uint32_t g = 0; g < PQGPU_MAX_NEST; g++) {
+      cd.group_def[g] = (uint8_t)(g < hc.ngroups ? hc.col.group_def[g] : 0);
+      cd.group_depth[g] = (uint8_t)(g < hc.ngroups ? hc.col.group_depth[g] : 0);
+      cd.group_validity[g] = hc.o_grp_valid[g] ? dp(hc.o_grp_valid[g]) : 0;  // 0: aliased, not written
+    }
     cd.offsets = hc.o_offsets ? dp(hc.o_offsets) : 0;
     cd.ba_index = hc.o_ba_index ? dp(hc.o_ba_index) : 0;
   }
@@ -1585,6 +1632,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
   HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 4), err);
   HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
+  HIPCHECK(up(b->l_grp_tiles, b->grp_tiles.data(), b->grp_tiles.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
   HIPCHECK(up(b->l_delta, b->delta_pages.data(), b->delta_pages.size() * 4), err);
   HIPCHECK(up(b->l_pba_pages, b->pba_pages.data(), b->pba_pages.size() * 4), err);
@@ -1692,6 +1740,8 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
   l.nest_chunks = (const uint32_t *)(A + b->l_nest_chunks);
   l.n_nest_chunks = (uint32_t)b->nest_chunks.size();
+  l.grp_tiles = (const uint32_t *)(A + b->l_grp_tiles);
+  l.n_grp_tiles = (uint32_t)b->grp_tiles.size();
   l.delta_pages = (const uint32_t *)(A + b->l_delta);
   l.n_delta_pages = (uint32_t)b->delta_pages.size();
   l.n_delta_tiles = b->n_delta_tiles;
@@ -1723,6 +1773,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   uint8_t *A = b->d_arena;
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
+  for (auto &hc : b->chunks) hc.share_from = -1;  // shared ancestors are re-checked after a decode
   // per-decode state: two contiguous fills (validity bitmaps + counters; error keys + tile table).
   // page_nn of pages without level streams is constant and was uploaded with the descriptors.
   (void)np;
@@ -1840,6 +1891,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
   HIPCHECK(timed(b, 16, s, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, s); }), err);
   HIPCHECK(timed(b, 14, s, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, s); }), err);
+  HIPCHECK(timed(b, 14, s, l.n_grp_tiles, [&] { return launch_group_flat(d, l, s); }), err);  // struct bitmaps, flat leaves
   b->decoded = true;
   return PQ_OK;
 }
@@ -2004,6 +2056,13 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         out_bytes += (hc.num_elems + 7) / 8;
         for (uint32_t k = 0; k < hc.nest; k++) out_bytes += 4 * (hc.num_lists[k] + 1) + (hc.num_lists[k] + 7) / 8;
       }
+      for (uint32_t g = 0; g < hc.ngroups; g++) {  // struct bitmaps of their own (k_nest_emit / k_group_flat)
+        if (hc.grp_alias[g] >= 0) continue;
+        const int j = hc.col.group_depth[g];
+        const int64_t ent = hc.col.max_rep == 0 ? (int64_t)hc.num_slots : (j < hc.col.max_rep ? hc.num_lists[j] : hc.num_elems);
+        out_bytes += (ent + 7) / 8;
+        kb[14] += (ent + 7) / 8 + (hc.col.max_rep == 0 ? (int64_t)hc.num_slots : 0);  // flat: + the u8 levels read
+      }
     }
   }
   kb[0] = lvl_bytes;
@@ -2120,9 +2179,16 @@ int pqgpu_file_column(const pqgpu_file *f, int col, pqgpu_column_info *out) {
   out->max_rep = l.max_rep;
   out->repetition = l.rep;
   snprintf(out->path, sizeof(out->path), "%s", l.path.c_str());
+  out->num_groups = (int32_t)std::min<size_t>(l.group_def.size(), PQGPU_MAX_NEST + 1);  // > MAX: not produced
+  for (size_t g = 0; g < l.group_def.size() && g < PQGPU_MAX_NEST; g++) {
+    out->group_def[g] = l.group_def[g];
+    out->group_depth[g] = l.group_depth[g];
+    out->group_node[g] = l.group_node[g];
+  }
   for (size_t k = 0; k < l.list_def.size() && k < PQGPU_MAX_NEST; k++) {
     out->list_def[k] = l.list_def[k];
     out->list_null_def[k] = l.list_null_def[k];
+    out->list_node[k] = l.list_node[k];
   }
   return PQ_OK;
 }
@@ -2567,6 +2633,24 @@ int pqgpu_batch_chunk_result(const pqgpu_batch *b, int32_t id, pqgpu_chunk_resul
   }
   out->num_elements = e ? 0 : hc.num_elems;
   out->element_validity = (!e && hc.o_elem_valid) ? (uint32_t *)(A + hc.o_elem_valid) : nullptr;
+  out->num_groups = e ? 0 : (int32_t)hc.ngroups;
+  for (uint32_t g = 0; g < hc.ngroups && !e; g++) {
+    const int j = hc.col.group_depth[g], a = hc.grp_alias[g];
+    out->group_entries[g] = hc.col.max_rep == 0 ? (int64_t)hc.num_slots : (j < hc.col.max_rep ? hc.num_lists[j] : hc.num_elems);
+    out->group_validity[g] = a < 0 ? (uint32_t *)(A + hc.o_grp_valid[g])
+                             : a < 8 ? out->lvl_validity[a] : a == 8 ? out->element_validity : out->validity;
+  }
+  if (!e && hc.share_from >= 0) {  // common ancestors shared with another leaf (checked equal)
+    pqgpu_chunk_result o;
+    pqgpu_error e2;
+    if (pqgpu_batch_chunk_result(b, hc.share_from, &o, &e2) == PQ_OK) {
+      for (uint32_t k = 0; k < hc.share_lists; k++) {
+        out->lvl_offsets[k] = o.lvl_offsets[k];
+        out->lvl_validity[k] = o.lvl_validity[k];
+      }
+      for (uint32_t g = 0; g < hc.share_groups; g++) out->group_validity[g] = o.group_validity[g];
+    }
+  }
   return e;
 }
 
@@ -2588,6 +2672,102 @@ int pqgpu_batch_copy_nested(const pqgpu_batch *b, int32_t id, int32_t level, int
     HIPCHECK(hipMemcpy(element_validity, r.element_validity, (size_t)((r.num_elements + 31) / 32) * 4,
                        hipMemcpyDeviceToHost),
              err);
+  return PQ_OK;
+}
+
+int pqgpu_batch_copy_group(const pqgpu_batch *b, int32_t id, int32_t group, uint32_t *validity, pqgpu_error *err) {
+  pqgpu_chunk_result r;
+  const int e = pqgpu_batch_chunk_result(b, id, &r, err);
+  if (e) return e;
+  NEED_CTX(b, err);
+  if (group < 0 || group >= r.num_groups) {
+    set_err(err, PQ_ERR_ARG, id, -1, "no such group");
+    return PQ_ERR_ARG;
+  }
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  const size_t n = (size_t)((r.group_entries[group] + 31) / 32) * 4;
+  if (validity && n) HIPCHECK(hipMemcpy(validity, r.group_validity[group], n, hipMemcpyDeviceToHost), err);
+  return PQ_OK;
+}
+
+static std::vector<std::string> path_parts(const char *p) {
+  std::vector<std::string> v;
+  std::string cur;
+  for (const char *c = p; *c; c++) {
+    if (*c == '.') { v.push_back(cur); cur.clear(); }
+    else cur += *c;
+  }
+  v.push_back(cur);
+  return v;
+}
+
+int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t *equal, pqgpu_error *err) {
+  clear_err(err);
+  if (equal) *equal = 0;
+  pqgpu_chunk_result ra, rb;
+  int e = pqgpu_batch_chunk_result(b, ia, &ra, err);
+  if (!e) e = pqgpu_batch_chunk_result(b, ib, &rb, err);
+  if (e) return e;
+  NEED_CTX(b, err);
+  HostChunk &ha = b->chunks[(size_t)ia], &hb = b->chunks[(size_t)ib];
+  // the common ancestors: the shared prefix of the two paths, short of either leaf
+  const auto pa = path_parts(ha.col.path), pb = path_parts(hb.col.path);
+  int32_t m = 0;
+  while ((size_t)m + 1 < pa.size() && (size_t)m + 1 < pb.size() && pa[(size_t)m] == pb[(size_t)m]) m++;
+  auto count_below = [m](const int32_t *node, int32_t n) {
+    int32_t c = 0;
+    while (c < n && node[c] < m) c++;
+    return c;
+  };
+  const int32_t La = count_below(ha.col.list_node, std::min(ha.col.max_rep, PQGPU_MAX_NEST));
+  const int32_t Lb = count_below(hb.col.list_node, std::min(hb.col.max_rep, PQGPU_MAX_NEST));
+  const int32_t Ga = count_below(ha.col.group_node, std::min(ha.col.num_groups, PQGPU_MAX_NEST));
+  const int32_t Gb = count_below(hb.col.group_node, std::min(hb.col.num_groups, PQGPU_MAX_NEST));
+  bool consistent = La == Lb && Ga == Gb && (La == 0 || (ra.nest_levels >= La && rb.nest_levels >= La)) &&
+                    (Ga == 0 || (ra.num_groups >= Ga && rb.num_groups >= Ga));
+  for (int32_t k = 0; k < La && consistent; k++)
+    consistent = ha.col.list_node[k] == hb.col.list_node[k] && ha.col.list_def[k] == hb.col.list_def[k] &&
+                 ha.col.list_null_def[k] == hb.col.list_null_def[k];
+  for (int32_t g = 0; g < Ga && consistent; g++)
+    consistent = ha.col.group_node[g] == hb.col.group_node[g] && ha.col.group_def[g] == hb.col.group_def[g];
+  if (!consistent) {
+    set_err(err, PQ_ERR_ARG, ib, -1, "the two leaves' common ancestors differ in the schema");
+    return PQ_ERR_ARG;
+  }
+  // every array pair compared on the device (one flag); entry counts first, on the host
+  bool same = true;
+  std::vector<std::tuple<const uint32_t *, const uint32_t *, uint64_t>> cmp;
+  for (int32_t k = 0; k < La && same; k++) {
+    same = ra.num_lists[k] == rb.num_lists[k];
+    cmp.emplace_back((const uint32_t *)ra.lvl_offsets[k], (const uint32_t *)rb.lvl_offsets[k], (uint64_t)ra.num_lists[k] + 1);
+    cmp.emplace_back(ra.lvl_validity[k], rb.lvl_validity[k], (uint64_t)(ra.num_lists[k] + 31) / 32);
+  }
+  for (int32_t g = 0; g < Ga && same; g++) {
+    same = ra.group_entries[g] == rb.group_entries[g];
+    cmp.emplace_back(ra.group_validity[g], rb.group_validity[g], (uint64_t)(ra.group_entries[g] + 31) / 32);
+  }
+  if (same && !cmp.empty()) {
+    HIPCHECK(hipSetDevice(b->ctx->device), err);
+    hipStream_t s = b->ctx->stream;
+    size_t cap = 0;
+    uint32_t *flag = (uint32_t *)b->ctx->scratch_get(256, &cap);
+    if (!flag) HIPCHECK(hipErrorOutOfMemory, err);
+    hipError_t he = hipMemsetAsync(flag, 0, 4, s);
+    for (auto &x : cmp)
+      if (he == hipSuccess && std::get<0>(x) != std::get<1>(x)) he = launch_words_differ(std::get<0>(x), std::get<1>(x), std::get<2>(x), flag, s);
+    uint32_t h = 1;
+    if (he == hipSuccess) he = hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    b->ctx->scratch_put(flag, cap);
+    HIPCHECK(he, err);
+    same = h == 0;
+  }
+  if (same) {
+    hb.share_from = ia;
+    hb.share_lists = (uint32_t)La;
+    hb.share_groups = (uint32_t)Ga;
+    if (equal) *equal = 1;
+  }
   return PQ_OK;
 }
 

@@ -76,6 +76,7 @@ struct LaunchLists {
   const uint32_t *nest_tiles; uint32_t n_nest_tiles;     // chunk of every 4,096-slot nested tile
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
   const uint32_t *nest_chunks; uint32_t n_nest_chunks;
+  const uint32_t *grp_tiles; uint32_t n_grp_tiles;       // chunk of every k_group_flat tile
   const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)
   uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE
 };
@@ -97,6 +98,10 @@ hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+constexpr uint32_t kGrpTileHost = 8192;  // nested.hip kGrpTile: slots per k_group_flat workgroup
+hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+// *flag |= 1 when the n words at a and b differ (pqgpu_batch_share_ancestors)
+hipError_t launch_words_differ(const uint32_t *a, const uint32_t *b, uint64_t n, uint32_t *flag, hipStream_t s);
 hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages

@@ -18,6 +18,8 @@
 // chunk's record offsets.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dev_util.h"
 
 namespace pq {
@@ -277,6 +279,40 @@ __global__ void __launch_bounds__(256) k_nest_emit(BatchDev b_in, const uint32_t
     nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
     wave_lds_sync();
   }
+  // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
+  // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
+  // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
+  // bits go where that counter's validity goes
+  for (uint32_t g = 0; g < cd.ngroups; g++) {
+    uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[g]);
+    if (!gv) continue;  // shares list / element validity (workgroup-uniform)
+    const uint32_t j = cd.group_depth[g], dg = cd.group_def[g];
+    uint32_t fj = 0, pj = 0, tj = 0;
+    uint64_t rj = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
+      if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
+    uint32_t vg = 0;
+    {
+      const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) {
+        const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
+        vg |= (uint32_t)(d >= dg) << q;
+      }
+    }
+    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+    wave_lds_sync();
+    const uint32_t c = (uint32_t)__popc(fj);
+    if (c) {
+      const uint32_t comp = compress32(vg, fj), sh = pj & 31;
+      atomicOr(&bits[pj >> 5], comp << sh);
+      if (sh && sh + c > 32) atomicOr(&bits[(pj >> 5) + 1], comp >> (32 - sh));
+    }
+    wave_lds_sync();
+    nest_put_bits(gv, rj, bits, tj, lane);
+    wave_lds_sync();
+  }
   // the chunk's last tile closes every level's offsets and the record offsets
   const uint32_t nt = (uint32_t)((cd.num_slots + kNestTile - 1) / kNestTile);
   if (x.local == nt - 1 && threadIdx.x < R) {
@@ -284,6 +320,60 @@ __global__ void __launch_bounds__(256) k_nest_emit(BatchDev b_in, const uint32_t
     gp_u64<int32_t>(cd.lvl_offsets[threadIdx.x])[tot[threadIdx.x]] = (int32_t)tot[threadIdx.x + 1];
     if (threadIdx.x == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
   }
+}
+
+// Struct validity of the OPTIONAL groups of a leaf with max_rep == 0: entries are the leaf's slots,
+// bit s = def[s] >= group_def (u8 definition levels: max_def > 1 whenever such a group owns a
+// bitmap). One thread per 32 slots, one word per group; tiles start on multiples of kGrpTile slots.
+constexpr uint32_t kGrpTile = kGrpTileHost;
+__global__ void __launch_bounds__(256) k_group_flat(BatchDev b_in, const uint32_t *tiles) {
+  const BatchDev b = global_view(b_in);
+  const uint32_t c = gp(tiles)[blockIdx.x];
+  const ChunkDesc &cd = b.chunks[c];
+  const uint64_t s = (uint64_t)(blockIdx.x - cd.grp_tile0) * kGrpTile + 32 * (uint64_t)threadIdx.x;
+  if (s >= cd.num_slots) return;
+  const uint32_t ns = (uint32_t)min((uint64_t)32, cd.num_slots - s);
+  const uint8_t *dl = gp_u64<const uint8_t>(cd.def_levels) + s;
+  uint32_t w[8];
+  if (ns == 32) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(dl), b2 = *reinterpret_cast<const uint4 *>(dl + 16);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b2.x; w[5] = b2.y; w[6] = b2.z; w[7] = b2.w;
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) w[k] = 0;
+    for (uint32_t q = 0; q < ns; q++) w[q >> 2] |= (uint32_t)dl[q] << (8 * (q & 3));
+  }
+  for (uint32_t g = 0; g < cd.ngroups; g++) {
+    uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[g]);
+    if (!gv) continue;
+    const uint32_t dg = cd.group_def[g];
+    uint32_t bitsw = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 32; q++) bitsw |= (uint32_t)(((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= dg) << q;
+    if (ns < 32) bitsw &= (1u << ns) - 1u;
+    gv[s >> 5] = bitsw;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_words_differ(const uint32_t *a_in, const uint32_t *b_in, uint64_t n,
+                                                      uint32_t *flag) {
+  const uint32_t *a = gp(a_in), *b = gp(b_in);
+  bool d = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    d |= a[i] != b[i];
+  if (__ballot(d) && lane_id() == 0) atomicOr(gp(flag), 1u);
+}
+hipError_t launch_words_differ(const uint32_t *a, const uint32_t *b, uint64_t n, uint32_t *flag, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(k_words_differ, dim3(grid), dim3(256), 0, s, a, b, n, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_grp_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_group_flat, dim3(l.n_grp_tiles), dim3(256), 0, s, b, l.grp_tiles);
+  return hipGetLastError();
 }
 
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

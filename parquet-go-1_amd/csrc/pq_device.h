@@ -124,6 +124,11 @@ struct ChunkDesc {       // 192 B
   uint64_t lvl_offsets[8];       // int32[num_lists + 1] per level
   uint64_t lvl_validity[8];      // uint32 bitmap per level
   uint64_t elem_validity;        // uint32 bitmap over the leaf's element slots
+  // struct (OPTIONAL group) validity, per group on the path: entries of list depth group_depth
+  // (records / a max_rep == 0 leaf's slots at 0), bit = def >= group_def; 0 = shares a bitmap above
+  uint32_t ngroups, grp_tile0;    // k_group_flat: the chunk's first tile
+  uint8_t group_def[8], group_depth[8];
+  uint64_t group_validity[8];
 };
 
 // Chunk flags

@@ -50,7 +50,9 @@ class Error(ctypes.Structure):
 class ColumnInfo(ctypes.Structure):
     _fields_ = [("physical_type", ctypes.c_int32), ("type_length", ctypes.c_int32), ("max_def", ctypes.c_int32),
                 ("max_rep", ctypes.c_int32), ("repetition", ctypes.c_int32), ("path", ctypes.c_char * 236),
-                ("list_null_def", ctypes.c_int32 * 8), ("list_def", ctypes.c_int32 * 8)]
+                ("list_null_def", ctypes.c_int32 * 8), ("list_def", ctypes.c_int32 * 8),
+                ("num_groups", ctypes.c_int32), ("group_def", ctypes.c_int32 * 8), ("group_depth", ctypes.c_int32 * 8),
+                ("group_node", ctypes.c_int32 * 8), ("list_node", ctypes.c_int32 * 8)]
 
 
 class ChunkMeta(ctypes.Structure):
@@ -69,7 +71,8 @@ class ChunkResult(ctypes.Structure):
                 ("list_offsets", ctypes.c_void_p), ("nest_levels", ctypes.c_int32), ("dictionary_page", ctypes.c_int32),
                 ("num_lists", ctypes.c_int64 * 8), ("lvl_offsets", ctypes.c_void_p * 8),
                 ("lvl_validity", ctypes.c_void_p * 8), ("num_elements", ctypes.c_int64),
-                ("element_validity", ctypes.c_void_p)]
+                ("element_validity", ctypes.c_void_p), ("num_groups", ctypes.c_int32), ("pad1", ctypes.c_int32),
+                ("group_entries", ctypes.c_int64 * 8), ("group_validity", ctypes.c_void_p * 8)]
 
 
 class BatchStats(ctypes.Structure):
@@ -128,6 +131,7 @@ _EXPORTS = [
     "pqgpu_pipeline_destroy", "pqgpu_batch_copy_nested", "pqgpu_page_index_build", "pqgpu_page_index_chunk",
     "pqgpu_page_index_page", "pqgpu_page_index_walk_ms", "pqgpu_page_index_stats", "pqgpu_page_index_destroy", "pqgpu_parse_page_header",
     "pqgpu_batch_add_indexed_chunk", "pqgpu_batch_add_indexed_file_chunk", "pqgpu_dev_alloc", "pqgpu_dev_free",
+    "pqgpu_batch_copy_group", "pqgpu_batch_share_ancestors",
 ]
 
 
@@ -178,6 +182,8 @@ def lib():
         "pqgpu_batch_kernel_bytes": ([P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
         "pqgpu_copy": ([P, P, P, ctypes.c_size_t, E], ctypes.c_int),
         "pqgpu_batch_copy_nested": ([P, ctypes.c_int32, ctypes.c_int32, P, P, P, E], ctypes.c_int),
+        "pqgpu_batch_copy_group": ([P, ctypes.c_int32, ctypes.c_int32, P, E], ctypes.c_int),
+        "pqgpu_batch_share_ancestors": ([P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
         "pqgpu_pipeline_create": ([P, P, P, ctypes.c_int32, P, ctypes.c_int32, ctypes.POINTER(PipelineOpts),
                                    ctypes.POINTER(P), E], ctypes.c_int),
         "pqgpu_pipeline_next": ([P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int32), E], ctypes.c_int),
@@ -532,7 +538,24 @@ class Batch:
             cd.nested.append((lo, np.unpackbits(lv.view(np.uint8), bitorder="little")[:n]))
             if ev is not None:
                 cd.element_validity = np.unpackbits(ev.view(np.uint8), bitorder="little")[: r.num_elements]
+        # struct validity of the OPTIONAL groups on the path: [(dotted group path, validity bits uint8[n])]
+        cd.groups = []
+        parts = info.path.decode().split(".")
+        for g in range(r.num_groups):
+            n = r.group_entries[g]
+            gv = np.zeros(max((n + 31) // 32, 1), np.uint32)
+            _check(lib().pqgpu_batch_copy_group(self._h, cid, g, gv.ctypes.data_as(ctypes.c_void_p), ctypes.byref(err)), err)
+            cd.groups.append((".".join(parts[: info.group_node[g] + 1]),
+                              np.unpackbits(gv.view(np.uint8), bitorder="little")[:n]))
         return cd
+
+    def share_ancestors(self, cid_a, cid_b):
+        """pqgpu_batch_share_ancestors: True when the two leaves' common ancestors (list levels and
+        OPTIONAL groups on the shared path prefix) decoded identically; chunk b's result then carries
+        chunk a's arrays for them (one shared offsets array per list level)."""
+        eq, err = ctypes.c_int32(0), Error()
+        _check(lib().pqgpu_batch_share_ancestors(self._h, cid_a, cid_b, ctypes.byref(eq), ctypes.byref(err)), err)
+        return bool(eq.value)
 
 
 class _PipelineBatch(Batch):

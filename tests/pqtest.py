@@ -106,3 +106,22 @@ def assert_chunk_equal(gpu, orc, where=""):
         starts = np.flatnonzero(orc.rep_levels == 0)
         exp = np.append(starts, len(orc.rep_levels)).astype(np.int32)
         np.testing.assert_array_equal(gpu.list_offsets, exp, err_msg=f"{where}: list offsets")
+
+
+def schema_levels(node_reps):
+    """From the repetition types of the path's nodes (0 REQUIRED, 1 OPTIONAL, 2 REPEATED; the
+    leaf last): [(null_def, def, node)] per REPEATED node, [(def, depth, node)] per OPTIONAL group,
+    and maxD (schema.go:893-990: every non-REQUIRED node adds a definition level, every REPEATED
+    one a repetition level)."""
+    d = r = 0
+    lists, groups = [], []
+    for i, t in enumerate(node_reps):
+        d0 = d
+        if t != 0:
+            d += 1
+        if t == 2:
+            r += 1
+            lists.append((d0, d, i))
+        elif t == 1 and i < len(node_reps) - 1:
+            groups.append((d, r, i))
+    return lists, groups, d

@@ -9,7 +9,8 @@ Column.getData schema.go:216-312: rLevel < maxR starts a new object, dLevel < ma
 absent value), and is pinned here by (1) the Dremel / Twitter documents of the reference's tests
 (data_store_test.go:227-390), whose nesting is written out by hand below, and (2) pyarrow's own
 ListArray / MapArray reading of the cfg4 fixtures (an independent Dremel -> Arrow implementation).
-The GPU must equal `nested_ref` applied to the oracle's levels."""
+The thresholds come from the oracle's schema walk (pqtest.schema_levels over the path's repetition
+types), independent of the product's. The GPU must equal `nested_ref` applied to the oracle's levels."""
 import io
 
 import numpy as np
@@ -53,9 +54,12 @@ GOLDEN = {
 }
 
 
-def _levels_of(f, col):
-    ci = f.column(col)
-    return list(ci.list_null_def[:ci.max_rep]), list(ci.list_def[:ci.max_rep]), ci.max_def
+def _levels_of(data, col):
+    """The list thresholds from the ORACLE's schema walk (the repetition type of every node on the
+    leaf's path, oracle.c read_group_schema), not from the product's: (null defs, defs, maxD)."""
+    oi = O.File(data).column_info(col)
+    lists, _groups, max_def = pqtest.schema_levels(list(oi.node_rep[:oi.path_len]))
+    return [x[0] for x in lists], [x[1] for x in lists], max_def
 
 
 def _check_nested(got_levels, got_elem, want_levels, want_elem, where):
@@ -73,7 +77,7 @@ def test_ref_documents(doc, path):
     data = G.build(doc)
     f = pqgpu.File(data)
     col = f.column_paths().index(path)
-    lnd, ld, md = _levels_of(f, col)
+    lnd, ld, md = _levels_of(data, col)
     _, cols, _ = G.DOCS[doc]
     _, _, _, _, dl, rl = cols[col]
     got_levels, got_elem = nested_ref(rl, dl, md, lnd, ld)
@@ -102,7 +106,7 @@ def test_ref_matches_pyarrow(name):
             if ci.max_rep == 0:
                 continue
             r = of.read_chunk(rg, col)
-            lnd, ld, md = _levels_of(f, col)
+            lnd, ld, md = _levels_of(data, col)
             levels, elem = nested_ref(r.rep_levels, r.def_levels, md, lnd, ld)
             arr = tbl.column(path.split(".")[0]).combine_chunks()
             offs = np.asarray(arr.offsets, np.int64)
@@ -158,7 +162,7 @@ def test_gpu_nested_vs_ref(gpu_ctx, name):
             assert not r.nested
             continue
         o = of.read_chunk(rg, col)
-        lnd, ld, md = _levels_of(f, col)
+        lnd, ld, md = _levels_of(data, col)
         want_levels, want_elem = nested_ref(o.rep_levels, o.def_levels, md, lnd, ld)
         _check_nested(r.nested, r.element_validity, want_levels, want_elem, f"{name} rg{rg} col{col}")
     b.close()

@@ -54,8 +54,22 @@ DOCS = {
 }
 
 
+# Not reference documents: inputs for other tests, built the same way.
+EXTRA = {
+    # a MAP whose key and value leaves disagree about the entries of each map (record 1: two keys but
+    # one value entry; record 2: one key, two value entries): test_struct's shared-ancestor check
+    "map_mismatch": (
+        [[(4, rawpq.BIN, "schema"), (5, rawpq.I32, 1)],
+         G("m", "OPTIONAL", 1), G("key_value", "REPEATED", 2), L("key", "INT32", "REQUIRED"),
+         L("value", "INT32", "OPTIONAL")],
+        [("m.key_value.key", 2, 1, [1, 2, 3], [2, 2, 2], [0, 1, 0]),
+         ("m.key_value.value", 3, 1, [10, 20], [3, 3, 2], [0, 0, 1])],
+        2),
+}
+
+
 def build(name, v2=False, crc=False):
-    schema, cols, nrec = DOCS[name]
+    schema, cols, nrec = DOCS[name] if name in DOCS else EXTRA[name]
     chunks = []
     for path, md, mr, vals, dl, rl in cols:
         body = rawpq.plain_encode("INT32", vals)

@@ -154,6 +154,50 @@ def cfg4(n=20_000, version="1.0", seed=5):
                  max_rows_per_page=4096)
 
 
+def struct_files(n=20_000, seed=7):
+    """OPTIONAL groups (structs) at list depth 0 and 1, around and inside lists, plus a MAP (f3:
+    struct validity and shared map offsets; Column.getNextData schema.go:216-260):
+      s  : struct<a: int32, l: list<int32>>, 5 % null structs, a 10 % null, l 5 % null / 5 % empty
+      ls : list<struct<x: int32, y: string>>, 5 % null lists, 5 % null struct elements
+      t  : struct<u: struct<x: int64 (required)>>, 5 % null t, 5 % null u
+      mm : map<string, int32>, 5 % null maps, 0-3 entries, 10 % null values"""
+    rng = np.random.default_rng(seed)
+
+    def i32():
+        return int(rng.integers(-2**31, 2**31 - 1))
+
+    s, ls, t, mm = [], [], [], []
+    for _ in range(n):
+        if rng.random() < 0.05:
+            s.append(None)
+        else:
+            u = rng.random()
+            lst = None if u < 0.05 else [] if u < 0.10 else [
+                None if rng.random() < 0.05 else i32() for _ in range(int(rng.integers(1, 5)))]
+            s.append({"a": None if rng.random() < 0.10 else i32(), "l": lst})
+        if rng.random() < 0.05:
+            ls.append(None)
+        else:
+            ls.append([None if rng.random() < 0.05 else
+                       {"x": None if rng.random() < 0.10 else i32(), "y": "w%d" % int(rng.integers(0, 50))}
+                       for _ in range(int(rng.integers(0, 4)))])
+        u = rng.random()
+        t.append(None if u < 0.05 else {"u": None} if u < 0.10 else {"u": {"x": int(rng.integers(-2**62, 2**62))}})
+        if rng.random() < 0.05:
+            mm.append(None)
+        else:
+            ks = rng.choice(40, int(rng.integers(0, 4)), replace=False)
+            mm.append([("k%d" % int(k), None if rng.random() < 0.10 else i32()) for k in ks])
+    tbl = pa.table({
+        "s": pa.array(s, pa.struct([("a", pa.int32()), ("l", pa.list_(pa.int32()))])),
+        "ls": pa.array(ls, pa.list_(pa.struct([("x", pa.int32()), ("y", pa.string())]))),
+        "t": pa.array(t, pa.struct([("u", pa.struct([pa.field("x", pa.int64(), nullable=False)]))])),
+        "mm": pa.array(mm, pa.map_(pa.string(), pa.int32())),
+    })
+    return {"struct_v1": write(tbl, data_page_version="1.0", compression="NONE", max_rows_per_page=4096),
+            "struct_v2": write(tbl, data_page_version="2.0", compression="NONE", max_rows_per_page=4096)}
+
+
 def cfg5(n=60_000, rg=20_000, compression="SNAPPY"):
     # 8-column mix (INT32 dict / INT64 DELTA / DOUBLE PLAIN / INT64 PLAIN), REQUIRED, V1
     rng = np.random.default_rng(6)
@@ -356,6 +400,11 @@ def corrupt(files):
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "--only-struct":  # add the f3 fixtures alone
+        for name, data in struct_files().items():
+            with open(os.path.join(OUT, name + ".parquet"), "wb") as f:
+                f.write(data)
+        return
     files = {
         "cfg1": cfg1(),
         "cfg2_v2_small": cfg2(),
@@ -371,6 +420,7 @@ def main():
     files.update(crc_files())
     files.update(edge_cases())
     files.update(delta_ba())
+    files.update(struct_files())
     files.update(corrupt(files))
     manifest = {}
     for name, data in sorted(files.items()):
