@@ -499,9 +499,15 @@ struct pqgpu_batch {
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
-  // PQ_COPY_FUSED=1: PLAIN / BOOLEAN copies inside k_values (the round-2 single grid), for comparison
-  bool copy_fused = getenv("PQ_COPY_FUSED") && atoi(getenv("PQ_COPY_FUSED")) != 0;
+  // PLAIN / BOOLEAN copies inside k_values (after the DELTA pages, in one grid) or as their own
+  // zero-LDS launch on the copy stream: fused in the speculative schedule (the level kernels and
+  // the DELTA pages already fill the CUs' LDS; cfg2: 0.54 ms fused against 0.57-0.58 split), split
+  // in the serial one. PQ_COPY_FUSED=0/1 forces either (set per plan).
+  bool copy_fused = false;
   uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
+  // PQ_COPY_MODE (speculative schedule): where k_values_copy waits — 0 from the start beside
+  // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
+  int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr;
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
@@ -1389,9 +1395,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_tile_first = take(b->tile_total * 4);
   b->f_end = a;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
-  // pages (long-running), then the bandwidth-bound tiles
-  // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (their own
-  // zero-LDS launch, k_values_copy, on the copy stream)
+  // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
+  // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
+  {
+    const char *cf = getenv("PQ_COPY_FUSED");
+    b->copy_fused = cf ? atoi(cf) != 0 : b->spec;
+  }
   const bool fused = b->copy_fused;
   auto rank = [fused](uint8_t k) {
     return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : (!fused && (k == WI_PLAIN || k == WI_BOOL)) ? 3 : 2;
@@ -1798,8 +1807,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   hipStream_t cs = b->ctx->copy;
   if (!b->ev_copy) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming), err);
   if (!b->ev_copy_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy_join, hipEventDisableTiming), err);
-  auto fork_copies = [&]() -> hipError_t {
-    hipError_t e = hipEventRecord(b->ev_copy, s);
+  auto fork_copies = [&](hipStream_t from) -> hipError_t {
+    hipError_t e = hipEventRecord(b->ev_copy, from);
     if (e == hipSuccess) e = hipStreamWaitEvent(cs, b->ev_copy, 0);
     if (e == hipSuccess) e = timed(b, 20, cs, l.n_copy_items, [&] { return launch_values_copy(d, l, cs); });
     if (e == hipSuccess) e = hipEventRecord(b->ev_copy_join, cs);
@@ -1812,28 +1821,39 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     hipStream_t v = b->ctx->side;
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
+    // PQ_COPY_MODE 4: the copies beside the level kernels, the values path after them;
+    // 5: the copies beside the values path, the level kernels after it (profiling)
+    const bool lv_then_val = b->copy_mode == 4, val_then_lv = b->copy_mode == 5;
+    if (lv_then_val || val_then_lv) HIPCHECK(fork_copies(s), err);
+    if (lv_then_val) HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
     HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
+    if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
+    if (b->copy_mode == 6)  // the copies first on the side stream, then the LDS kinds
+      HIPCHECK(timed(b, 20, v, l.n_copy_items, [&] { return launch_values_copy(d, l, v); }), err);
     HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
-    HIPCHECK(fork_copies(), err);
+    if (b->copy_mode == 1) HIPCHECK(fork_copies(v), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
     HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
-    if (!b->levels_first)
+    if (val_then_lv) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    if (!b->levels_first && !lv_then_val)
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
+    if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
-    HIPCHECK(fork_copies(), err);
+    if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
     HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
     if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items as two launches (profiling)
@@ -1846,6 +1866,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
+    if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);  // PQ_COPY_MODE=3: after everything (profiling)
     HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
   }
   if (!b->ba_chunks.empty()) {
