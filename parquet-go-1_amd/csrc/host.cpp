@@ -457,7 +457,9 @@ struct pqgpu_batch {
     uint32_t comp_len, vlen;     // block bytes, preamble bytes
     uint32_t raw_len, dlen;      // V2 level bytes, decoded length
     uint32_t page;               // global page index
+    bool to_values = false;      // plan: k_snappy writes the page into the chunk's values (SnappyJob::lead)
   };
+  bool snappy_direct = !(getenv("PQ_SNAPPY_DIRECT") && atoi(getenv("PQ_SNAPPY_DIRECT")) == 0);
   bool dev_snappy = !(getenv("PQ_HOST_SNAPPY") && atoi(getenv("PQ_HOST_SNAPPY")) != 0);
   std::vector<DevSnappy> snappy;
   std::vector<uint8_t> pagebuf;  // the planner's copy of a device-decompressed page's head
@@ -1178,6 +1180,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.grp_alias[g] < 0) hc.o_grp_valid[g] = take(words);
     }
   }
+  {  // nested counters per 4,096-slot tile: added by k_level_fill while it expands the levels
+    uint64_t nt = 0;
+    for (uint32_t c = 0; c < nc; c++)
+      if (b->chunks[c].nest) nt += (b->chunks[c].num_slots + 4095) / 4096;
+    b->o_nest_cnt = take(nt * kNestCnt * 4);
+  }
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
   b->o_spec_flag = take(4);
@@ -1276,8 +1284,18 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       auto tiles = [&](uint8_t kind, uint32_t tile) {
         for (uint32_t v0 = 0; v0 < ns_p; v0 += tile) b->items.push_back(WorkItem{p, v0, std::min(v0 + tile, ns_p), kind, {0, 0, 0}});
       };
+      if (pd.flags & PF_DEV_SNAPPY) {
+        // a REQUIRED fixed-width PLAIN page whose decoded bytes are exactly its values: k_snappy
+        // writes them into the values array itself and no k_values item copies them again
+        pqgpu_batch::DevSnappy &j = b->snappy[pd.data];
+        const int w = hc.value_width;
+        j.to_values = b->snappy_direct && hc.col.max_def == 0 && hc.col.max_rep == 0 && w > 0 &&
+                      (pd.vkind == VK_PLAIN_FIXED || pd.vkind == VK_PLAIN_INT96) && j.raw_len == 0 && pd.val_off == 0 &&
+                      (uint64_t)pd.num_slots * (uint64_t)w == j.dlen && pd.val_len == j.dlen;
+      }
+      const bool snappy_values = (pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values;
       switch (pd.vkind) {
-        case VK_PLAIN_FIXED: case VK_PLAIN_INT96: tiles(WI_PLAIN, kPlainTile); break;
+        case VK_PLAIN_FIXED: case VK_PLAIN_INT96: if (!snappy_values) tiles(WI_PLAIN, kPlainTile); break;
         case VK_PLAIN_BOOL: tiles(WI_BOOL, kPlainTile); break;
         case VK_DICT: case VK_RLE_BOOL: {
           if (pd.dict_bw > 0 && ns_p > 0) {
@@ -1461,7 +1479,6 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_nest_tiles = take(b->nest_tiles.size() * 4);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
-  b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * kNestCnt * 4);
   b->o_nest_base = take((uint64_t)b->nest_tiles.size() * kNestCnt * 8);
   b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
   b->arena_size = a;
@@ -1487,7 +1504,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   uint64_t dec = 0;
   for (size_t k = 0; k < b->snappy.size(); k++) {
     dec_off[k] = dec;
-    dec = align_up(dec + align_up((uint64_t)b->snappy[k].raw_len + b->snappy[k].dlen, 16) + 64, 256);
+    if (!b->snappy[k].to_values)  // direct pages need no region of their own
+      dec = align_up(dec + align_up((uint64_t)b->snappy[k].raw_len + b->snappy[k].dlen, 16) + 64, 256);
   }
   // then the resident UNCOMPRESSED pages k_page_gather copies in (same layout)
   const uint64_t gat_base = align_up(dec_base + dec, 256);
@@ -1597,6 +1615,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     const uint64_t comp = j.comp_gather >= 0 ? gjobs[(size_t)j.comp_gather].dst : (uint64_t)(b->d_stage + j.comp_off);
     jobs[k] = SnappyJob{comp + j.vlen, (uint64_t)(b->d_stage + j.raw_off), (uint64_t)(b->d_stage + dec_base + dec_off[k]),
                         j.comp_len - j.vlen, j.raw_len, j.dlen, pd.chunk, pd.page_in_chunk, 0};
+    if (j.to_values) {  // straight into the values array at the page's first value (REQUIRED: slot base)
+      const HostChunk &hc = b->chunks[pd.chunk];
+      jobs[k].dst = (uint64_t)(b->d_arena + hc.o_values) + pd.slot_base * (uint64_t)hc.value_width;
+      jobs[k].lead = 1 + (uint32_t)(jobs[k].dst & 15);
+    }
   }
   std::vector<PageDesc> pages = b->pages;
   for (auto &pd : pages)
@@ -1909,7 +1932,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)
-  HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
+  // (the per-tile nested counts were added by k_level_fill; k_nest_count re-read the levels for them)
   HIPCHECK(timed(b, 16, s, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, s); }), err);
   HIPCHECK(timed(b, 14, s, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, s); }), err);
   HIPCHECK(timed(b, 14, s, l.n_grp_tiles, [&] { return launch_group_flat(d, l, s); }), err);  // struct bitmaps, flat leaves
@@ -1977,7 +2000,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->page_vbase_out = vbase;
   b->page_nn_out = nn;
   int first = PQ_OK;
-  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0;
+  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0, snappy_direct_bytes = 0;
   int64_t kb[PQGPU_TIMER_SLOTS] = {0};  // algorithmic bytes per launch slot
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -2041,6 +2064,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           if (hc.ba_sync) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices (CF_BA_SYNC chunks)
           kb[6] += pd.val_len;
           ba_dict_nn += nn[p];
+        } else if ((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values) {
+          snappy_direct_bytes += pd.val_len;  // written by k_snappy into the values: no k_values work
         } else {
           val_bytes += pd.val_len;  // k_values reads the page's value section
           if (w == 0) ba_other_nn += nn[p];
@@ -2058,7 +2083,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         else lvl_bytes += lv_out;
       }
       if (w) {
-        val_bytes += hc.nn * w;
+        val_bytes += hc.nn * w;  // (less the direct SNAPPY pages' values, below)
       } else {
         // lengths of the non-dictionary pages: read by k_ba_sums; read with their sources and
         // bytes by k_ba_emit, which writes every offset and the payload
@@ -2088,6 +2113,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   kb[0] = lvl_bytes;
   kb[1] = dl_bytes;
+  val_bytes -= snappy_direct_bytes;
   kb[9] = val_bytes - kb[20];  // k_values: the LDS kinds (DELTA, dictionary tiles)
   kb[8] = val_bytes - dl_bytes;
   kb[11] = b->stats.snappy_kernel_bytes;

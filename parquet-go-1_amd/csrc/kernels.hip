@@ -994,6 +994,7 @@ struct LevelFillLDS {
   uint2 run[kLfRuns];
   uint32_t vb[kLfTile / 32];
   uint32_t cnt[kLvThreads / 64];
+  uint32_t nest[2][kNestCnt][kLvThreads / 64];  // nested counters of the tile's two 4,096-slot halves
 };
 // The eight values of the group [g, g + 8) that lie in [vs, ve), from run table `R` (m runs):
 // one step per run the values cross (usually one, at a run boundary two), each step an RLE
@@ -1054,6 +1055,12 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
   const int64_t t0 = (int64_t)k * kLfTile - a;  // page value index of the tile's first (aligned) slot
   const uint32_t lo = (uint32_t)max(t0, (int64_t)0), hi = (uint32_t)min(t0 + kLfTile, (int64_t)ns);
   const uint8_t *page = gp_u64<const uint8_t>(pd.data);
+  // nested chunks: the tile's (rep, def) words stay in registers for the nested counters
+  const uint32_t R = cd.nest;
+  uint64_t rw[kLfGroups], dw[kLfGroups];
+  uint32_t rm[kLfGroups], dm[kLfGroups];  // groups' values covered by each stream (bit per value)
+#pragma unroll
+  for (uint32_t z = 0; z < kLfGroups; z++) { rw[z] = dw[z] = 0; rm[z] = 0; dm[z] = cd.max_def == 0 ? 0xffu : 0u; }
   for (uint32_t which = 0; which < 2; which++) {
     const bool rep = which == 0;
     if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
@@ -1098,6 +1105,14 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
       }
       nc += __popc(eq);
       if (vbits) reinterpret_cast<uint8_t *>(L.vb)[q * kLvThreads + tid] = (uint8_t)eq;
+      if (R) {  // selects, not a dynamic index (which would put the arrays in scratch)
+        const uint32_t cm = vs < ve ? ((1u << (ve - vs)) - 1u) << (vs - (uint32_t)g) : 0u;
+#pragma unroll
+        for (uint32_t z = 0; z < kLfGroups; z++)
+          if (z == q) {
+            if (rep) { rw[z] = word; rm[z] = cm; } else { dw[z] = word; dm[z] = cm; }
+          }
+      }
     }
     // counts: one atomic per tile
     const uint32_t wc = (uint32_t)wave_sum64(nc);
@@ -1119,6 +1134,46 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
       }
     }
     wg_barrier();  // L is reused by the next stream
+  }
+  if (R) {
+    // nested counters (nested.hip nest_flag: lists of levels 1..R starting, then leaf elements) of
+    // the tile's two 4,096-slot halves: groups 0-1 / 2-3 of every thread; one atomic per counter
+    // per half, the counters ride in 5-bit fields of one 64-bit sum (at most 16 slots per thread-half).
+    // Counter j < R: a level-(j+1) list starts (r <= j, d >= D_j); counter R: a leaf element (d >= D_R)
+    uint32_t th[kNestCnt], rc[kNestCnt];
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++) {
+      th[j] = j > R ? 0x100u : (j ? (uint32_t)cd.list_def[j - 1] : 0u);  // > R: never counted
+      rc[j] = j < R ? j : 0xffu;
+    }
+    uint64_t pa = 0, pb = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kLfGroups; q++) {
+      const uint32_t vm = rm[q] & dm[q];
+      const uint64_t rq = rw[q], dq = dw[q];
+      uint64_t acc = 0;
+#pragma unroll 1
+      for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t r = (uint32_t)(rq >> (8 * i)) & 0xffu, d = (uint32_t)(dq >> (8 * i)) & 0xffu;
+        uint64_t fl = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kNestCnt; j++) fl |= (uint64_t)(r <= rc[j] && d >= th[j]) << (5 * j);
+        acc += ((vm >> i) & 1u) ? fl : 0ull;
+      }
+      if (q < kLfGroups / 2) pa += acc; else pb += acc;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++) {
+      const uint32_t a2 = (uint32_t)wave_sum64((pa >> (5 * j)) & 31u), b2 = (uint32_t)wave_sum64((pb >> (5 * j)) & 31u);
+      if (lane == 0) { L.nest[0][j][wv] = a2; L.nest[1][j][wv] = b2; }
+    }
+    wg_barrier();
+    if (tid < 2 * kNestCnt) {
+      const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
+      const uint32_t c = L.nest[h][j][0] + L.nest[h][j][1] + L.nest[h][j][2] + L.nest[h][j][3];
+      const uint64_t cs = ((sbase + (uint64_t)t0) >> 12) + h;  // the chunk's 4,096-slot nested tile
+      if (c) atomicAdd(&b.nest_cnt[(uint64_t)(cd.nest_tile0 + cs) * kNestCnt + j], c);
+    }
   }
 }
 
@@ -2610,11 +2665,25 @@ struct SnappyOut {
   uint8_t *ring;      // LDS, 16-B aligned
   uint8_t *dst;       // page data (global, 16-B aligned)
   uint32_t flushed;   // page bytes [0, flushed) are in dst; a multiple of 16
+  uint32_t lo, hi;    // the bytes of dst this page owns (direct output: [lead, lead + dlen); else all)
 };
 
+// Direct output (SnappyJob::lead): the page is written straight into a values array whose start
+// need not be 16-B aligned; dst is rounded down and page byte P lives at dst + P, so the first
+// and the last 16-B piece hold bytes of the neighbouring pages' values and are written bytewise.
+DEV uint8_t *snappy_base(const SnappyJob &jb) { return gp_u64<uint8_t>(jb.dst) - (jb.lead ? jb.lead - 1 : 0u); }
+
 DEV void snappy_flush(SnappyOut &o, uint32_t upto) {  // ring[flushed, upto) -> dst, upto % 16 == 0
-  for (uint32_t x = o.flushed + lane_id() * 16; x < upto; x += 64 * 16)
-    *(uint4 *)(o.dst + x) = *(const uint4 *)(o.ring + (x & kRingMask));
+  for (uint32_t x = o.flushed + lane_id() * 16; x < upto; x += 64 * 16) {
+    const uint4 v = *(const uint4 *)(o.ring + (x & kRingMask));
+    if (x >= o.lo && x + 16 <= o.hi) {
+      *(uint4 *)(o.dst + x) = v;
+    } else {
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t i = 0; i < 16; i++)
+        if (x + i >= o.lo && x + i < o.hi) o.dst[x + i] = (uint8_t)(vw[i >> 2] >> (8 * (i & 3)));
+    }
+  }
   o.flushed = upto;
 }
 // make room for page bytes [P, P + k) in the ring (k <= kSnappyRing - 16)
@@ -2858,7 +2927,9 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
   const uint8_t *src = gp_u64<const uint8_t>(jb.src);
   const uint32_t n = sgpr(jb.src_len), raw = sgpr(jb.raw_len), dlen = sgpr(jb.dlen);
   const uint32_t lane = lane_id();
-  SnappyOut o{ring, gp_u64<uint8_t>(jb.dst), 0};
+  // direct output: the page starts `lead` bytes into its aligned base (there is no raw prefix)
+  const uint32_t direct = sgpr(jb.lead), base = direct ? direct - 1 : raw;
+  SnappyOut o{ring, snappy_base(jb), 0, direct ? base : 0u, direct ? base + dlen : 0xffffffffu};
   for (uint32_t k = 0; k < raw; k += kSnappyRing / 2)  // V2: the uncompressed level sections first
     snappy_put(o, gp_u64<const uint8_t>(jb.raw) + k, k, min(raw - k, kSnappyRing / 2));
   uint32_t pos = 0, op = 0;  // stream position, decoded bytes
@@ -2937,7 +3008,7 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
       const uint64_t batch = fl < 64 ? chain & ((1ull << fl) - 1ull) : chain;
       if (batch) {
         uint32_t T;
-        if (!snappy_batch(o, st, batch, raw + op, op, dlen, n, pos, t, hdr, val, clen, w, T)) { bad = true; break; }
+        if (!snappy_batch(o, st, batch, base + op, op, dlen, n, pos, t, hdr, val, clen, w, T)) { bad = true; break; }
         op += T;
         sp.lap(2);
         sp.add(6, T);
@@ -2953,7 +3024,7 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
         if (s > n) { bad = true; break; }
         const uint64_t len = (uint64_t)ev + 1;
         if (len > dlen - op || len > n - s) { bad = true; break; }
-        snappy_literal(o, cmd, src + s, raw + op, (uint32_t)len);
+        snappy_literal(o, cmd, src + s, base + op, (uint32_t)len);
         op += (uint32_t)len;
         sp.lap(3);
       }
@@ -2967,12 +3038,13 @@ DEV void snappy_page(const BatchDev &b, const SnappyJob &jb, uint8_t *ring, Snap
     if (lane == 0) report(b, jb.chunk, 0, jb.page_in_chunk, ST_DECOMP, 0, PQ_ERR_DECOMPRESS);
     return;
   }
-  // last piece: zeros past the page end, then the 64 B zero pad every page section carries
-  const uint32_t end = raw + dlen, end16 = (end + 15) & ~15u;
+  // last piece: zeros past the page end, then the 64 B zero pad every page section carries (direct
+  // output: the bytes past the end belong to the next page's values and are not written)
+  const uint32_t end = base + dlen, end16 = (end + 15) & ~15u;
   snappy_room(o, end, 16);
   if (end + lane < end16) o.ring[(end + lane) & kRingMask] = 0;
   snappy_flush(o, end16);
-  if (lane < 4) *(uint4 *)(o.dst + end16 + lane * 16) = uint4{0, 0, 0, 0};
+  if (!direct && lane < 4) *(uint4 *)(o.dst + end16 + lane * 16) = uint4{0, 0, 0, 0};
 }
 
 __global__ void __launch_bounds__(64 * kSnappyWaves) k_snappy(BatchDev b_in, const SnappyJob *jobs) {
@@ -2990,7 +3062,7 @@ __global__ void __launch_bounds__(64 * kSnappyWaves) k_snappy(BatchDev b_in, con
     for (;;) {  // one round per long literal; exits when wave 0 is done (every path sets stop)
       wg_barrier();
       if (cmd.stop) break;
-      snappy_body(cmd, ring, gp_u64<uint8_t>(jb.dst), w);
+      snappy_body(cmd, ring, snappy_base(jb), w);
       wg_barrier();
     }
   }

@@ -189,7 +189,11 @@ struct SnappyJob {       // 48 B
   uint32_t dlen;         // decoded length from the preamble (== the page's decompressed size)
   uint32_t chunk;
   uint32_t page_in_chunk;
-  uint32_t pad;
+  uint32_t lead;         // 0, or direct output: 1 + (dst & 15). A REQUIRED PLAIN fixed-width page whose
+                         // decoded bytes are exactly its values (no level sections, num_values x width
+                         // == dlen) is written straight into the chunk's values array at its value base,
+                         // without the 64-B pad; no k_values item copies it again (the
+                         // decompressed body IS the output, page_v1.go:87-122, type_*.go PLAIN)
 };
 constexpr uint32_t kSnappyRing = 16384;  // LDS window of the most recent output bytes per page
 enum : uint32_t { ST_DECOMP = 4 };       // err_key stage of a device decompression error

@@ -396,3 +396,59 @@ def test_oracle_pyarrow_pages(kind):
 def test_gpu_pyarrow_pages(gpu_ctx, kind):
     data = _pyarrow_snappy_file(kind)
     _compare(_gpu(gpu_ctx, data)[0], data, kind)
+
+
+# ------------------------------------------------------------------ direct output (SnappyJob::lead)
+def _typed_file(typ, width, counts, seed, extra=None):
+    """One REQUIRED column of `typ` (PLAIN, SNAPPY V1): pages of `counts` values; extra[k] = bytes
+    appended to page k's body (or removed, when negative) so its decoded length is not count x width."""
+    rng = np.random.default_rng(seed)
+    ps = []
+    for k, nv in enumerate(counts):
+        body = bytes(rng.integers(0, 256, nv * width, dtype=np.uint8)) if k % 2 else \
+            rng.integers(0, 7, nv * width, dtype=np.uint8).tobytes()
+        d = (extra or {}).get(k, 0)
+        body = body + bytes(range(d)) if d > 0 else body[:len(body) + d]
+        ps.append(rawpq.page_v1c(body, nv, "PLAIN", b"", lambda b: rawpq.snappy_compress(b)))
+    n = sum(counts)
+    return rawpq.write_file([("a", typ, False)], [(n, [ps], [n])], codec=1)
+
+
+DIRECT = {  # value bases not 16-B aligned in every combination, one-value and odd-length pages
+    "int32": ("INT32", 4, [1, 3, 2, 5, 1000, 20_001, 7]),
+    "float": ("FLOAT", 4, [6, 1, 4097, 3]),
+    "int96": ("INT96", 12, [1, 2, 3, 333, 5000, 1]),
+    "int64": ("INT64", 8, [1, 1, 1, 7, 9, 65_537]),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(DIRECT))
+def test_gpu_direct_values(gpu_ctx, name):
+    """REQUIRED PLAIN pages that k_snappy writes straight into the values array (no k_values copy):
+    neighbouring pages share 16-B pieces at every alignment; the result equals the oracle, with the
+    direct path on and off."""
+    typ, w, counts = DIRECT[name]
+    data = _typed_file(typ, w, counts, seed=len(name))
+    g = _gpu(gpu_ctx, data)[0]
+    _compare(g, data, f"direct {name}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("delta", [-1, -4, 3, 8])
+def test_gpu_direct_values_size_mismatch(gpu_ctx, delta):
+    """A page whose decoded length is not num_values x width takes the copy path and keeps the
+    reference's outcome (a short body: EOF / ErrUnexpectedEOF at the first missing value; a longer
+    one: the extra bytes are ignored)."""
+    data = _typed_file("INT64", 8, [5, 11, 3], seed=3, extra={1: delta})
+    _compare(_gpu(gpu_ctx, data)[0], data, f"mismatch {delta}")
+
+
+@pytest.mark.gpu
+def test_gpu_direct_switch(gpu_ctx, monkeypatch):
+    """PQ_SNAPPY_DIRECT=0 (every page through k_values) gives the same values."""
+    data = _typed_file("INT32", 4, DIRECT["int32"][2], seed=9)
+    a = _gpu(gpu_ctx, data)[0]
+    monkeypatch.setenv("PQ_SNAPPY_DIRECT", "0")
+    b = _gpu(gpu_ctx, data)[0]
+    assert np.asarray(a.values_raw).tobytes() == np.asarray(b.values_raw).tobytes()
