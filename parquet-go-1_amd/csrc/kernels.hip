@@ -1055,12 +1055,7 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
   const int64_t t0 = (int64_t)k * kLfTile - a;  // page value index of the tile's first (aligned) slot
   const uint32_t lo = (uint32_t)max(t0, (int64_t)0), hi = (uint32_t)min(t0 + kLfTile, (int64_t)ns);
   const uint8_t *page = gp_u64<const uint8_t>(pd.data);
-  // nested chunks: the tile's (rep, def) words stay in registers for the nested counters
-  const uint32_t R = cd.nest;
-  uint64_t rw[kLfGroups], dw[kLfGroups];
-  uint32_t rm[kLfGroups], dm[kLfGroups];  // groups' values covered by each stream (bit per value)
-#pragma unroll
-  for (uint32_t z = 0; z < kLfGroups; z++) { rw[z] = dw[z] = 0; rm[z] = 0; dm[z] = cd.max_def == 0 ? 0xffu : 0u; }
+  const uint32_t R = cd.nest;  // nested chunks: the tile's nested counters at the end
   for (uint32_t which = 0; which < 2; which++) {
     const bool rep = which == 0;
     if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
@@ -1105,14 +1100,6 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
       }
       nc += __popc(eq);
       if (vbits) reinterpret_cast<uint8_t *>(L.vb)[q * kLvThreads + tid] = (uint8_t)eq;
-      if (R) {  // selects, not a dynamic index (which would put the arrays in scratch)
-        const uint32_t cm = vs < ve ? ((1u << (ve - vs)) - 1u) << (vs - (uint32_t)g) : 0u;
-#pragma unroll
-        for (uint32_t z = 0; z < kLfGroups; z++)
-          if (z == q) {
-            if (rep) { rw[z] = word; rm[z] = cm; } else { dw[z] = word; dm[z] = cm; }
-          }
-      }
     }
     // counts: one atomic per tile
     const uint32_t wc = (uint32_t)wave_sum64(nc);
@@ -1139,26 +1126,53 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
     // nested counters (nested.hip nest_flag: lists of levels 1..R starting, then leaf elements) of
     // the tile's two 4,096-slot halves: groups 0-1 / 2-3 of every thread; one atomic per counter
     // per half, the counters ride in 5-bit fields of one 64-bit sum (at most 16 slots per thread-half).
-    // Counter j < R: a level-(j+1) list starts (r <= j, d >= D_j); counter R: a leaf element (d >= D_R)
-    uint32_t th[kNestCnt], rc[kNestCnt];
-#pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++) {
-      th[j] = j > R ? 0x100u : (j ? (uint32_t)cd.list_def[j - 1] : 0u);  // > R: never counted
-      rc[j] = j < R ? j : 0xffu;
-    }
+    // Counter j < R: a level-(j+1) list starts (r <= j, d >= D_j); counter R: a leaf element
+    // (d >= D_R). Eight levels per 64-bit word compared at once (SWAR: levels below 128; wider
+    // levels take the byte loop).
+    constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
+    auto ge = [&](uint64_t x, uint32_t t) -> uint64_t { return ((x | H) - L1 * t) & H; };  // bytes x >= t
+    // The levels are read back from this thread's own stores of the two passes (each thread expanded
+    // the same groups of both streams), the definition bits from the LDS bitmap when max_def == 1.
+    const bool swar = cd.max_def < 128;
+    const uint32_t cov_r = b.lv_meta[4 * pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * pi + 3] : ns;
+    const uint32_t endc = min(hi, min(cov_r, cov_d));
+    const uint8_t *ro = gp_u64<const uint8_t>(cd.rep_levels) + sbase;
+    const uint8_t *dlv = cd.def_levels ? gp_u64<const uint8_t>(cd.def_levels) + sbase : nullptr;
     uint64_t pa = 0, pb = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kLfGroups; q++) {
-      const uint32_t vm = rm[q] & dm[q];
-      const uint64_t rq = rw[q], dq = dw[q];
+      const int64_t g = t0 + (int64_t)(q * 8 * kLvThreads + 8 * tid);
+      const uint32_t vs = (uint32_t)max(g, (int64_t)lo), ve = (uint32_t)max(min(g + 8, (int64_t)endc), (int64_t)vs);
+      const uint32_t vm = vs < ve ? ((1u << (ve - vs)) - 1u) << (vs - (uint32_t)g) : 0u;
       uint64_t acc = 0;
+      uint64_t rwq = 0, dwq = 0;
+      if (vm) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(ro + g);  // 8-B aligned: g is a group start
+        rwq = ((uint64_t)x.y << 32) | x.x;
+        if (dlv) {
+          const uint2 y = *reinterpret_cast<const uint2 *>(dlv + g);
+          dwq = ((uint64_t)y.y << 32) | y.x;
+        } else if (cd.max_def == 1) {  // the bitmap byte of the group: definition level = bit
+          const uint32_t e = reinterpret_cast<const uint8_t *>(L.vb)[q * kLvThreads + tid];
+          dwq = ((uint64_t)e * L1) & 0x8040201008040201ull;
+          dwq = ((dwq + 0x7f7f7f7f7f7f7f7full) & H) >> 7;
+        }
+      }
+      if (swar) {
+        const uint64_t mb = (((uint64_t)vm * L1) & 0x8040201008040201ull) + 0x7f7f7f7f7f7f7f7full & H;  // covered slots
+        for (uint32_t j = 0; j <= R; j++) {
+          const uint64_t th = j ? cd.list_def[j - 1] : 0u;
+          const uint64_t f = j < R ? ge(dwq, (uint32_t)th) & ~ge(rwq, j + 1) : ge(dwq, cd.list_def[R - 1]);
+          acc += (uint64_t)__popcll(f & mb) << (5 * j);
+        }
+      } else {
 #pragma unroll 1
-      for (uint32_t i = 0; i < 8; i++) {
-        const uint32_t r = (uint32_t)(rq >> (8 * i)) & 0xffu, d = (uint32_t)(dq >> (8 * i)) & 0xffu;
-        uint64_t fl = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kNestCnt; j++) fl |= (uint64_t)(r <= rc[j] && d >= th[j]) << (5 * j);
-        acc += ((vm >> i) & 1u) ? fl : 0ull;
+        for (uint32_t i = 0; i < 8; i++) {
+          if (!((vm >> i) & 1u)) continue;
+          const uint32_t r = (uint32_t)(rwq >> (8 * i)) & 0xffu, d = (uint32_t)(dwq >> (8 * i)) & 0xffu;
+          for (uint32_t j = 0; j <= R; j++)
+            acc += (uint64_t)(j < R ? (r <= j && d >= (j ? cd.list_def[j - 1] : 0u)) : d >= cd.list_def[R - 1]) << (5 * j);
+        }
       }
       if (q < kLfGroups / 2) pa += acc; else pb += acc;
     }
