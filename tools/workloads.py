@@ -170,10 +170,13 @@ def cfg5_template(rows=CFG5_RG_ROWS, seed=6, page_rows=65_536):
                   dictionary_pagesize_limit=1 << 20)
 
 
-def replicate_row_groups(templates, n):
+def replicate_row_groups(templates, n, shared=False):
     """A file of `n` row groups whose row group g is the (only) row group of templates[g mod T],
     byte for byte, behind a footer written here (rawpq's Thrift writer) with every column chunk's
-    offsets moved to its copy. Decoding needs nothing else of the template footers."""
+    offsets moved to its copy. Decoding needs nothing else of the template footers.
+    shared=True: each template's bytes are written once and every row group built from it points at
+    them (the whole 256-row-group cfg5 file in two templates' bytes; a reader sees ordinary column
+    chunks at the offsets the footer gives)."""
     import pyarrow.parquet as pq
     import rawpq as R
     metas = [pq.ParquetFile(io.BytesIO(t)).metadata for t in templates]
@@ -186,14 +189,19 @@ def replicate_row_groups(templates, n):
     codec = {"UNCOMPRESSED": 0, "SNAPPY": 1, "GZIP": 2}
     out = bytearray(b"PAR1")
     rgs, total_rows = [], 0
+    placed = {}  # shared: template index -> shift of its one copy
     for g in range(n):
         t, md = templates[g % len(templates)], metas[g % len(templates)].row_group(0)
         cols = [md.column(c) for c in range(md.num_columns)]
         start = [c.dictionary_page_offset if c.has_dictionary_page else c.data_page_offset for c in cols]
         lo = min(start)
         hi = max(s + c.total_compressed_size for s, c in zip(start, cols))
-        shift = len(out) - lo
-        out += t[lo:hi]
+        if shared and g % len(templates) in placed:
+            shift = placed[g % len(templates)]
+        else:
+            shift = len(out) - lo
+            out += t[lo:hi]
+            placed[g % len(templates)] = shift
         ccs = []
         for s0, c in zip(start, cols):
             md_f = [(1, R.I32, R.TYPES[c.physical_type]), (2, R.LIST, (R.I32, [R.ENC[e] for e in c.encodings])),
@@ -209,6 +217,13 @@ def replicate_row_groups(templates, n):
                      (4, R.LIST, (R.STRUCT, rgs)), (6, R.BIN, "cfg5 row-group templates replicated")])
     out += fmd + len(fmd).to_bytes(4, "little") + b"PAR1"
     return bytes(out)
+
+
+def gen_cfg5_file(num_row_groups=256, rg_rows=CFG5_RG_ROWS, seed=6, templates=2):
+    """The whole configs[4] file: `num_row_groups` row groups (256 x 3,906,250 rows = 1e9 rows of 64
+    columns) over `templates` shared row-group templates (replicate_row_groups shared=True)."""
+    tpl = [cfg5_template(rg_rows, seed=[seed, k]) for k in range(min(templates, num_row_groups))]
+    return replicate_row_groups(tpl, num_row_groups, shared=True)
 
 
 def gen_cfg5(rows=8 * CFG5_RG_ROWS, rg_rows=CFG5_RG_ROWS, seed=6, first_rg=0, templates=2):
