@@ -919,6 +919,389 @@ DEV void levels_page(const BatchDev &b, const uint32_t *pages, LevelLDS &lds) {
   if (tid == 0) b.page_nn[pi] = nn;
 }
 
+// ---------------------------------------------------------------------------
+// k_levels_bw1w: flat OPTIONAL pages (definition levels of bit width 1, validity output), ONE
+// wavefront per page (hybrid_decoder.go:81-165 through decodePackedArray helpers.go:133-149).
+//
+// The run-header chain is walked 64 stream positions per step: lane l decodes the header that
+// would start at pos + l from a 1 KiB LDS ring of the stream (two 512-B halves; the next half is
+// loaded into registers while the current one is walked), the true chain is followed lane to lane
+// with one readlane per run, and the step's runs expand in parallel into an LDS bitmap of the
+// page's first kSegSlots slots (the chunk bitmap beyond): RLE runs of ones set a bit range, bit-
+// packed runs OR their payload words (bit k of the payload = value k). pyarrow's streams have
+// runs of ~2.7 bytes, so a step covers ~24 runs; a page of 65,536 slots is ~150 steps of one wave
+// and every page of a batch is resident at once (a 4-wave list-ranking workgroup per page held 27
+// KB of LDS and 80 VGPRs, six pages per CU).
+// A header the fast decode does not take (a varint of more than 4 bytes, a run reaching past the
+// stream or 72 bytes, an RLE value >= 2, a zero count, EOF) is decoded exactly (decode_hdr, the
+// reference's full header semantics) by the whole wave: an error ends the page at the value where
+// next() fails, a valid run is expanded cooperatively and the chain continues after it. Runs past
+// the one that reaches num_values are never read.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLwRing = 1024;             // LDS ring of stream bytes (two halves)
+constexpr uint32_t kLwHalf = kLwRing / 2;
+constexpr uint32_t kLwMaxAdv = 72;             // fast runs: header + payload within 72 bytes
+constexpr uint32_t kLwLong = 512;              // runs longer than this expand with the whole wave
+struct LevelWaveLDS {
+  uint32_t bits[kSegSlots / 32];  // the page's first kSegSlots validity bits
+  uint32_t ring[kLwRing / 4];     // stream dword k (of the 4-B aligned stream) in slot k mod 256
+};
+
+// 4 stream bytes at aligned offset ax (the ring holds aligned bytes [RA, RA + kLwRing))
+DEV uint32_t lw_bytes4(const uint32_t *ring, uint32_t ax) {
+  const uint32_t k = ax >> 2, sh = ax & 3;
+  const uint32_t w0 = ring[k & (kLwRing / 4 - 1)], w1 = ring[(k + 1) & (kLwRing / 4 - 1)];
+  return __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// One half of the ring: aligned bytes [A, A + kLwHalf) of the stream (bytes at or past the stream
+// end read as zero), two dwords per lane.
+struct LwHalf { uint32_t d0, d1; };
+DEV LwHalf lw_load(const uint32_t *sal, uint32_t A, uint32_t nal) {
+  const uint32_t lane = lane_id();
+  LwHalf h;
+  uint32_t *o[2] = {&h.d0, &h.d1};
+#pragma unroll
+  for (uint32_t j = 0; j < 2; j++) {
+    const uint32_t x = A + 4 * (lane + 64 * j);  // aligned byte offset of the dword
+    uint32_t v = 0;
+    if (x < nal) {
+      v = sal[x >> 2];
+      if (x + 4 > nal) v &= (1u << (8 * (nal - x))) - 1u;
+    }
+    *o[j] = v;
+  }
+  return h;
+}
+DEV void lw_store(uint32_t *ring, uint32_t A, const LwHalf &h) {
+  const uint32_t lane = lane_id(), k = A >> 2;
+  ring[(k + lane) & (kLwRing / 4 - 1)] = h.d0;
+  ring[(k + lane + 64) & (kLwRing / 4 - 1)] = h.d1;
+}
+
+// Expand one run with the whole wave: values [0, take) of the run (RLE value `val`, or bit-packed
+// with payload at stream byte `pay`, read from global memory with zero past the end).
+DEV void lw_run_wave(LevelSink &sk, uint32_t first, uint32_t take, bool bp, uint32_t val, uint32_t pay) {
+  for (uint32_t q = lane_id() * 32; q < take; q += 64 * 32) {
+    const uint32_t m = take - q >= 32 ? ~0u : ((1u << (take - q)) - 1u);
+    uint32_t w;
+    if (bp) w = bits32c(sk.s, sk.n, (uint64_t)pay * 8 + q, 32) & m;
+    else w = val == sk.cmp ? m : 0u;
+    sk.count += __popc(w);
+    lv_or_bits(sk, first + q, w);
+  }
+}
+
+DEV void lw_walk(LevelSink &sk, uint32_t need, uint32_t *ring) {
+  const uint32_t lane = lane_id();
+  const uint8_t *s = sk.s;
+  const uint32_t n = sk.n;
+  const uint32_t sa = (uint32_t)((uintptr_t)s & 3u);
+  const uint32_t *sal = (const uint32_t *)(s - sa);  // 4-B aligned view (pointer arithmetic keeps the space)
+  const uint32_t nal = n + sa;
+  // exact decodes read the stream straight from global memory (decode_hdr's "stage" = the aligned view)
+  const uint32_t gsb = 0u - sa;
+  uint32_t pos = 0, done = 0;
+  uint32_t RA = 0;  // aligned offset of the ring's first half (a multiple of kLwHalf)
+  lw_store(ring, 0, lw_load(sal, 0, nal));
+  lw_store(ring, kLwHalf, lw_load(sal, kLwHalf, nal));
+  LwHalf nxt = lw_load(sal, kLwRing, nal);
+  wave_lds_sync();
+  while (done < need) {
+    // ---- keep pos in the ring's first half
+    const uint32_t ap = pos + sa;
+    if (ap >= RA + kLwHalf) {
+      if (ap < RA + kLwRing) {
+        lw_store(ring, RA + kLwRing, nxt);  // the dead first half takes [RA + 1024, RA + 1536)
+        RA += kLwHalf;
+      } else {  // jumped past the ring (a long run): restage
+        RA = ap & ~(kLwHalf - 1);
+        lw_store(ring, RA, lw_load(sal, RA, nal));
+        lw_store(ring, RA + kLwHalf, lw_load(sal, RA + kLwHalf, nal));
+      }
+      nxt = lw_load(sal, RA + kLwRing, nal);
+      wave_lds_sync();
+    }
+    // ---- fast decode of the header that would start at c = pos + lane (bit width 1: the RLE value
+    // is one byte and must be 0 or 1; a bit-packed run of k groups has k payload bytes)
+    const uint32_t c = pos + lane, ac = c + sa;
+    const uint32_t u0 = lw_bytes4(ring, ac), u1 = lw_bytes4(ring, ac + 4);
+    const uint32_t t = ~u0 & 0x80808080u;
+    const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+    const uint32_t y = (L >= 4 ? u0 : (u0 & ((1u << (8 * L)) - 1u))) & 0x7f7f7f7fu;
+    const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+    const uint32_t cnt = h >> 1, isbp = h & 1u;
+    const uint32_t adv = isbp ? L + cnt : L + 1;
+    const uint32_t v = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * L)) & 0xffu;
+    const uint32_t nv = isbp ? cnt * 8 : cnt;
+    const bool ok = t != 0 && cnt != 0 && adv <= kLwMaxAdv && (uint64_t)c + adv <= n && (isbp || v <= 1) &&
+                    nv < (1u << 24);
+    const uint32_t pk = ok ? adv | (nv << 8) : 0u;
+    // ---- the true chain, lane to lane
+    const uint32_t rem = need - done;
+    uint64_t mask = 0;
+    uint32_t cur = 0, cum = 0;
+    bool stop = false, last = false;
+    while (cur < 64) {
+      const uint32_t pc = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)cur);
+      if (!pc) { stop = true; break; }
+      mask |= 1ull << cur;
+      const uint32_t nvc = pc >> 8;
+      if (nvc >= rem - cum) { cum = rem; last = true; break; }
+      cum += nvc;
+      cur += pc & 0xffu;
+    }
+    // ---- the step's runs expand in parallel
+    const bool mine = (mask >> lane) & 1ull;
+    const uint32_t first = wave_excl_scan(mine ? nv : 0u);
+    const uint32_t take = mine ? min(nv, rem - first) : 0u;
+    const uint32_t f = done + first;
+    if (take && (isbp || take <= kLwLong)) {  // (a fast bit-packed run has at most 71 groups)
+      if (isbp) {
+        const uint32_t pay = ac + L;  // aligned offset of the payload
+        for (uint32_t q = 0; q < take; q += 32) {
+          const uint32_t m = take - q >= 32 ? ~0u : ((1u << (take - q)) - 1u);
+          const uint32_t w = lw_bytes4(ring, pay + (q >> 3)) & m;
+          sk.count += __popc(w);
+          lv_or_bits(sk, f + q, w);
+        }
+      } else if (v == sk.cmp) {
+        sk.count += take;
+        for (uint32_t q = 0; q < take; q += 32) lv_or_bits(sk, f + q, take - q >= 32 ? ~0u : ((1u << (take - q)) - 1u));
+      }
+    }
+    for (uint64_t big = __ballot(!isbp && take > kLwLong); big; big &= big - 1) {  // long RLE runs: the whole wave
+      const uint32_t r = (uint32_t)__builtin_ctzll(big);
+      lw_run_wave(sk, rdlane(f, r), rdlane(take, r), false, rdlane(v, r), 0);
+    }
+    done += cum;
+    if (last) break;
+    if (!stop) { pos += cur; continue; }
+    // ---- the header at pos + cur, decoded exactly
+    const uint32_t P = pos + cur;
+    const Hdr eh = decode_hdr(sal, gsb, s, P, n, 1, 1);
+    if (eh.err) {
+      sk.error(done, eh.err == kErrLongVarint ? resolve_long_varint(s, P, n) : eh.err);
+      break;
+    }
+    const uint32_t okv = min(eh.nvals, eh.okvals), r2 = need - done, tk = min(okv, r2);
+    lw_run_wave(sk, done, tk, eh.bp != 0, eh.value, eh.value);
+    if (okv < eh.nvals && okv < r2) {  // a bit-packed run cut by EOF: next() fails after its groups
+      sk.error(done + okv, PQ_ERR_EOF);
+      break;
+    }
+    done += tk;
+    pos = P + eh.adv;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_levels_bw1w(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelWaveLDS L;
+  const uint32_t pi = pages[blockIdx.x], lane = lane_id();
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t ns = pd.num_slots;
+  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  for (uint32_t k = lane; k < kSegSlots / 32; k += 64) L.bits[k] = 0;
+  LevelSink sk;
+  sk.s = gp_u64<const uint8_t>(pd.data) + pd.def_off;
+  sk.n = pd.def_len;
+  sk.bw = 1;
+  sk.out = nullptr;
+  sk.bits_lds = L.bits;
+  sk.bits_glob = vbits;
+  sk.slot_base = pd.slot_base;
+  sk.cmp = (uint32_t)cd.max_def;  // 1
+  sk.count = 0;
+  sk.err_code = 0;
+  sk.err_pos = 0;
+  sk.stage_len = 0;
+  sk.ablate = b.ablate;
+  wave_lds_sync();
+  if (!(pd.flags & PF_DEF)) {
+    if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+  } else if (ns) {
+    lw_walk(sk, ns, L.ring);
+  }
+  const uint32_t cnt = (uint32_t)wave_sum64(sk.count);
+  if (sk.err_code) {  // wave-uniform: the reference fails the page at the first level error
+    if (lane == 0) {
+      report(b, pd.chunk, 1, pd.page_in_chunk, ST_DEF, sk.err_pos, sk.err_code);
+      b.page_nn[pi] = 0;
+    }
+    return;
+  }
+  wave_lds_sync();
+  // the LDS bitmap segment to the chunk bitmap (the first and last words may be shared with the
+  // neighbouring pages: OR-ed atomically)
+  const uint32_t seg = min(ns, kSegSlots), nw = (seg + 31) / 32;
+  const uint32_t sh = (uint32_t)(pd.slot_base & 31);
+  const uint64_t w0 = pd.slot_base >> 5;
+  for (uint32_t k = lane; k < nw; k += 64) {
+    uint32_t x = L.bits[k];
+    if (k == nw - 1 && (seg & 31)) x &= (1u << (seg & 31)) - 1u;
+    if (sh == 0) {
+      if (k == 0 || k == nw - 1) atomicOr(&vbits[w0 + k], x);
+      else vbits[w0 + k] = x;
+    } else if (x) {
+      atomicOr(&vbits[w0 + k], x << sh);
+      const uint32_t hi = x >> (32 - sh);
+      if (hi) atomicOr(&vbits[w0 + k + 1], hi);
+    }
+  }
+  if (lane == 0) b.page_nn[pi] = cnt;
+}
+
+// The same walk for the generic level streams (repetition levels, definition levels of max > 1):
+// one wavefront per (page, stream) writes the stream's run table (first value index; bit-packed
+// flag | payload position, or the RLE value) and the run of every k_level_fill tile's first value,
+// which k_level_fill expands chip-wide; the payload is not read here, so a fast run may reach up
+// to 4 KiB past its header.
+constexpr uint32_t kLwMaxAdvG = 4095;
+DEV void lw_put_tiles(LevelSink &sk, uint32_t idx, uint32_t f, uint32_t cnt) {
+  if (!cnt || !sk.ntiles) return;
+  const uint64_t a = sk.tile_a;  // fill tiles whose first value lies in [f, f + cnt): tile k > 0 starts at k * T - a
+  uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
+  const uint64_t khi = min(((uint64_t)f + cnt - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+  for (; k <= khi; k++) sk.trun[2 * k] = idx;
+}
+
+DEV void lw_walk_gen(LevelSink &sk, uint32_t need, uint32_t *ring) {
+  const uint32_t lane = lane_id();
+  const uint8_t *s = sk.s;
+  const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3;
+  const uint32_t sa = (uint32_t)((uintptr_t)s & 3u);
+  const uint32_t *sal = (const uint32_t *)(s - sa);
+  const uint32_t nal = n + sa, gsb = 0u - sa;
+  uint32_t pos = 0, done = 0, nruns = 0, RA = 0;
+  lw_store(ring, 0, lw_load(sal, 0, nal));
+  lw_store(ring, kLwHalf, lw_load(sal, kLwHalf, nal));
+  LwHalf nxt = lw_load(sal, kLwRing, nal);
+  wave_lds_sync();
+  while (done < need) {
+    const uint32_t ap = pos + sa;
+    if (ap >= RA + kLwHalf) {
+      if (ap < RA + kLwRing) {
+        lw_store(ring, RA + kLwRing, nxt);
+        RA += kLwHalf;
+      } else {
+        RA = ap & ~(kLwHalf - 1);
+        lw_store(ring, RA, lw_load(sal, RA, nal));
+        lw_store(ring, RA + kLwHalf, lw_load(sal, RA + kLwHalf, nal));
+      }
+      nxt = lw_load(sal, RA + kLwRing, nal);
+      wave_lds_sync();
+    }
+    const uint32_t c = pos + lane, ac = c + sa;
+    const uint32_t u0 = lw_bytes4(ring, ac), u1 = lw_bytes4(ring, ac + 4);
+    const uint32_t t = ~u0 & 0x80808080u;
+    const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+    const uint32_t y = (L >= 4 ? u0 : (u0 & ((1u << (8 * L)) - 1u))) & 0x7f7f7f7fu;
+    const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+    const uint32_t cnt = h >> 1, isbp = h & 1u;
+    const uint64_t adv = isbp ? L + (uint64_t)cnt * bw : (uint64_t)(L + rs);
+    const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * L));
+    const uint32_t v = rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u));
+    const uint32_t nv = isbp ? cnt * 8 : cnt;
+    const bool ok = t != 0 && cnt != 0 && adv <= kLwMaxAdvG && (uint64_t)c + adv <= n &&
+                    (isbp || bw >= 32 || (v >> bw) == 0) && nv < (1u << 20);
+    const uint32_t pk = ok ? (uint32_t)adv | (nv << 12) : 0u;
+    const uint32_t rem = need - done;
+    uint64_t mask = 0;
+    uint32_t cur = 0, cum = 0;
+    bool stop = false, last = false;
+    while (cur < 64) {
+      const uint32_t pc = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)cur);
+      if (!pc) { stop = true; break; }
+      mask |= 1ull << cur;
+      const uint32_t nvc = pc >> 12;
+      if (nvc >= rem - cum) { cum = rem; last = true; break; }
+      cum += nvc;
+      cur += pc & 0xfffu;
+    }
+    const bool mine = (mask >> lane) & 1ull;
+    const uint32_t first = wave_excl_scan(mine ? nv : 0u);
+    const uint32_t ri = nruns + wave_excl_scan(mine ? 1u : 0u);
+    if (mine) {
+      const uint32_t f = done + first;
+      sk.runs[ri] = make_uint2(f, isbp ? 0x80000000u | (c + L) : v);
+      lw_put_tiles(sk, ri, f, min(nv, rem - first));
+    }
+    nruns += (uint32_t)__popcll(mask);
+    done += cum;
+    if (last) break;
+    if (!stop) { pos += cur; continue; }
+    const uint32_t P = pos + cur;
+    const Hdr eh = decode_hdr(sal, gsb, s, P, n, bw, rs);
+    if (eh.err) {
+      sk.error(done, eh.err == kErrLongVarint ? resolve_long_varint(s, P, n) : eh.err);
+      break;
+    }
+    const uint32_t okv = min(eh.nvals, eh.okvals), r2 = need - done, tk = min(okv, r2);
+    if (tk) {
+      if (lane == 0) sk.runs[nruns] = make_uint2(done, eh.bp ? 0x80000000u | eh.value : eh.value);
+      // the tiles of a long run: lanes split the tile range
+      if (sk.ntiles) {
+        const uint64_t a = sk.tile_a;
+        const uint64_t k0 = done == 0 ? 0 : ((uint64_t)done + a + kLfTile - 1) / kLfTile;
+        const uint64_t khi = min(((uint64_t)done + tk - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+        for (uint64_t k = k0 + lane; k <= khi; k += 64) sk.trun[2 * k] = nruns;
+      }
+      nruns++;
+    }
+    if (okv < eh.nvals && okv < r2) {
+      sk.error(done + okv, PQ_ERR_EOF);
+      break;
+    }
+    done += tk;
+    pos = P + eh.adv;
+  }
+  sk.nruns = nruns;
+  sk.covered = min(done, need);
+}
+
+__global__ void __launch_bounds__(64) k_levels_w(BatchDev b_in, const uint32_t *units) {
+  const BatchDev b = global_view(b_in);
+  __shared__ uint32_t ring[kLwRing / 4];
+  const uint32_t u = units[blockIdx.x], pi = u >> 1, which = u & 1, lane = lane_id();
+  const bool rep = which == 0;
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t ns = pd.num_slots;
+  LevelSink sk;
+  sk.s = gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off);
+  sk.n = rep ? pd.rep_len : pd.def_len;
+  sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+  sk.out = nullptr;
+  sk.bits_lds = nullptr;
+  sk.bits_glob = nullptr;
+  sk.slot_base = pd.slot_base;
+  sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
+  sk.count = 0;
+  sk.err_code = 0;
+  sk.err_pos = 0;
+  sk.stage_len = 0;
+  sk.ablate = b.ablate;
+  sk.runs = b.lv_runs + b.lv_run_base[2 * pi + which];
+  sk.trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[pi] + which;
+  sk.tile_a = (uint32_t)(pd.slot_base & (kLfTile - 1));
+  sk.ntiles = lf_tiles(pd.slot_base, ns);
+  sk.covered = 0;
+  sk.nruns = 0;
+  if (!rep && lane == 0) b.page_nn[pi] = 0;  // k_level_fill adds the page's non-null count
+  if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+    if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+  } else if (ns) {
+    lw_walk_gen(sk, ns, ring);
+  }
+  if (lane == 0) {
+    b.lv_meta[4 * pi + 2 * which] = sk.nruns;
+    b.lv_meta[4 * pi + 2 * which + 1] = sk.err_code ? 0u : sk.covered;  // a failed page is not expanded
+    if (sk.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
+  }
+}
+
 // Flat OPTIONAL columns (bit width 1, validity only): held to 80 VGPRs so six workgroups fit
 // per CU (24 KB LDS each): the kernel is latency-bound per page, so resident pages set its time.
 __global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu(PQ_LV_WPE))) k_levels_bw1(BatchDev b_in,
@@ -3091,10 +3474,16 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
   return hipGetLastError();
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
-  if (l.n_level_pages_bw1)
-    hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
-  if (l.n_level_pages)
-    hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
+  if (l.n_level_pages_bw1) {
+    const char *lw = getenv("PQ_LV_WAVE");  // 0: the 4-wave list-ranking kernel
+    if (!(lw && atoi(lw) == 0)) hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
+    else hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
+  }
+  if (l.n_level_pages) {
+    const char *lw = getenv("PQ_LV_WAVE");
+    if (!(lw && atoi(lw) == 0)) hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
+    else hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
+  }
   return hipGetLastError();
 }
 hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
