@@ -148,8 +148,11 @@ struct ScanLDS {
 };
 
 template <class Sink>
-DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink) {
+DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink,
+                      unsigned long long *dbg = nullptr) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  PQ_STAMPS(st, dbg);  // diagnostic build: 0 fast hops, 1 decode, 2 chain, 3 sink, 4 window wait, 5 hops#, 6 steps#
+  st.begin();
   const uint32_t rs = (bw + 7) >> 3;
   // window w holds the bytes at 16-B aligned global addresses [s_al + w * kScanWin, + kScanWin + kScanOver)
   const uintptr_t s_al = (uintptr_t)s & ~(uintptr_t)15;
@@ -216,6 +219,8 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
               const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - done;
               const uint32_t take = min(nv, rem);
               sink.one(done, take, isbp != 0, val, pos);
+              st.lap(0);
+              st.add(5, 1);
               done += take;
               if (nv >= rem) break;
               pos += (uint32_t)adv;
@@ -226,6 +231,8 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
         // ---- speculative header decode at c = pos + lane
         const uint32_t c = pos + lane;
         const Hdr h = decode_hdr(L.win, sb, s, c, n, bw, rs);
+        st.lap(1);
+        st.add(6, 1);
         // ---- follow the true chain lane to lane (scalar registers)
         uint64_t mask = 0;
         uint32_t cum = 0, p = 0, next_pos = pos;
@@ -244,12 +251,15 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
           if (q >= 64) { next_pos = pos + q; break; }
           p = q;
         }
+        st.lap(2);
+        st.add(5, (uint64_t)__popcll(mask));
         // ---- the runs of this step
         const bool mine = (mask >> lane) & 1ull;
         const uint32_t first = wave_excl_scan(mine ? h.nvals : 0u);
         uint32_t cnt = 0;
         if (mine && first < cum) cnt = min(h.nvals, cum - first);
         sink.window(mine && cnt > 0, done + first, cnt, h.bp != 0, h.value, c, L.win, sb);
+        st.lap(3);
         done = sgpr(done + cum);
         if (stop) {
           if (stop_err) sink.error(stop_pos, stop_err);
@@ -263,6 +273,7 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
         L.ctl_stop = stop || done >= need;
       }
     }
+    st.lap(3);
     wg_barrier();
     pos = L.ctl_pos;
     done = L.ctl_done;
@@ -279,7 +290,9 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
     }
     w = nw;
     wg_barrier();
+    st.lap(4);
   }
+  if (wv == 0) st.flush(56);
   return done;
 }
 
@@ -1682,7 +1695,7 @@ __global__ void __launch_bounds__(256) k_scan_runs(BatchDev b_in, const uint32_t
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
   uint32_t done = 0;
   if (nn && pd.dict_bw > 0) {  // workgroup-uniform
-    done = hyb_scan(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs);
+    done = hyb_scan(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs, b.dbg);
   }
   if (threadIdx.x == 0) {  // wave 0 walked: its sink holds the run count and the error
     b.run_count[pi] = rs.nruns;

@@ -45,3 +45,7 @@ dn = ["reload", "walk_wait", "unpack", "scan", "write", "hops#x4", "parse", "wal
 for k, n in enumerate(dn):
     v = int(d[8 + k])
     print(f"delta  {n:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
+sn = ["fast_hops", "decode", "chain", "sink", "window", "hops#", "steps#", "-"]
+for k, n in enumerate(sn[:7]):
+    v = int(d[56 + k])
+    print(f"scan   {n:12s} total {v:>14d}")
