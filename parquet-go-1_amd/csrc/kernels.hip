@@ -3488,13 +3488,13 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (l.n_level_pages_bw1) {
-    const char *lw = getenv("PQ_LV_WAVE");  // 0: the 4-wave list-ranking kernel
-    if (!(lw && atoi(lw) == 0)) hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
+    const char *lw = getenv("PQ_LV_WAVE");  // 1: one wavefront per page (slower: DESIGN.md §5)
+    if (lw && atoi(lw) == 1) hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
     else hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
   }
   if (l.n_level_pages) {
     const char *lw = getenv("PQ_LV_WAVE");
-    if (!(lw && atoi(lw) == 0)) hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
+    if (lw && atoi(lw) == 1) hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
     else hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
   }
   return hipGetLastError();
