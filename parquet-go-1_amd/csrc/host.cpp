@@ -2065,7 +2065,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           kb[6] += pd.val_len;
           ba_dict_nn += nn[p];
         } else if ((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values) {
-          snappy_direct_bytes += pd.val_len;  // written by k_snappy into the values: no k_values work
+          snappy_direct_bytes += (int64_t)nn[p] * w;  // written by k_snappy into the values: no k_values work
         } else {
           val_bytes += pd.val_len;  // k_values reads the page's value section
           if (w == 0) ba_other_nn += nn[p];
