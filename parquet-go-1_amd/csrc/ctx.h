@@ -13,6 +13,7 @@ struct pqgpu_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
   hipStream_t copy = nullptr;  // PLAIN / BOOLEAN copies (k_values_copy) beside both
+  hipStream_t delta = nullptr; // DELTA_BINARY_PACKED pages (k_values_delta) beside all three
   // Device scratch of the page index builds, kept between calls (hipMalloc'd: kernel stores into
   // stream-ordered hipMallocAsync memory from workgroups off the first XCD were observed never to
   // reach a later device-to-host copy of it)

@@ -501,16 +501,16 @@ struct pqgpu_batch {
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
-  // PLAIN / BOOLEAN copies inside k_values (after the DELTA pages, in one grid) or as their own
-  // zero-LDS launch on the copy stream: fused in the speculative schedule (the level kernels and
-  // the DELTA pages already fill the CUs' LDS; cfg2: 0.54 ms fused against 0.57-0.58 split), split
-  // in the serial one. PQ_COPY_FUSED=0/1 forces either (set per plan).
+  // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
+  // k_values_delta) or as their own zero-LDS launch on the copy stream: fused in the speculative
+  // schedule (cfg2: 0.51-0.53 ms fused against 0.56-0.58 split), split in the serial one.
+  // PQ_COPY_FUSED=0/1 forces either (set per plan).
   bool copy_fused = false;
   uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
   // PQ_COPY_MODE (speculative schedule): where k_values_copy waits — 0 from the start beside
   // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr, ev_delta_join = nullptr;
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
   uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
@@ -1825,6 +1825,17 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   l1.n_items = b->n_delta_items;
   l2.items = l.items + b->n_delta_items;
   l2.n_items = l.n_items - b->n_delta_items;
+  // DELTA_BINARY_PACKED items (the first n_delta_items) go to k_values_delta on the DELTA stream,
+  // beside the level kernels, the copies and the other values kinds; the default stream joins it
+  hipStream_t ds = b->ctx->delta;
+  if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
+  auto fork_delta = [&](hipEvent_t after) -> hipError_t {
+    hipError_t e = hipStreamWaitEvent(ds, after, 0);
+    if (e == hipSuccess) e = timed(b, 10, ds, l.n_delta_pages, [&] { return launch_delta_prep(d, l, ds); });
+    if (e == hipSuccess) e = timed(b, 1, ds, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, ds); });
+    if (e == hipSuccess) e = hipEventRecord(b->ev_delta_join, ds);
+    return e;
+  };
   // PLAIN / BOOLEAN copies (k_values_copy) run on the copy stream beside everything else once
   // their value bases are known: at the start in speculative mode, after k_bases otherwise.
   hipStream_t cs = b->ctx->copy;
@@ -1853,12 +1864,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
+    HIPCHECK(fork_delta(b->ev_fork), err);
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
-    HIPCHECK(timed(b, 10, v, l.n_delta_pages, [&] { return launch_delta_prep(d, l, v); }), err);
     if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
     if (b->copy_mode == 6)  // the copies first on the side stream, then the LDS kinds
       HIPCHECK(timed(b, 20, v, l.n_copy_items, [&] { return launch_values_copy(d, l, v); }), err);
-    HIPCHECK(timed(b, 9, v, l.n_items, [&] { return launch_values(d, l, v); }), err);
+    HIPCHECK(timed(b, 9, v, l2.n_items, [&] { return launch_values(d, l2, v); }), err);
     if (b->copy_mode == 1) HIPCHECK(fork_copies(v), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
     HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
@@ -1872,25 +1883,28 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
-    HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
-    HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
-    if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items as two launches (profiling)
-      HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values(d, l1, s); }), err);
-      HIPCHECK(timed(b, 8, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
+    if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
+    HIPCHECK(hipEventRecord(b->ev_fork, s), err);  // after k_bases: the value bases are known
+    if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items one after the other (profiling)
+      HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
+      HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s); }), err);
+      HIPCHECK(hipEventRecord(b->ev_delta_join, s), err);
     } else {
-      // one grid: the DELTA pages (latency-bound: serial header walks and per-batch barriers)
-      // are dispatched first and the bandwidth-bound tiles fill the CUs around them
-      HIPCHECK(timed(b, 9, s, l.n_items, [&] { return launch_values(d, l, s); }), err);
+      HIPCHECK(fork_delta(b->ev_fork), err);
     }
+    HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
+    HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);  // PQ_COPY_MODE=3: after everything (profiling)
     HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   }
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
@@ -2114,7 +2128,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   kb[0] = lvl_bytes;
   kb[1] = dl_bytes;
   val_bytes -= snappy_direct_bytes;
-  kb[9] = val_bytes - kb[20];  // k_values: the LDS kinds (DELTA, dictionary tiles)
+  kb[9] = val_bytes - kb[20] - dl_bytes;  // k_values: the LDS kinds other than DELTA (dictionary tiles, ...)
   kb[8] = val_bytes - dl_bytes;
   kb[11] = b->stats.snappy_kernel_bytes;
   memcpy(b->slot_bytes, kb, sizeof(kb));
@@ -2169,9 +2183,11 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->delta, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
     set_err(err, PQ_ERR_HIP, -1, -1, hipGetErrorString(e));
     return PQ_ERR_HIP;
@@ -2186,6 +2202,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->copy) (void)hipStreamDestroy(c->copy);
+  if (c->delta) (void)hipStreamDestroy(c->delta);
   c->scratch_release();
   delete c;
 }
@@ -2299,6 +2316,7 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
   if (b->ev_copy) (void)hipEventDestroy(b->ev_copy);
   if (b->ev_copy_join) (void)hipEventDestroy(b->ev_copy_join);
+  if (b->ev_delta_join) (void)hipEventDestroy(b->ev_delta_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);

@@ -2413,7 +2413,7 @@ struct DeltaPageLDS {
   int64_t md[kDeltaMaxBlk];
   uint64_t wd[kDeltaMaxBlk];            // miniblock widths, 8 bits each
   uint64_t wsum[2][4];                  // per-wave batch totals (double-buffered by batch parity)
-  uint4 xpose[4][256];                  // per-wave output transpose (64 lanes x 64 B)
+  uint4 xpose[4][128];                  // per-wave output transpose (2 KiB of output at a time)
   unsigned long long stop;              // (value position << 4 | class) of the first error
   uint32_t nb, next;
 };
@@ -2656,51 +2656,59 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
       uint64_t run = carry + before + incl - sum;
       carry += total;
       st.lap(3);
-      uint64_t out[8];
+      uint64_t *out = d;  // values in place of their deltas (registers)
 #pragma unroll
-      for (int q = 0; q < 8; q++) { out[q] = run; run += d[q]; }
+      for (int q = 0; q < 8; q++) { const uint64_t t = d[q]; d[q] = run; run += t; }
       if (PQ_ABLATE(b, 0)) {  // diagnostic: no stores (kept live by an impossible condition)
         if (out[7] == 0x0123456789abcdefull && valid) ((uint64_t *)ds.out)[d0] = out[0];
       } else if (__ballot(valid && d0 + 8 <= stop) == ~0ull) {
         // the wave's 64 groups are 512 consecutive values: transpose through LDS so that every
-        // store instruction writes 1 KiB contiguous (16 B per lane) instead of 64 B-strided pieces
-        // Piece e (16 B) of the wave's output is held by lane e / vw as its piece e % vw; it sits in
-        // LDS slot xsw(e): the piece index within the lane is XOR-swizzled with lane bits so that
+        // store instruction writes 1 KiB contiguous (16 B per lane) instead of 64 B-strided pieces.
+        // The output leaves in 2 KiB halves (int64: lanes 0-31, then lanes 32-63; int32: one half,
+        // every lane). Piece e (16 B) of a half is held by lane e / vw as its piece e % vw; it sits
+        // in LDS slot xsw(e): the piece index within the lane is XOR-swizzled with lane bits so that
         // the 16-B writes of 16 (int64) / 8 (int32) consecutive lanes cover all 64 banks (lanes
         // 64 B / 32 B apart would otherwise meet in the same banks, 4- / 2-way).
         uint4 *xw = L.xpose[wv];
-        const uint32_t vw = is64 ? 4u : 2u;  // uint4 per lane
         auto xsw = [&](uint32_t e) -> uint32_t {
           return is64 ? (e & ~3u) | ((e ^ (e >> 4)) & 3u) : (e & ~1u) | ((e ^ (e >> 4)) & 1u);
         };
-        if (is64) {
-#pragma unroll
-          for (int q = 0; q < 4; q++)
-            xw[xsw(lane * 4 + q)] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32), (uint32_t)out[2 * q + 1],
-                                               (uint32_t)(out[2 * q + 1] >> 32));
-        } else {
-          xw[xsw(lane * 2)] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
-          xw[xsw(lane * 2 + 1)] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
-        }
-        asm volatile("" ::: "memory");  // same wave: LDS executes its accesses in order
         const uint32_t wd0 = rdlane(d0, 0);
-        uint8_t *dst0 = ds.out + (uint64_t)wd0 * (is64 ? 8 : 4);
-        if (al16) {
-          uint4 *dst = (uint4 *)dst0;
-          for (uint32_t q = 0; q < vw; q++) dst[q * 64 + lane] = xw[xsw(q * 64 + lane)];
-        } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
-          const uint32_t bytes = vw * 1024, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
-          const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;
-          const uint32_t *xs = (const uint32_t *)xw;
-          auto xd = [&](uint32_t D) -> uint32_t { return xs[xsw(D >> 2) * 4 + (D & 3)]; };  // dword D
-          uint4 *body = (uint4 *)(dst0 + adj);
-          for (uint32_t j = lane; j < nbody; j += 64) {
-            const uint32_t o = a4 + 4 * j;
-            body[j] = make_uint4(xd(o), xd(o + 1), xd(o + 2), xd(o + 3));
+        const uint32_t nhalf = is64 ? 2u : 1u;
+        for (uint32_t h = 0; h < nhalf; h++) {
+          if (is64) {
+            if ((lane >> 5) == h) {
+              const uint32_t l32 = lane & 31u;
+#pragma unroll
+              for (int q = 0; q < 4; q++)
+                xw[xsw(l32 * 4 + q)] = make_uint4((uint32_t)out[2 * q], (uint32_t)(out[2 * q] >> 32),
+                                                  (uint32_t)out[2 * q + 1], (uint32_t)(out[2 * q + 1] >> 32));
+            }
+          } else {
+            xw[xsw(lane * 2)] = make_uint4((uint32_t)out[0], (uint32_t)out[1], (uint32_t)out[2], (uint32_t)out[3]);
+            xw[xsw(lane * 2 + 1)] = make_uint4((uint32_t)out[4], (uint32_t)out[5], (uint32_t)out[6], (uint32_t)out[7]);
           }
-          const uint32_t nt = (bytes - adj - 16 * nbody) >> 2;
-          if (lane < a4) ((uint32_t *)dst0)[lane] = xd(lane);
-          if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xd(a4 + 4 * nbody + lane);
+          asm volatile("" ::: "memory");  // same wave: LDS executes its accesses in order
+          uint8_t *dst0 = ds.out + (uint64_t)wd0 * (is64 ? 8 : 4) + 2048u * h;
+          if (al16) {
+            uint4 *dst = (uint4 *)dst0;
+#pragma unroll
+            for (uint32_t q = 0; q < 2; q++) dst[q * 64 + lane] = xw[xsw(q * 64 + lane)];
+          } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
+            const uint32_t bytes = 2048, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
+            const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;
+            const uint32_t *xs = (const uint32_t *)xw;
+            auto xd = [&](uint32_t D) -> uint32_t { return xs[xsw(D >> 2) * 4 + (D & 3)]; };  // dword D
+            uint4 *body = (uint4 *)(dst0 + adj);
+            for (uint32_t j = lane; j < nbody; j += 64) {
+              const uint32_t o = a4 + 4 * j;
+              body[j] = make_uint4(xd(o), xd(o + 1), xd(o + 2), xd(o + 3));
+            }
+            const uint32_t nt = (bytes - adj - 16 * nbody) >> 2;
+            if (lane < a4) ((uint32_t *)dst0)[lane] = xd(lane);
+            if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xd(a4 + 4 * nbody + lane);
+          }
+          asm volatile("" ::: "memory");  // this half's LDS reads precede the next half's writes
         }
       } else if (valid) {
         if (d0 + 8 <= stop && al16) {
@@ -2819,6 +2827,27 @@ __global__ void __launch_bounds__(256) k_values_copy(BatchDev b_in, const WorkIt
   const uint32_t nn = b.page_nn_v[wi.page];
   if (wi.kind == WI_PLAIN) do_plain(b, wi, pd, cd, nn);
   else do_bool(b, wi, pd, cd, nn);
+}
+
+// DELTA_BINARY_PACKED work items (pages, tiles, the scalar path) in their own launch: the kernel's
+// registers and LDS are the DELTA decoder's alone, not the maximum over every work-item kind, so
+// the level kernels and the zero-LDS copies fit on a CU beside its workgroups.
+union DeltaLDS {
+  DeltaTileLDS dtile;
+  DeltaPageLDS dpage;
+};
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_values_delta(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
+  __shared__ DeltaLDS lds;
+  const WorkItem wi = items[blockIdx.x];
+  const PageDesc &pd = b.pages[wi.page];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t nn = b.page_nn_v[wi.page];
+  switch (wi.kind) {
+    case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
+    case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
+    case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *items) {
@@ -3517,6 +3546,11 @@ hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_items) return hipSuccess;
   hipLaunchKernelGGL(k_values, dim3(l.n_items), dim3(256), 0, s, b, l.items);
+  return hipGetLastError();
+}
+hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_values_delta, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();
 }
 hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

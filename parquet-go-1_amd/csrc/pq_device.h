@@ -152,9 +152,12 @@ struct DeltaBlk {        // 32 B
 // DELTA_BINARY_PACKED page decoder (WI_DELTA_PAGE): the stream is staged through an LDS
 // window of kDeltaWinLoad bytes; a block (header + payload) must fit in it with 48 bytes of
 // slack (host check, else PF_DELTA_SLOW). At most kDeltaMaxBlk blocks are walked per window.
-constexpr uint32_t kDeltaWin = 16384;
+#ifndef PQ_DELTA_WIN
+#define PQ_DELTA_WIN 8000  // kDeltaWinLoad + 32 <= 8 KiB: two 16-B loads per thread
+#endif
+constexpr uint32_t kDeltaWin = PQ_DELTA_WIN;
 constexpr uint32_t kDeltaWinLoad = kDeltaWin + 128;
-constexpr uint32_t kDeltaMaxBlk = 256;
+constexpr uint32_t kDeltaMaxBlk = kDeltaWin > 8192 ? 256 : 128;
 // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (type_bytearray.go:98-240). The host walks
 // the DELTA lengths streams' headers at init (the reference decodes every length in init():
 // its errors and where the payload starts follow from the stream layout alone, SURVEY.md

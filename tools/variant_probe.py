@@ -18,6 +18,31 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import bench  # noqa: E402
 
 
+def cfg2_shape(rows, flags, rg_rows=4_194_304, page_rows=65_536):
+    """cfg2's columns with parts of the work removed (probe only): which kernels interfere."""
+    import numpy as np
+    import pyarrow as pa
+    import workloads as W
+    rng = np.random.default_rng(2)
+    a = np.cumsum(rng.integers(0, 2**16, rows)).astype(np.int64)
+    b = rng.random(rows)
+    m = None if "req" in flags else rng.random(rows) < 0.1
+    m2 = None if "req" in flags else rng.random(rows) < 0.1
+    if m is not None:  # no DELTA page with a non-null count = 1 (mod 256) or <= 1 (App. A Q1), as gen_cfg2
+        pages = m[: rows // page_rows * page_rows].reshape(-1, page_rows)
+        nn = page_rows - pages.sum(1)
+        for p in np.flatnonzero((nn % 256 == 1) | (nn <= 1)):
+            pages[p, np.flatnonzero(pages[p])[0]] = False
+    cols = {}
+    if "b" not in flags:
+        cols["a"] = pa.array(a, mask=m)
+    if "a" not in flags:
+        cols["b"] = pa.array(b, mask=m2)
+    enc = {k: ("PLAIN" if (k == "b" or "plain" in flags) else "DELTA_BINARY_PACKED") for k in cols}
+    return W._write(pa.table(cols), use_dictionary=False, data_page_version="2.0", compression="NONE",
+                    column_encoding=enc, max_rows_per_page=page_rows, row_group_size=rg_rows)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
@@ -26,11 +51,16 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--variants", default="[{}]")
+    ap.add_argument("--shape", default="", help="cfg2 ablation shapes: req (no nulls), plain (column a PLAIN), "
+                                               "a (column a only), b (column b only); comma-separated flags")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     rows = args.rows or cfg["rows"]
     t0 = time.perf_counter()
-    data, _ = bench.generate(args.config, rows, 0, args.codec)
+    if args.shape:
+        data = cfg2_shape(rows, set(args.shape.split(",")))
+    else:
+        data, _ = bench.generate(args.config, rows, 0, args.codec)
     print(json.dumps({"generated_s": round(time.perf_counter() - t0, 1)}), flush=True)
     import pqgpu
     ctx = pqgpu.Context(0)
