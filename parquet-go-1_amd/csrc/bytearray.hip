@@ -97,6 +97,40 @@ DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
   }
 }
 
+#ifndef PQ_BA_STORES
+#define PQ_BA_STORES 1  // 1: pass B writes its bytes with plain LDS stores (no atomics, no zeroing)
+#endif
+// The same with plain stores: a destination word inside the value is written whole; the two edge
+// words (shared with the neighbouring values) byte by byte. Every byte of a round's range belongs
+// to exactly one value, so the buffer needs no zeroing and no atomics.
+template <int NP>
+DEV void lds_put_slot_st(uint8_t *lb, uint32_t d, const uint4 *sl, uint32_t len) {
+  constexpr int NW = 4 * NP;
+  uint32_t W[NW];
+#pragma unroll
+  for (int q = 0; q < NW / 4; q++) {
+    const uint32_t x[4] = {sl[q].x, sl[q].y, sl[q].z, sl[q].w};
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * q + i >= 1) W[4 * q + i - 1] = x[i];
+  }
+  W[NW - 1] = 0;
+  uint32_t *lw = (uint32_t *)lb;
+  const uint32_t sh = d & 3u, d0 = d >> 2, end = sh + len;
+#pragma unroll
+  for (int m = 0; m < NW; m++) {
+    if (4u * m >= end) break;
+    const uint32_t prev = m ? W[m - 1] : 0u;
+    const uint32_t word = sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m];
+    const uint32_t lo = max(sh, 4u * m) - 4u * m, hi = min(end, 4u * m + 4) - 4u * m;  // valid bytes [lo, hi)
+    if (lo == 0 && hi == 4) {
+      lw[d0 + m] = word;
+    } else {
+      for (uint32_t k = lo; k < hi; k++) lb[4 * (d0 + m) + k] = (uint8_t)(word >> (8 * k));
+    }
+  }
+}
+
 // The same straight to global memory (rounds whose bytes exceed the LDS buffer).
 DEV void global_put(uint8_t *dst, const uint8_t *src, uint32_t len) {
   uint32_t k = 0;
@@ -145,7 +179,7 @@ __global__ void __launch_bounds__(256) k_ba_sums(BatchDev b_in) {
   const uint32_t t = blockIdx.x, p = b.ba_tile_page[t];
   const PageDesc &pd = b.pages[p];
   const ChunkDesc &cd = b.chunks[pd.chunk];
-  if (!(cd.flags & CF_BA_SYNC)) return;  // workgroup-uniform
+  if (!(cd.flags & (CF_BA_SYNC | CF_BA_PRESUM))) return;  // workgroup-uniform
   const uint32_t nn = b.page_nn_v[p];
   const uint32_t v0 = (t - pd.ba_tile) * kBaTile, v1 = min(v0 + kBaTile, nn);
   uint64_t sum = 0;
@@ -177,7 +211,7 @@ __global__ void __launch_bounds__(256) k_ba_scan(BatchDev b_in, const uint32_t *
   __shared__ uint64_t wsum[4];
   const uint32_t c = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[c];
-  if (!(cd.flags & CF_BA_SYNC)) return;
+  if (!(cd.flags & (CF_BA_SYNC | CF_BA_PRESUM))) return;
   uint64_t *ts = b.ba_tile_sum + cd.ba_tile0;
   uint64_t carry = 0;
   for (uint32_t t0 = 0; t0 < cd.ba_ntiles; t0 += blockDim.x) {
@@ -364,7 +398,8 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   const uint64_t wt = wave_sum64(mine);
   st.lap(1);
   uint4 *wb = &L.wbuf[wv][0];
-  for (uint32_t k = lane; k < kWaveVec; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
+  if (!PQ_BA_STORES)
+    for (uint32_t k = lane; k < kWaveVec; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
   if (lane == 0) L.wtot[wv] = wt;
   wg_barrier();
   st.lap(2);
@@ -372,7 +407,7 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   if (wv == 0) {
     uint64_t agg = 0;
     for (uint32_t q = 0; q < kEmitWaves; q++) agg += L.wtot[q];
-    const uint64_t base = (cd.flags & CF_BA_SYNC) ? b.ba_tile_sum[t]
+    const uint64_t base = (cd.flags & (CF_BA_SYNC | CF_BA_PRESUM)) ? b.ba_tile_sum[t]
                           : PQ_ABLATE(b, 8) ? 0  // diagnostic: no look-back
                                             : lookback(b, cd, pd.chunk, t, agg, L.tile, st);
     if (lane == 0) L.base = base;
@@ -426,8 +461,12 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
       if (!T) continue;
       if (cur + T <= kWaveBuf) {
         if (l) {
-          if constexpr (SLOT) lds_put_slot<SV>(lw, cur + ex, sl[rr], l);
-          else if (src[rr]) lds_put(lb, cur + ex, src[rr], l);
+          if constexpr (SLOT) {
+            if (PQ_BA_STORES) lds_put_slot_st<SV>(lb, cur + ex, sl[rr], l);
+            else lds_put_slot<SV>(lw, cur + ex, sl[rr], l);
+          } else if (src[rr]) {
+            lds_put(lb, cur + ex, src[rr], l);
+          }
         }
         wave_lds_sync();
         const uint32_t end = cur + T, full = end >> 4;
@@ -438,8 +477,10 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         if (full) {
           if (lane == 0) wb[0] = wb[full];  // the unfinished piece becomes piece 0
           wave_lds_sync();
-          for (uint32_t k = 1 + lane; k <= full; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
-          wave_lds_sync();
+          if (!PQ_BA_STORES) {
+            for (uint32_t k = 1 + lane; k <= full; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_sync();
+          }
           gblk += 16 * full;
           own = 0;
         }

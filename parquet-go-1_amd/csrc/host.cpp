@@ -518,6 +518,9 @@ struct pqgpu_batch {
   std::vector<uint32_t> slot_chunks;   // byte-array dictionaries materialised in slots
   uint32_t slot_grid_x = 0;
   bool any_ba_sync = false;
+  // byte-array tile bases: k_ba_sums + k_ba_scan before k_ba_emit (default), or k_ba_emit's
+  // decoupled look-back (PQ_BA_LOOKBACK=1)
+  bool ba_presum = !(getenv("PQ_BA_LOOKBACK") && atoi(getenv("PQ_BA_LOOKBACK")) == 1);
   uint8_t *d_payload = nullptr;         // payload arena of the bounded byte-array chunks
   size_t d_payload_cap = 0;
   // device
@@ -1570,6 +1573,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       cd.ba_ntiles = 0;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
         cd.ba_ntiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
+      if (!hc.ba_sync && b->ba_presum) cd.flags |= CF_BA_PRESUM;
       if (hc.ba_sync) {
         cd.flags |= CF_BA_SYNC;
         cd.payload = hc.payload ? (uint64_t)hc.payload : 0;  // (re)sized after the scan of each decode
@@ -1909,9 +1913,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
     HIPCHECK(timed(b, 12, s, l.n_slot_chunks, [&] { return launch_dict_slots(d, l, s); }), err);
-    if (b->any_ba_sync) {
+    if (b->any_ba_sync || b->ba_presum) {
       HIPCHECK(timed(b, 4, s, l.n_ba_tiles, [&] { return launch_ba_sums(d, l, s); }), err);
       HIPCHECK(timed(b, 5, s, l.n_ba_chunks, [&] { return launch_ba_scan(d, l, s); }), err);
+    }
+    if (b->any_ba_sync) {
       // chunks without an upload-time payload bound (DELTA_BYTE_ARRAY pages): size them now
       std::vector<uint64_t> totals(nc);
       HIPCHECK(hipMemcpyAsync(totals.data(), A + b->o_ba_totals, (size_t)nc * 8, hipMemcpyDeviceToHost, s), err);
@@ -2075,7 +2081,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
           kb[20] += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_PLAIN_BOOL ? 1 : w);  // k_values_copy
         if (pd.vkind == VK_DICT || pd.vkind == VK_RLE_BOOL) kb[2] += pd.val_len;  // k_scan_runs: index streams
         if (w == 0 && pd.vkind == VK_DICT) {
-          if (hc.ba_sync) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices (CF_BA_SYNC chunks)
+          if (hc.ba_sync || b->ba_presum) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices
           kb[6] += pd.val_len;
           ba_dict_nn += nn[p];
         } else if ((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values) {
@@ -2101,7 +2107,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       } else {
         // lengths of the non-dictionary pages: read by k_ba_sums; read with their sources and
         // bytes by k_ba_emit, which writes every offset and the payload
-        if (hc.ba_sync) kb[4] += 4 * ba_other_nn;
+        if (hc.ba_sync || b->ba_presum) kb[4] += 4 * ba_other_nn;
         kb[6] += 4 * (hc.nn + 1) + hc.payload_bytes + 12 * ba_other_nn;
         kb[5] += 16 * (int64_t)b->chunk_desc[c].ba_ntiles;
         if (hc.slot_shift) kb[12] += (int64_t)hc.dict_len + 8 * (int64_t)hc.dict_count + ((int64_t)hc.dict_count << hc.slot_shift);

@@ -216,14 +216,36 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
             const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
             const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
             if (ok && adv >= 64) {
+              // Stride speculation: lane k decodes the header that would start k runs further on if
+              // the next runs had this run's header (same varint length, kind and count: writers emit
+              // maximal literal runs back to back). Lanes 0 .. m-1 with that header are exact chain
+              // nodes by induction (lane j's position is true and its run is adv long); lane m's
+              // position is the true next header whatever it holds.
               const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - done;
-              const uint32_t take = min(nv, rem);
-              sink.one(done, take, isbp != 0, val, pos);
+              const uint64_t Pk = (uint64_t)pos + (uint64_t)lane * adv;
+              bool same = lane == 0;
+              uint32_t vk = val;
+              if (lane > 0 && Pk < lim && Pk < n) {
+                const uint32_t o = (uint32_t)Pk - sb;
+                const uint32_t a0 = lds_ld32(L.win, o), a1 = lds_ld32(L.win, o + 4);
+                const uint32_t tk = ~a0 & 0x80808080u;
+                const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
+                const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
+                const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
+                const uint32_t rk = (uint32_t)((((uint64_t)a1 << 32) | a0) >> (8 * Lk));
+                vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
+                same = tk != 0 && Lk == Lv && hk == h && Pk + adv <= n && (isbp || bw >= 32 || (vk >> bw) == 0);
+              }
+              const uint64_t nb = ~__ballot(same);
+              const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);  // runs that cover rem
+              const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, mneed);
+              const uint32_t first = done + lane * nv;  // < need for lanes < m
+              sink.window(lane < m, first, lane < m ? min(nv, need - first) : 0u, isbp != 0, vk, (uint32_t)Pk, L.win, sb);
               st.lap(0);
-              st.add(5, 1);
-              done += take;
-              if (nv >= rem) break;
-              pos += (uint32_t)adv;
+              st.add(5, m);
+              if (m == mneed) { done = need; break; }
+              done += m * nv;
+              pos += (uint32_t)(m * adv);
               continue;
             }
           }
@@ -1769,6 +1791,44 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values
   uint32_t first_err = 0xffffffffu;
   uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
+  if (!is_bool && (w == 4 || w == 8)) {
+    // the 16 rounds' indices first (LDS), then all gathers in flight at once, then the stores
+    uint32_t idx[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+      const uint32_t v = seg0 + r * 64 + lane;
+      idx[r] = ~0u;
+      if (v >= t.v0 && v < t.v1) {
+        const uint32_t x = dict_tile_value(t, lds, ri, v);
+        if (x < dcount) idx[r] = x;
+        else first_err = min(first_err, v);
+      }
+    }
+    if (w == 4) {
+      const uint32_t *dv = gp_u64<const uint32_t>(cd.dict_values);
+      uint32_t *out = gp_u64<uint32_t>(cd.values) + vb + seg0 + lane;
+      uint32_t val[16];
+#pragma unroll
+      for (uint32_t r = 0; r < 16; r++) val[r] = idx[r] != ~0u ? dv[idx[r]] : 0u;
+#pragma unroll
+      for (uint32_t r = 0; r < 16; r++)
+        if (idx[r] != ~0u) out[r * 64] = val[r];
+    } else {
+      const uint64_t *dv = gp_u64<const uint64_t>(cd.dict_values);
+      uint64_t *out = gp_u64<uint64_t>(cd.values) + vb + seg0 + lane;
+#pragma unroll
+      for (uint32_t h = 0; h < 16; h += 8) {
+        uint64_t val[8];
+#pragma unroll
+        for (uint32_t r = 0; r < 8; r++) val[r] = idx[h + r] != ~0u ? dv[idx[h + r]] : 0ull;
+#pragma unroll
+        for (uint32_t r = 0; r < 8; r++)
+          if (idx[h + r] != ~0u) out[(h + r) * 64] = val[r];
+      }
+    }
+    if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
+    return;
+  }
   for (uint32_t r = 0; r < 16; r++) {
     const uint32_t v = seg0 + r * 64 + lane;
     if (v < t.v0 || v >= t.v1) continue;
@@ -1781,11 +1841,7 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
       first_err = min(first_err, v);
       continue;
     }
-    if (w == 4) {
-      (gp_u64<uint32_t>(cd.values))[vb + v] = (gp_u64<const uint32_t>(cd.dict_values))[idx];
-    } else if (w == 8) {
-      (gp_u64<uint64_t>(cd.values))[vb + v] = (gp_u64<const uint64_t>(cd.dict_values))[idx];
-    } else {
+    {
       const uint8_t *src = gp_u64<const uint8_t>(cd.dict_values) + (uint64_t)idx * w;
       uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v) * w;
       for (uint32_t k = 0; k < w; k++) dst[k] = src[k];
