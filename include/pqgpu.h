@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 6
+#define PQGPU_ABI_VERSION 7
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -402,6 +402,9 @@ typedef struct {
   double h2d_ms;           /* GPU: upload enqueue .. done, summed over row groups */
   double decode_ms;        /* GPU: decode launches .. done, summed over row groups */
   double index_ms;         /* device_index: byte-range copy + device page walk, summed (part of plan_ms) */
+  /* device_index builds (pqgpu_page_index_stats summed): result re-reads, chunks whose walk never
+   * reported (walked by the host), chunks the host walked for any reason */
+  int64_t ix_polls, ix_unreported, ix_fallback_chunks;
 } pqgpu_pipeline_stats;
 /* rgs / cols may be NULL for all row groups / all columns. */
 int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const int32_t *rgs, int32_t n_rgs, const int32_t *cols,

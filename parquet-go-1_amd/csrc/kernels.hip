@@ -2513,6 +2513,18 @@ DEV uint32_t delta_blk_len_v(const uint32_t *win, int32_t win0, uint32_t pos, ui
   return sgpr(bl * ok);
 }
 
+// The same per lane (positions differ between lanes): 0 = not a fast block.
+DEV uint32_t delta_blk_len_lane(const uint32_t *win, int32_t win0, uint32_t pos, uint32_t mbc, uint32_t g8) {
+  const uint32_t off = (uint32_t)((int32_t)pos - win0), a = off >> 2, sh = off & 3;
+  const uint32_t x0 = win[a], x1 = win[a + 1], x2 = win[a + 2];
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(x1, x0, sh), u1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+  const uint32_t t = ~u0 & 0x80808080u;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+  const uint32_t ww = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * L)) & (mbc >= 4 ? ~0u : ((1u << (8 * mbc)) - 1u));
+  const uint32_t bl = __umul24(g8, __builtin_amdgcn_sad_u8(ww, 0u, 0u)) + L + mbc;
+  return (t != 0 && L + mbc <= 8) ? bl : 0u;
+}
+
 // One DELTA_BINARY_PACKED stream to decode: an INT32/INT64 page's values section, or a
 // lengths stream of a DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page (validated on the host).
 struct DeltaStream {
@@ -2600,9 +2612,16 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
         while (mbc <= 4 && k < kmax) {
           const uint32_t bl = delta_blk_len_v(L.win, win0, p, mbc, g8);
           if (!bl || p + bl > lim) break;
-          if (lane == 0) L.hpos[k] = p;
-          k++;
-          p += bl;
+          // stride speculation: lane j takes the block that starts j blocks on if the blocks between
+          // have this block's length (writers with steady miniblock widths); lanes 0 .. m-1 whose
+          // block has that length are true block starts by induction
+          const uint64_t Pj = (uint64_t)p + (uint64_t)lane * bl;
+          const uint32_t bj = lane == 0 ? bl : (Pj + bl <= lim ? delta_blk_len_lane(L.win, win0, (uint32_t)Pj, mbc, g8) : 0u);
+          const uint64_t nb = ~__ballot(bj == bl);
+          const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, kmax - k);
+          if (lane < m) L.hpos[k + lane] = (uint32_t)Pj;
+          k += m;
+          p += m * bl;
         }
         // one block by the exact rules (or the end of the walk)
         if (k >= kmax) break;

@@ -139,6 +139,8 @@ static void worker(pqgpu_pipeline *p) {
     const int32_t rg = p->rgs[(size_t)i];
     pqgpu_page_index *ix = p->device_index ? index_row_group(p, sl, rg) : nullptr;
     const double ixms = ix ? ms_since(tp) : 0.0;
+    int32_t ix_polls = 0, ix_unrep = 0, ix_fb = 0;
+    if (ix) (void)pqgpu_page_index_stats(ix, &ix_polls, &ix_unrep, &ix_fb, nullptr);
     for (size_t k = 0; k < p->cols.size(); k++) {
       int32_t id;
       pqgpu_error e;
@@ -162,6 +164,9 @@ static void worker(pqgpu_pipeline *p) {
       sl->state = LAUNCHED;
       p->st.plan_ms += plan;
       p->st.index_ms += ixms;
+      p->st.ix_polls += ix_polls;
+      p->st.ix_unreported += ix_unrep;
+      p->st.ix_fallback_chunks += ix_fb;
       p->st.upload_ms += up;
     }
     p->cv.notify_all();

@@ -110,7 +110,8 @@ class PipelineStats(ctypes.Structure):
     _fields_ = [("row_groups", ctypes.c_int64), ("rows", ctypes.c_int64), ("chunks", ctypes.c_int64),
                 ("failed_chunks", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
                 ("wall_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
-                ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("index_ms", ctypes.c_double)]
+                ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("index_ms", ctypes.c_double),
+                ("ix_polls", ctypes.c_int64), ("ix_unreported", ctypes.c_int64), ("ix_fallback_chunks", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -118,7 +119,7 @@ class PipelineStats(ctypes.Structure):
 
 _LIB = None
 TIMER_SLOTS = 21  # PQGPU_TIMER_SLOTS
-ABI_VERSION = 6  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+ABI_VERSION = 7  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",

@@ -129,6 +129,8 @@ def test_gpu_pipeline_parity(gpu_ctx, name, depth, threads, device_index):
     st = p.stats()
     assert st["row_groups"] == f.num_row_groups and st["chunks"] == f.num_row_groups * f.num_columns
     assert (st["index_ms"] > 0) == device_index
+    # every device walk reported on the first read-back
+    assert st["ix_polls"] == 0 and st["ix_unreported"] == 0, st
     p.close()
 
 

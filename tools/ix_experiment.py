@@ -48,6 +48,26 @@ def main():
             out["builds_with_unreported"] += int(st["unreported"] > 0)
             ix.close()
         out["per_fixture"][name] = agg
+    # concurrent builds: the streaming pipeline's worker threads build the indexes of different row
+    # groups at once, each on its own slot stream (the configuration of the original failures)
+    for name in ("cfg5_small", "cfg2_v2_small", "cfg4_small"):
+        try:
+            data = pqtest.load(name)
+        except Exception:
+            continue
+        f = pqgpu.File(data)
+        rgs = list(range(f.num_row_groups)) * max(1, 64 // max(1, f.num_row_groups))
+        p = pqgpu.Pipeline(ctx, f, row_groups=rgs, depth=8, threads=8, device_index=True)
+        fails = 0
+        for _rg, _b, err in p:
+            fails += err is not None
+        st = p.stats()
+        p.close()
+        out["per_fixture"][name + "_pipeline"] = {"row_groups": len(rgs), "polls": st["ix_polls"],
+                                                  "unreported": st["ix_unreported"],
+                                                  "fallback_chunks": st["ix_fallback_chunks"], "failed_row_groups": fails}
+        out["polls"] += st["ix_polls"]
+        out["unreported"] += st["ix_unreported"]
     print(json.dumps(out), flush=True)
 
 
