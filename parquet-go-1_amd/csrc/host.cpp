@@ -511,6 +511,7 @@ struct pqgpu_batch {
   // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr, ev_delta_join = nullptr;
+  hipEvent_t ev_levels = nullptr, ev_nest_join = nullptr;
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
   uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
@@ -1840,6 +1841,22 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (e == hipSuccess) e = hipEventRecord(b->ev_delta_join, ds);
     return e;
   };
+  // Nested (Arrow-style) arrays and struct bitmaps need only the decoded levels and the per-tile
+  // counts k_level_fill wrote: they run on the DELTA stream (after its DELTA pages) beside the values
+  // path, from the moment k_bases is queued; the batch stream joins them at the end.
+  if (!b->ev_levels) HIPCHECK(hipEventCreateWithFlags(&b->ev_levels, hipEventDisableTiming), err);
+  if (!b->ev_nest_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_nest_join, hipEventDisableTiming), err);
+  const bool any_nest = l.n_nest_chunks || l.n_nest_tiles || l.n_grp_tiles;
+  auto fork_nest = [&]() -> hipError_t {
+    if (!any_nest) return hipSuccess;
+    hipError_t e = hipEventRecord(b->ev_levels, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ds, b->ev_levels, 0);
+    if (e == hipSuccess) e = timed(b, 16, ds, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, ds); });
+    if (e == hipSuccess) e = timed(b, 14, ds, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, ds); });
+    if (e == hipSuccess) e = timed(b, 14, ds, l.n_grp_tiles, [&] { return launch_group_flat(d, l, ds); });  // flat leaves
+    if (e == hipSuccess) e = hipEventRecord(b->ev_nest_join, ds);
+    return e;
+  };
   // PLAIN / BOOLEAN copies (k_values_copy) run on the copy stream beside everything else once
   // their value bases are known: at the start in speculative mode, after k_bases otherwise.
   hipStream_t cs = b->ctx->copy;
@@ -1883,6 +1900,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(fork_nest(), err);
     if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);
@@ -1902,6 +1920,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     } else {
       HIPCHECK(fork_delta(b->ev_fork), err);
     }
+    HIPCHECK(fork_nest(), err);  // on the DELTA stream after its pages
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
     HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
@@ -1953,9 +1972,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)
   // (the per-tile nested counts were added by k_level_fill; k_nest_count re-read the levels for them)
-  HIPCHECK(timed(b, 16, s, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, s); }), err);
-  HIPCHECK(timed(b, 14, s, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, s); }), err);
-  HIPCHECK(timed(b, 14, s, l.n_grp_tiles, [&] { return launch_group_flat(d, l, s); }), err);  // struct bitmaps, flat leaves
+  if (any_nest) HIPCHECK(hipStreamWaitEvent(s, b->ev_nest_join, 0), err);  // nested arrays (fork_nest)
   b->decoded = true;
   return PQ_OK;
 }
@@ -2323,6 +2340,8 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (b->ev_copy) (void)hipEventDestroy(b->ev_copy);
   if (b->ev_copy_join) (void)hipEventDestroy(b->ev_copy_join);
   if (b->ev_delta_join) (void)hipEventDestroy(b->ev_delta_join);
+  if (b->ev_levels) (void)hipEventDestroy(b->ev_levels);
+  if (b->ev_nest_join) (void)hipEventDestroy(b->ev_nest_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);

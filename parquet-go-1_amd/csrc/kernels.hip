@@ -599,64 +599,6 @@ DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uin
   lv_emit_run<BW1>(sk, L.stage, sb, send, f, cnt, bp, value);
 }
 
-// Bit width 1 with validity output (flat OPTIONAL pages): the chunk's values [done, end) from its
-// run list (LDS rbuf, chain order: first value, bit-packed flag | payload position, or the RLE
-// value), written straight into the chunk bitmap by output word. Thread t assembles a contiguous
-// block of the words covering global bits [slot_base + done, slot_base + end): one binary search for
-// its first run, then a cursor; a word takes its bits from every run that overlaps it (value k of a
-// bit-packed run is payload bit k; an RLE run is all ones iff its value is maxD). Words the chunk
-// owns whole are stored, the two edge words (shared with the neighbouring chunk or page) are OR-ed.
-// No LDS bitmap, no atomics inside the range, the same work per thread whatever the run lengths.
-DEV void lv_bw1_words(const LevelLDS &L, LevelSink &sk, uint32_t cs, uint32_t send, uint32_t done, uint32_t end,
-                      uint32_t nr) {
-  if (end <= done || nr == 0 || !sk.bits_glob) return;
-  const uint64_t b0 = sk.slot_base + done, b1 = sk.slot_base + end;  // global bits [b0, b1)
-  const uint64_t w0 = b0 >> 5, w1 = (b1 + 31) >> 5;
-  const uint32_t nw = (uint32_t)(w1 - w0);
-  const uint32_t K = (nw + kLvThreads - 1) / kLvThreads;
-  const uint32_t wa = threadIdx.x * K, wb = min(nw, wa + K);
-  if (wa >= wb) return;
-  const int64_t vb0 = (int64_t)((w0 + wa) << 5) - (int64_t)sk.slot_base;  // page value of the first word's bit 0
-  const uint32_t vfirst = (uint32_t)max(vb0, (int64_t)done);
-  uint32_t lo = 0, hi = nr;  // the last run starting at or before vfirst
-  while (hi - lo > 1) {
-    const uint32_t m = (lo + hi) >> 1;
-    if (L.rbuf[m].x <= vfirst) lo = m; else hi = m;
-  }
-  uint32_t r = lo;
-  uint2 R = L.rbuf[r];
-  uint32_t rnext = r + 1 < nr ? L.rbuf[r + 1].x : 0xffffffffu;
-  uint32_t *bits = gp(sk.bits_glob);
-  for (uint32_t w = wa; w < wb; w++) {
-    const uint64_t gw = w0 + w;
-    const int64_t base = (int64_t)(gw << 5) - (int64_t)sk.slot_base;
-    const uint32_t va = (uint32_t)max(base, (int64_t)done), ve = (uint32_t)min(base + 32, (int64_t)end);
-    uint32_t word = 0;
-    for (uint32_t v = va; v < ve;) {
-      while (rnext <= v) {
-        R = L.rbuf[++r];
-        rnext = r + 1 < nr ? L.rbuf[r + 1].x : 0xffffffffu;
-      }
-      const uint32_t e = min(rnext, ve), cnt = e - v, sh = (uint32_t)((int64_t)v - base);
-      uint32_t x;
-      if (R.y >> 31) {  // bit-packed, width 1
-        const uint64_t bo = (uint64_t)(R.y & 0x7fffffffu) * 8 + (v - R.x);
-        const uint32_t by = (uint32_t)(bo >> 3);
-        x = (by >= cs && by + 8 <= send) ? (uint32_t)lds_bits64(L.stage, (uint32_t)(bo - (uint64_t)cs * 8), cnt)
-                                        : bits32c(sk.s, sk.n, bo, cnt);
-      } else {
-        x = R.y == sk.cmp ? ~0u : 0u;
-      }
-      word |= (x & (cnt >= 32 ? ~0u : ((1u << cnt) - 1u))) << sh;
-      v = e;
-    }
-    sk.count += __popc(word);
-    const bool edge = (w == 0 && (b0 & 31)) || (gw == w1 - 1 && (b1 & 31));
-    if (!edge) bits[gw] = word;
-    else if (word) atomicOr(&bits[gw], word);
-  }
-}
-
 // Decode `need` level values of one stream into the sink; every thread of the workgroup
 // calls this (control flow outside per-lane work is workgroup-uniform). Chunks are fixed
 // stream ranges [k * kLvChunk, (k + 1) * kLvChunk); the chain enters chunk k where it left
@@ -818,8 +760,8 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     uint64_t mine = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 8; k++) mine += (mbits >> k) & 1u ? nv[k] : 0u;
-    // the marked runs' count rides in bits 48.. of the scan (values < 2^41)
-    mine += (uint64_t)__popc(mbits) << kLvRunShift;
+    // generic widths: the marked runs' count rides in bits 48.. of the scan (values < 2^41)
+    if constexpr (!BW1) mine += (uint64_t)__popc(mbits) << kLvRunShift;
     for (uint32_t mm = mbits; mm; mm &= mm - 1) {
       const uint32_t k = __builtin_ctz(mm);
       if (L.J0[i0 + k] == i0 + k) {  // a stop on the chain: the exact decoder (hybrid_decoder.go:142-165)
@@ -841,10 +783,12 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       total += t;
     }
     uint64_t ex = before + incl - mine;
-    // this thread's first entry in the chunk's part of the run table (bit width 1: the chunk's run list)
-    uint32_t ri = (BW1 ? 0u : runs_done) + (uint32_t)(ex >> kLvRunShift);
-    ex &= kLvValMask;
-    total &= kLvValMask;
+    uint32_t ri = 0;  // generic widths: this thread's first entry in the chunk's part of the run table
+    if constexpr (!BW1) {
+      ri = runs_done + (uint32_t)(ex >> kLvRunShift);
+      ex &= kLvValMask;
+      total &= kLvValMask;
+    }
     if (tid == 0) L.total = total;
     uint64_t v = (uint64_t)done + ex;  // value index of this thread's first marked run
     // Generic widths: the marked runs go to the stream's run table in global memory, in chain
@@ -853,9 +797,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     // and an error stop come last in chain order and are not written.
     auto put = [&](uint32_t f, uint32_t cnt, uint32_t bp, uint32_t value) {
       if constexpr (BW1) {
-        (void)cnt;
-        L.rbuf[ri++] = make_uint2(f, bp ? 0x80000000u | value : value);
-        atomicAdd(&L.nput, 1u);
+        lv_fill_run<true>(L, sk, cs, send, f, cnt, bp, value);
       } else {
         put_run(ri++, f, cnt, bp, value);
       }
@@ -892,10 +834,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
     }
     st.lap(5);
     wg_barrier();
-    if constexpr (BW1) {
-      if (!PQ_ABLATE(sk, 2))  // diagnostic: no expansion
-        lv_bw1_words(L, sk, cs, send, done, (uint32_t)min((uint64_t)done + L.total, (uint64_t)need), L.nput);
-    } else {
+    if constexpr (!BW1) {
       pend_base = runs_done;
       pend_n = L.nput;
       pend_t = min(L.ntb, kLvTileBuf);
@@ -941,6 +880,7 @@ DEV void levels_page(const BatchDev &b, const uint32_t *pages, LevelLDS &lds) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint32_t ns = pd.num_slots;
   uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  for (uint32_t k = tid; k < kSegSlots / 32; k += blockDim.x) lds.bits[k] = 0;
   uint32_t nn = ns;  // constDecoder(0) == maxD(0): every slot is a value
   PQ_STAMPS(st, b.dbg);
   st.begin();
@@ -953,7 +893,7 @@ DEV void levels_page(const BatchDev &b, const uint32_t *pages, LevelLDS &lds) {
     sk.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
     sk.out = rep ? gp_u64<uint8_t>(cd.rep_levels) + pd.slot_base
                  : (cd.def_levels ? gp_u64<uint8_t>(cd.def_levels) + pd.slot_base : nullptr);
-    sk.bits_lds = nullptr;  // bit width 1: words go straight to the chunk bitmap (lv_bw1_words)
+    sk.bits_lds = rep ? nullptr : lds.bits;
     sk.bits_glob = rep ? nullptr : vbits;
     sk.slot_base = pd.slot_base;
     sk.cmp = rep ? 0u : (uint32_t)cd.max_def;
@@ -988,6 +928,26 @@ DEV void levels_page(const BatchDev &b, const uint32_t *pages, LevelLDS &lds) {
       nn = (uint32_t)cntv;
     }
     wg_barrier();
+  }
+  if (cd.max_def > 0) {
+    wg_barrier();
+    // flush the LDS bitmap segment to the chunk bitmap
+    const uint32_t seg = min(ns, kSegSlots);
+    const uint32_t nw = (seg + 31) / 32;
+    const uint32_t sh = (uint32_t)(pd.slot_base & 31);
+    const uint64_t w0 = pd.slot_base >> 5;
+    for (uint32_t k = tid; k < nw; k += blockDim.x) {
+      uint32_t v = lds.bits[k];
+      if (k == nw - 1 && (seg & 31)) v &= (1u << (seg & 31)) - 1u;
+      if (sh == 0) {
+        if (k == 0 || k == nw - 1) atomicOr(&vbits[w0 + k], v);
+        else vbits[w0 + k] = v;
+      } else if (v) {
+        atomicOr(&vbits[w0 + k], v << sh);
+        uint32_t hi = v >> (32 - sh);
+        if (hi) atomicOr(&vbits[w0 + k + 1], hi);
+      }
+    }
   }
   st.lap(6);
   st.flush(0);
