@@ -380,7 +380,7 @@ struct KernelTimer {
   }
 };
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
-    "k_levels", "k_values[delta]", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
+    "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
     "k_values_copy"};
@@ -1424,8 +1424,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->copy_fused = cf ? atoi(cf) != 0 : b->spec;
   }
   const bool fused = b->copy_fused;
+  // ranks: DELTA tiles, DELTA pages, fused PLAIN / BOOLEAN copies (these three are k_values_delta's
+  // launch: latency-bound pages first, the bandwidth-bound copies fill the CUs around them), the
+  // LDS-staged kinds (k_values), unfused copies (k_values_copy)
   auto rank = [fused](uint8_t k) {
-    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : (!fused && (k == WI_PLAIN || k == WI_BOOL)) ? 3 : 2;
+    const bool copy = k == WI_PLAIN || k == WI_BOOL;
+    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 4) : 3;
   };
   std::stable_sort(b->items.begin(), b->items.end(),
                    [&](const WorkItem &x, const WorkItem &y) { return rank(x.kind) < rank(y.kind); });
@@ -1433,9 +1437,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->n_delta_tiles = 0;
   b->n_copy_items = 0;
   for (auto &it : b->items) {
-    b->n_delta_items += it.kind == WI_DELTA || it.kind == WI_DELTA_TILE || it.kind == WI_DELTA_PAGE;
+    b->n_delta_items += rank(it.kind) <= 2;  // k_values_delta's launch
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
-    b->n_copy_items += rank(it.kind) == 3;
+    b->n_copy_items += rank(it.kind) == 4;
   }
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
@@ -2037,7 +2041,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->page_vbase_out = vbase;
   b->page_nn_out = nn;
   int first = PQ_OK;
-  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0, snappy_direct_bytes = 0;
+  int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0, snappy_direct_bytes = 0,
+          cp_bytes = 0;
   int64_t kb[PQGPU_TIMER_SLOTS] = {0};  // algorithmic bytes per launch slot
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -2094,8 +2099,9 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         const PageDesc &pd = b->pages[p];
         lvl_bytes += pd.rep_len + pd.def_len;
         if (pd.vkind == VK_DELTA32 || pd.vkind == VK_DELTA64) dl_bytes += pd.val_len + (int64_t)nn[p] * w;
-        if (!b->copy_fused && (pd.vkind == VK_PLAIN_FIXED || pd.vkind == VK_PLAIN_INT96 || pd.vkind == VK_PLAIN_BOOL))
-          kb[20] += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_PLAIN_BOOL ? 1 : w);  // k_values_copy
+        if ((pd.vkind == VK_PLAIN_FIXED || pd.vkind == VK_PLAIN_INT96 || pd.vkind == VK_PLAIN_BOOL) &&
+            !((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values))
+          cp_bytes += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_PLAIN_BOOL ? 1 : w);  // the copies' launch
         if (pd.vkind == VK_DICT || pd.vkind == VK_RLE_BOOL) kb[2] += pd.val_len;  // k_scan_runs: index streams
         if (w == 0 && pd.vkind == VK_DICT) {
           if (hc.ba_sync || b->ba_presum) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices
@@ -2149,9 +2155,10 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
   }
   kb[0] = lvl_bytes;
-  kb[1] = dl_bytes;
+  kb[20] = b->copy_fused ? 0 : cp_bytes;            // k_values_copy
+  kb[1] = dl_bytes + (b->copy_fused ? cp_bytes : 0);  // k_values_delta: DELTA pages (+ the fused copies)
   val_bytes -= snappy_direct_bytes;
-  kb[9] = val_bytes - kb[20] - dl_bytes;  // k_values: the LDS kinds other than DELTA (dictionary tiles, ...)
+  kb[9] = val_bytes - cp_bytes - dl_bytes;  // k_values: the LDS kinds other than DELTA (dictionary tiles, ...)
   kb[8] = val_bytes - dl_bytes;
   kb[11] = b->stats.snappy_kernel_bytes;
   memcpy(b->slot_bytes, kb, sizeof(kb));

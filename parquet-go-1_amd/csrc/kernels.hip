@@ -189,10 +189,67 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
     }
     if (tid < 8) L.win[kScanVec * 4 + tid] = 0;
   };
-  fetch(0);
+  uint32_t pos = 0, done = 0;
+  // Prelude (wave 0): while the runs are long (>= 64 stream bytes) the chain is followed by stride
+  // speculation straight from global memory — lane k reads the 8 header bytes k runs ahead — so a
+  // stream of maximal literal runs is walked without staging its payload in LDS at all (a dictionary
+  // page's payload is read later, by the tiles that decode it). Anything else (a short run, a run
+  // that differs, the stream end, an error) stops the prelude; the windowed walk below takes over
+  // at that position with the reference's exact semantics.
+  if (wv == 0) {
+    const uint8_t *sg = gp_u64<const uint8_t>((uint64_t)(uintptr_t)s);
+    while (done < need && pos < n) {
+      const uint64_t x0 = ld64(sg + pos);  // bytes past the stream end are never used (checks below)
+      const uint32_t u0 = sgpr((uint32_t)x0), u1 = sgpr((uint32_t)(x0 >> 32));
+      const uint32_t tm = ~u0 & 0x80808080u;
+      if (!tm) break;
+      const uint32_t Lv = (uint32_t)(__builtin_ctz(tm) >> 3) + 1;
+      const uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
+      const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+      const uint32_t cnt = h >> 1, isbp = h & 1u;
+      const uint64_t adv = isbp ? Lv + (uint64_t)cnt * bw : (uint64_t)(Lv + rs);
+      const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
+      const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
+      const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
+      if (!(ok && adv >= 64)) break;
+      const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - done;
+      const uint64_t Pk = (uint64_t)pos + (uint64_t)lane * adv;
+      bool same = lane == 0;
+      uint32_t vk = val;
+      if (lane > 0 && Pk + adv <= n) {
+        const uint64_t xk = ld64(sg + Pk);
+        const uint32_t a0 = (uint32_t)xk;
+        const uint32_t tk = ~a0 & 0x80808080u;
+        const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
+        const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
+        const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
+        const uint32_t rk = (uint32_t)(xk >> (8 * Lk));
+        vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
+        same = tk != 0 && Lk == Lv && hk == h && (isbp || bw >= 32 || (vk >> bw) == 0);
+      }
+      const uint64_t nb = ~__ballot(same);
+      const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);
+      const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, mneed);
+      const uint32_t first = done + lane * nv;
+      sink.window(lane < m, first, lane < m ? min(nv, need - first) : 0u, isbp != 0, vk, (uint32_t)Pk, nullptr, 0u);
+      st.add(5, m);
+      if (m == mneed) { done = need; break; }
+      done += m * nv;
+      pos += (uint32_t)(m * adv);
+    }
+    if (lane == 0) { L.ctl_pos = pos; L.ctl_done = done; }
+  }
+  wg_barrier();
+  pos = L.ctl_pos;
+  done = L.ctl_done;
+  if (done >= need) {
+    if (wv == 0) st.flush(56);
+    return done;
+  }
+  uint32_t w = (pos + sbase) / kScanWin;  // the window holding the chain's position
+  fetch(w);
   store();
-  fetch(1);
-  uint32_t w = 0, pos = 0, done = 0;
+  fetch(w + 1);
   wg_barrier();
   for (;;) {
     if (wv == 0) {
@@ -2904,9 +2961,11 @@ __global__ void __launch_bounds__(256) k_values_copy(BatchDev b_in, const WorkIt
   else do_bool(b, wi, pd, cd, nn);
 }
 
-// DELTA_BINARY_PACKED work items (pages, tiles, the scalar path) in their own launch: the kernel's
-// registers and LDS are the DELTA decoder's alone, not the maximum over every work-item kind, so
-// the level kernels and the zero-LDS copies fit on a CU beside its workgroups.
+// DELTA_BINARY_PACKED work items (pages, tiles, the scalar path) in their own launch, followed in
+// the speculative schedule by the PLAIN / BOOLEAN copies (the latency-bound pages are dispatched
+// first and the bandwidth-bound copies fill the CUs around them): the kernel's registers and LDS
+// are the DELTA decoder's, not the maximum over every work-item kind (dictionary tiles stay in
+// k_values).
 union DeltaLDS {
   DeltaTileLDS dtile;
   DeltaPageLDS dpage;
@@ -2922,6 +2981,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
+    case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;  // fused copies (speculative schedule)
+    case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
   }
 }
 
