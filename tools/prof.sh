@@ -19,5 +19,5 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $CMD > $OUT/write.log 2>&1 &&
 timeout -s KILL 150 rocprofv3 --pmc $SQ --output-format csv -d $OUT/sq -o run -- $CMD > $OUT/sq.log 2>&1
 rc=$?
-tail -3 $OUT/*.log
+tail -n 3 $OUT/*.log
 exit $rc
