@@ -1838,7 +1838,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // beside the level kernels, the copies and the other values kinds; the default stream joins it
   hipStream_t ds = b->ctx->delta;
   if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
+  // streams with nothing to run are neither forked nor joined (a cross-stream wait costs latency)
+  const bool any_delta = l1.n_items || l.n_delta_pages;
   auto fork_delta = [&](hipEvent_t after) -> hipError_t {
+    if (!any_delta) return hipSuccess;
     hipError_t e = hipStreamWaitEvent(ds, after, 0);
     if (e == hipSuccess) e = timed(b, 10, ds, l.n_delta_pages, [&] { return launch_delta_prep(d, l, ds); });
     if (e == hipSuccess) e = timed(b, 1, ds, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, ds); });
@@ -1867,6 +1870,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (!b->ev_copy) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming), err);
   if (!b->ev_copy_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy_join, hipEventDisableTiming), err);
   auto fork_copies = [&](hipStream_t from) -> hipError_t {
+    if (!l.n_copy_items) return hipSuccess;
     hipError_t e = hipEventRecord(b->ev_copy, from);
     if (e == hipSuccess) e = hipStreamWaitEvent(cs, b->ev_copy, 0);
     if (e == hipSuccess) e = timed(b, 20, cs, l.n_copy_items, [&] { return launch_values_copy(d, l, cs); });
@@ -1877,7 +1881,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
     // side stream concurrently with the level decode; k_bases then checks the header counts
     // the values path used against the decoded ones (sync_impl re-runs serially on a miss).
-    hipStream_t v = b->ctx->side;
+    // no level streams in the batch (REQUIRED columns only): the values path runs on the batch stream
+    const bool lvl = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
+    hipStream_t v = lvl ? b->ctx->side : s;
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
     // PQ_COPY_MODE 4: the copies beside the level kernels, the values path after them;
@@ -1888,7 +1894,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
-    HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
+    if (v != s) HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(fork_delta(b->ev_fork), err);
     HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
     if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
@@ -1898,18 +1904,18 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->copy_mode == 1) HIPCHECK(fork_copies(v), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
     HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
-    HIPCHECK(hipEventRecord(b->ev_join, v), err);
-    if (val_then_lv) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    if (v != s) HIPCHECK(hipEventRecord(b->ev_join, v), err);
+    if (val_then_lv && v != s) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (!b->levels_first && !lv_then_val)
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(fork_nest(), err);
     if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    if (v != s) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
+    if (l.n_copy_items) HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    if (any_delta) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
@@ -1930,8 +1936,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);  // PQ_COPY_MODE=3: after everything (profiling)
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
+    if (l.n_copy_items) HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    if (any_delta && !b->split_values) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   }
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)

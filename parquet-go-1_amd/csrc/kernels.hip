@@ -2986,7 +2986,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
   }
 }
 
-__global__ void __launch_bounds__(256) k_values(BatchDev b_in, const WorkItem *items) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_values(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
   __shared__ ValuesLDS lds;
   const WorkItem wi = items[blockIdx.x];
