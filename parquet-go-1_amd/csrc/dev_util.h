@@ -84,7 +84,7 @@ DEV BatchDev global_view(BatchDev b) {
   b.page_rec = gp(b.page_rec); b.page_vbase = gp(b.page_vbase); b.page_rbase = gp(b.page_rbase);
   b.nest_cnt = gp(b.nest_cnt); b.nest_base = gp(b.nest_base); b.nest_tot = gp(b.nest_tot);
   b.runs = gp(b.runs); b.run_base = gp(b.run_base); b.run_count = gp(b.run_count);
-  b.tile_first = gp(b.tile_first); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
+  b.tile_first = gp(b.tile_first); b.tile_desc = gp(b.tile_desc); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
   b.ba_tile_page = gp(b.ba_tile_page); b.ba_tile_order = gp(b.ba_tile_order);
   b.ba_state = gp(b.ba_state); b.ba_totals = gp(b.ba_totals);
   b.dblk = gp(b.dblk); b.dblk_base = gp(b.dblk_base); b.dblk_n = gp(b.dblk_n); b.dblk_sum = gp(b.dblk_sum);

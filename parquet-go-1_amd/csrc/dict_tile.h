@@ -29,15 +29,19 @@ struct DictTile {
   uint32_t nr;           // number of runs
   uint64_t sbit;         // stream bit of stage[0] (staged)
   uint32_t v0, v1;       // tile values [v0, v1) after clipping to the runs the scan validated
+  uint32_t lo, hi;       // stream bytes of the tile's bit-packed values (from the descriptor)
   bool staged;
 };
 
-// Open tile [v0, v1) of page `page` (values within the page) without staging: the tile's runs
-// are read from the run table in global memory. Returns false when no value of the tile is
-// decodable (the scan failed before it: the error is already reported at the right value
+// Open tile [v0, v1) of page `page` (values within the page; a whole kDictTile tile, clipped to the
+// page's values) without staging: one read of the tile's descriptor, written by k_scan_runs after its
+// walk ({first run, last run, stream bytes [lo, hi)}, {values the valid runs cover, valid}); the
+// runs are then read from the run table in global memory. Returns false when no value of the tile
+// is decodable (the scan failed before it: the error is already reported at the right value
 // position). Any lane may call it.
 DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
                         DictTile &t, uint32_t &r0, uint32_t &r1) {
+  (void)nn;
   t.s = gp_u64<const uint8_t>(pd.data) + pd.val_off;
   t.n = pd.val_len;
   t.bw = pd.dict_bw;
@@ -47,20 +51,19 @@ DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   t.sbit = 0;
   t.v0 = v0;
   t.v1 = v1;
+  t.lo = t.hi = 0;
   if (t.bw == 0) return v0 < v1;  // bit width 0: every index is 0 and no stream is read
-  const uint32_t nruns = b.run_count[page];
-  if (nruns == 0) return false;
-  const HybRun *rg = b.runs + b.run_base[page];
-  const uint32_t *tf = b.tile_first + b.tile_base[page];
-  const uint32_t tile = v0 / kDictTile;
-  r0 = tf[tile];
-  if (r0 >= nruns) return false;
-  r1 = ((uint64_t)(tile + 1) * kDictTile < nn) ? tf[tile + 1] : nruns - 1;
-  if (r1 >= nruns) r1 = nruns - 1;
-  t.v1 = min(v1, rg[nruns].value_start);  // sentinel: values covered by valid runs
+  const uint64_t di = 2 * ((uint64_t)pd.dict_tile0 + v0 / kDictTile);
+  const uint4 D = b.tile_desc[di], E = b.tile_desc[di + 1];
+  if (!E.y) return false;
+  r0 = D.x;
+  r1 = D.y;
+  t.v1 = min(v1, E.x);  // values covered by valid runs
   if (t.v0 >= t.v1) return false;
   t.nr = r1 - r0 + 1;
-  t.runs = rg + r0;
+  t.runs = b.runs + b.run_base[page] + r0;
+  t.lo = D.z;
+  t.hi = D.w;
   return true;
 }
 
@@ -73,20 +76,13 @@ DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   uint32_t r0 = 0, r1 = 0;
   if (!dict_tile_open(b, pd, page, v0, v1, nn, t, r0, r1)) return false;
   if (t.bw == 0) return true;
-  const HybRun *rg = b.runs + b.run_base[page];
+  const HybRun *rg = t.runs;
   if (t.nr <= kTileRuns) {
-    for (uint32_t k = threadIdx.x; k < t.nr; k += blockDim.x) L.runs[k] = rg[r0 + k];
+    for (uint32_t k = threadIdx.x; k < t.nr; k += blockDim.x) L.runs[k] = rg[k];
     t.runs = L.runs;
   }
-  // stream bytes of the tile's bit-packed values: from the first value's byte to the last's
-  const HybRun f = rg[r0], l = rg[r1];
-  const uint32_t bw = t.bw;
-  uint64_t lo = (f.info & 0x80000000u) ? (uint64_t)f.payload_off + (((uint64_t)(t.v0 - f.value_start) * bw) >> 3)
-                                       : (uint64_t)f.payload_off;
-  uint64_t hi = (l.info & 0x80000000u) && t.v1 > l.value_start
-                    ? (uint64_t)l.payload_off + (((uint64_t)(t.v1 - l.value_start) * bw + 7) >> 3)
-                    : (uint64_t)l.payload_off + 8;
-  hi = min(hi, (uint64_t)t.n);
+  // stream bytes of the tile's bit-packed values (the descriptor's [lo, hi))
+  const uint64_t lo = t.lo, hi = t.hi;
   const uintptr_t ga = ((uintptr_t)(t.s + lo)) & ~(uintptr_t)15;  // 16-B aligned global start
   const uint64_t sb = (uint64_t)(ga - (uintptr_t)t.s);             // its stream offset (may be "negative")
   const uint64_t span = hi > lo ? (hi + 8) - (lo & ~(uint64_t)15) + 16 : 0;

@@ -533,7 +533,7 @@ struct pqgpu_batch {
   // arena offsets of batch-level arrays
   uint64_t o_nnv = 0, o_spec_flag = 0, o_dblk = 0, o_dblk_base = 0, o_dblk_n = 0, o_dblk_sum = 0, l_delta = 0;
   uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
-           o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
+           o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_desc = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_page = 0, o_ba_tile_order = 0, o_ba_totals = 0, l_slot = 0,
            o_ba_state = 0;
   uint64_t l_level_bw1 = 0;
@@ -1308,6 +1308,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
             b->run_base[p] = b->run_total;
             b->run_total += cap;
             b->tile_base[p] = b->tile_total;
+            pd.dict_tile0 = (uint32_t)b->tile_total;
             b->tile_total += (ns_p + kDictTile - 1) / kDictTile;
           }
           if (!is_ba) tiles(WI_DICT, kDictTile);  // byte-array dictionaries: k_ba_sums / k_ba_emit
@@ -1416,6 +1417,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_begin = b->o_err;
   b->o_tile_first = take(b->tile_total * 4);
   b->f_end = a;
+  b->o_tile_desc = take(b->tile_total * 32);
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
   // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
@@ -1723,6 +1725,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.run_base = (const uint64_t *)(A + b->o_run_base);
   d.run_count = (uint32_t *)(A + b->o_run_count);
   d.tile_first = (uint32_t *)(A + b->o_tile_first);
+  d.tile_desc = (uint4 *)(A + b->o_tile_desc);
   d.tile_base = (const uint64_t *)(A + b->o_tile_base);
   d.ba_tile_sum = (uint64_t *)(A + b->o_ba_tile_sum);
   d.ba_tile_page = (const uint32_t *)(A + b->o_ba_tile_page);

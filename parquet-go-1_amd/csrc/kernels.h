@@ -27,6 +27,9 @@ struct BatchDev {
   const uint64_t *run_base;       // [npages] first entry of each page's run table
   uint32_t *run_count;            // [npages]
   uint32_t *tile_first;           // dict tiles: first run index per tile
+  uint4 *tile_desc;               // dict tiles: 2 x uint4 per tile written by k_scan_runs ({r0, r1, lo, hi},
+                                  // {values covered, valid}): dict_tile.h reads one descriptor instead of
+                                  // the run count, two tile_first entries and two runs one after another
   const uint64_t *tile_base;      // [npages] first tile-table entry per page
   uint64_t *ba_tile_sum;          // byte-array tiles: payload bytes per tile, then (k_ba_scan) its
                                   // exclusive base within the chunk

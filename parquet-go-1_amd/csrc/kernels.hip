@@ -1785,6 +1785,36 @@ __global__ void __launch_bounds__(256) k_scan_runs(BatchDev b_in, const uint32_t
     rs.runs[rs.nruns] = sentinel;
     if (rs.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, rs.err_pos, rs.err_code);
   }
+  // Tile descriptors (wave 0, which wrote the run table and the tiles' first runs): for tile t the
+  // runs [r0, r1] its values cross, the stream bytes [lo, hi) its bit-packed values occupy and the
+  // values the valid runs cover — dict_tile.h reads this instead of chasing the table itself.
+  if (threadIdx.x < 64 && nn && pd.dict_bw > 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the lanes' run / tile stores
+    const uint32_t nr = rs.nruns, bw = pd.dict_bw, ntile = (nn + kDictTile - 1) / kDictTile;
+    const uint32_t *tf = b.tile_first + pd.dict_tile0;
+    const HybRun *rg = rs.runs;
+    uint4 *desc = b.tile_desc + 2 * (uint64_t)pd.dict_tile0;
+    for (uint32_t t = threadIdx.x; t < ntile; t += 64) {
+      const uint32_t v0 = t * kDictTile, v1 = min(min(v0 + kDictTile, nn), done);
+      uint32_t r0 = tf[t], r1 = t + 1 < ntile ? tf[t + 1] : nr - 1;
+      if (r1 >= nr) r1 = nr - 1;
+      const bool ok = nr > 0 && r0 < nr && v0 < v1;
+      uint32_t lo = 0, hi = 0;
+      if (ok) {
+        const HybRun f = rg[r0], l = rg[r1];
+        const uint64_t a = (f.info & 0x80000000u) ? (uint64_t)f.payload_off + (((uint64_t)(v0 - f.value_start) * bw) >> 3)
+                                                 : (uint64_t)f.payload_off;
+        uint64_t z = (l.info & 0x80000000u) && v1 > l.value_start
+                         ? (uint64_t)l.payload_off + (((uint64_t)(v1 - l.value_start) * bw + 7) >> 3)
+                         : (uint64_t)l.payload_off + 8;
+        z = min(z, (uint64_t)pd.val_len);
+        lo = (uint32_t)a;
+        hi = (uint32_t)z;
+      }
+      desc[2 * t] = make_uint4(r0, r1, lo, hi);
+      desc[2 * t + 1] = make_uint4(done, ok ? 1u : 0u, 0u, 0u);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

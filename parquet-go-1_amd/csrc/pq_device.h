@@ -84,7 +84,7 @@ struct PageDesc {        // 104 B
   uint32_t delta_mbvc;   // DELTA: values per miniblock
   uint32_t ba_delta;     // VK_DLBA / VK_DBA: index of the page's BaDelta entry
   uint32_t ba_tile;      // byte-array chunks: global index of the page's first BA tile (kBaTile values)
-  uint32_t pad1;
+  uint32_t dict_tile0;   // VK_DICT / VK_RLE_BOOL with a run scan: the page's first entry of the tile tables
 };
 
 struct ChunkDesc {       // 192 B
