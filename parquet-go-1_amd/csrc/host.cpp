@@ -512,6 +512,16 @@ struct pqgpu_batch {
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr, ev_delta_join = nullptr;
   hipEvent_t ev_levels = nullptr, ev_nest_join = nullptr;
+  // Column-group pipeline (speculative batches of flat REQUIRED columns with device SNAPPY pages):
+  // the chunks are cut into n_groups contiguous groups; group g's SNAPPY launch is followed on the
+  // values streams by its run scan, dictionary tiles and DELTA pages while group g+1 decompresses.
+  // Per group: [first, end) of the SNAPPY jobs, the scan pages, the work items, and the number of
+  // work items of k_values_delta's launch at the group's start.
+  static constexpr int kMaxGroups = 8;
+  uint32_t n_groups = 0;
+  uint32_t grp_job[kMaxGroups + 1] = {}, grp_scan[kMaxGroups + 1] = {}, grp_item[kMaxGroups + 1] = {},
+           grp_delta[kMaxGroups] = {};
+  hipEvent_t ev_snap[kMaxGroups] = {};
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
   uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
@@ -1433,8 +1443,24 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     const bool copy = k == WI_PLAIN || k == WI_BOOL;
     return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 4) : 3;
   };
-  std::stable_sort(b->items.begin(), b->items.end(),
-                   [&](const WorkItem &x, const WorkItem &y) { return rank(x.kind) < rank(y.kind); });
+  // column-group pipeline: only for speculative batches whose pages are all flat REQUIRED (no level
+  // streams, no byte-array or nested outputs) with device SNAPPY pages, copies fused, no DELTA tiles
+  b->n_groups = 0;
+  {
+    const char *ge = getenv("PQ_SNAPPY_GROUPS");
+    const int want = ge ? atoi(ge) : 1;  // (default: off until measured)
+    bool ok = b->spec && want > 1 && !b->snappy.empty() && fused && b->level_pages.empty() &&
+              b->level_pages_bw1.empty() && b->ba_chunks.empty() && nc >= 2;
+    for (const auto &hc : b->chunks) ok = ok && hc.col.max_rep == 0 && hc.col.max_def == 0 && !hc.nest;
+    for (const auto &it : b->items) ok = ok && it.kind != WI_DELTA_TILE && it.kind != WI_DLENS;
+    if (ok) b->n_groups = (uint32_t)std::min<int>(std::min<int>(want, pqgpu_batch::kMaxGroups), (int)nc);
+  }
+  const uint32_t G = b->n_groups;
+  auto grp = [&](uint32_t page) { return G ? b->pages[page].chunk * G / nc : 0u; };
+  std::stable_sort(b->items.begin(), b->items.end(), [&](const WorkItem &x, const WorkItem &y) {
+    const uint32_t gx = grp(x.page), gy = grp(y.page);
+    return gx != gy ? gx < gy : rank(x.kind) < rank(y.kind);
+  });
   b->n_delta_items = 0;
   b->n_delta_tiles = 0;
   b->n_copy_items = 0;
@@ -1442,6 +1468,22 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->n_delta_items += rank(it.kind) <= 2;  // k_values_delta's launch
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
     b->n_copy_items += rank(it.kind) == 4;
+  }
+  if (G) {
+    for (uint32_t g = 0; g <= G; g++) b->grp_job[g] = b->grp_scan[g] = b->grp_item[g] = 0;
+    for (uint32_t g = 0; g < G; g++) b->grp_delta[g] = 0;
+    // jobs, scan pages and items are in chunk order: group g's ranges are contiguous
+    for (uint32_t j = 0; j < (uint32_t)b->snappy.size(); j++) b->grp_job[b->pages[b->snappy[j].page].chunk * G / nc + 1]++;
+    for (uint32_t p : b->scan_pages) b->grp_scan[grp(p) + 1]++;
+    for (auto &it : b->items) {
+      b->grp_item[grp(it.page) + 1]++;
+      b->grp_delta[grp(it.page)] += rank(it.kind) <= 2;
+    }
+    for (uint32_t g = 0; g < G; g++) {
+      b->grp_job[g + 1] += b->grp_job[g];
+      b->grp_scan[g + 1] += b->grp_scan[g];
+      b->grp_item[g + 1] += b->grp_item[g];
+    }
   }
   // batch-level arrays
   b->o_pages = take((uint64_t)np * sizeof(PageDesc));
@@ -1826,12 +1868,25 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
   const PbaLists pl = pba_lists(b);
-  // SNAPPY pages first: every later kernel reads page data
-  if (!b->snappy.empty())
+  // SNAPPY pages first: every later kernel reads page data (column-group pipeline: one launch per
+  // group, each followed by an event the group's values work waits for)
+  const uint32_t G = b->n_groups;
+  if (G) {
+    for (uint32_t g = 0; g < G; g++) {
+      if (!b->ev_snap[g]) HIPCHECK(hipEventCreateWithFlags(&b->ev_snap[g], hipEventDisableTiming), err);
+      const uint32_t j0 = b->grp_job[g], j1 = b->grp_job[g + 1];
+      HIPCHECK(timed(b, 11, s, j1 - j0, [&] {
+                 return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy) + j0, j1 - j0, s);
+               }),
+               err);
+      HIPCHECK(hipEventRecord(b->ev_snap[g], s), err);
+    }
+  } else if (!b->snappy.empty()) {
     HIPCHECK(timed(b, 11, s, b->snappy.size(), [&] {
                return launch_snappy(d, (const SnappyJob *)(A + b->o_snappy), (uint32_t)b->snappy.size(), s);
              }),
              err);
+  }
   // DELTA work items and the other value work items go out as two launches (separately profiled).
   LaunchLists l1 = l, l2 = l;
   l1.n_items = b->n_delta_items;
@@ -1880,7 +1935,34 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (e == hipSuccess) e = hipEventRecord(b->ev_copy_join, cs);
     return e;
   };
-  if (b->spec) {
+  if (G) {
+    // Column-group pipeline: group g's run scan and dictionary tiles (side stream) and its DELTA
+    // pages and fused copies (DELTA stream) start when group g's SNAPPY launch is done, beside the
+    // decompression of the later groups on the batch stream.
+    hipStream_t v = b->ctx->side;
+    if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
+    for (uint32_t g = 0; g < G; g++) {
+      LaunchLists lg = l;
+      lg.scan_pages = l.scan_pages + b->grp_scan[g];
+      lg.n_scan_pages = b->grp_scan[g + 1] - b->grp_scan[g];
+      const WorkItem *it0 = l.items + b->grp_item[g];
+      const uint32_t nd = b->grp_delta[g], ni = b->grp_item[g + 1] - b->grp_item[g];
+      lg.items = it0 + nd;
+      lg.n_items = ni - nd;
+      HIPCHECK(hipStreamWaitEvent(v, b->ev_snap[g], 0), err);
+      HIPCHECK(timed(b, 2, v, lg.n_scan_pages, [&] { return launch_scan_runs(d, lg, v); }), err);
+      HIPCHECK(timed(b, 9, v, lg.n_items, [&] { return launch_values(d, lg, v); }), err);
+      if (nd) {
+        HIPCHECK(hipStreamWaitEvent(ds, b->ev_snap[g], 0), err);
+        HIPCHECK(timed(b, 1, ds, nd, [&] { return launch_values_delta(d, it0, nd, ds); }), err);
+      }
+    }
+    HIPCHECK(hipEventRecord(b->ev_join, v), err);
+    HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
+    HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
+  } else if (b->spec) {
     // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
     // side stream concurrently with the level decode; k_bases then checks the header counts
     // the values path used against the decoded ones (sync_impl re-runs serially on a miss).
@@ -2357,6 +2439,8 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   if (b->ev_copy_join) (void)hipEventDestroy(b->ev_copy_join);
   if (b->ev_delta_join) (void)hipEventDestroy(b->ev_delta_join);
   if (b->ev_levels) (void)hipEventDestroy(b->ev_levels);
+  for (auto &e : b->ev_snap)
+    if (e) (void)hipEventDestroy(e);
   if (b->ev_nest_join) (void)hipEventDestroy(b->ev_nest_join);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);

@@ -452,3 +452,17 @@ def test_gpu_direct_switch(gpu_ctx, monkeypatch):
     monkeypatch.setenv("PQ_SNAPPY_DIRECT", "0")
     b = _gpu(gpu_ctx, data)[0]
     assert np.asarray(a.values_raw).tobytes() == np.asarray(b.values_raw).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("groups", ["1", "2", "3", "8"])
+def test_gpu_column_groups(gpu_ctx, monkeypatch, groups):
+    """The column-group pipeline (host.cpp n_groups: group g's run scan, dictionary tiles and DELTA
+    pages start when group g's SNAPPY launch is done) on the 64-column cfg5 replica, with 1 (off) to 8
+    groups: every chunk equals the oracle."""
+    import test_gpu_parity as P
+    monkeypatch.setenv("PQ_SNAPPY_GROUPS", groups)
+    data = pqtest.load("cfg5_small")
+    gpu = P._gpu_decode(gpu_ctx, data)
+    for rg, col, r in pqtest.oracle_decode(data):
+        pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"groups {groups} rg{rg} col{col}")
