@@ -1431,10 +1431,21 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
   // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
+  // column-group pipeline: only for batches whose pages are all flat REQUIRED (no level streams,
+  // no byte-array or nested outputs: every value base is known at upload, k_bases can run before
+  // the first SNAPPY launch) with device SNAPPY pages and no DELTA tiles; its copies are fused
+  const char *cf = getenv("PQ_COPY_FUSED");
+  b->n_groups = 0;
   {
-    const char *cf = getenv("PQ_COPY_FUSED");
-    b->copy_fused = cf ? atoi(cf) != 0 : b->spec;
+    const char *ge = getenv("PQ_SNAPPY_GROUPS");
+    const int want = ge ? atoi(ge) : 1;  // (default: off until measured)
+    bool ok = want > 1 && !b->snappy.empty() && (!cf || atoi(cf) != 0) && b->level_pages.empty() &&
+              b->level_pages_bw1.empty() && b->ba_chunks.empty() && nc >= 2;
+    for (const auto &hc : b->chunks) ok = ok && hc.col.max_rep == 0 && hc.col.max_def == 0 && !hc.nest;
+    for (const auto &it : b->items) ok = ok && it.kind != WI_DELTA_TILE && it.kind != WI_DLENS;
+    if (ok) b->n_groups = (uint32_t)std::min<int>(std::min<int>(want, pqgpu_batch::kMaxGroups), (int)nc);
   }
+  b->copy_fused = cf ? atoi(cf) != 0 : (b->spec || b->n_groups > 0);
   const bool fused = b->copy_fused;
   // ranks: DELTA tiles, DELTA pages, fused PLAIN / BOOLEAN copies (these three are k_values_delta's
   // launch: latency-bound pages first, the bandwidth-bound copies fill the CUs around them), the
@@ -1443,18 +1454,6 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     const bool copy = k == WI_PLAIN || k == WI_BOOL;
     return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 4) : 3;
   };
-  // column-group pipeline: only for speculative batches whose pages are all flat REQUIRED (no level
-  // streams, no byte-array or nested outputs) with device SNAPPY pages, copies fused, no DELTA tiles
-  b->n_groups = 0;
-  {
-    const char *ge = getenv("PQ_SNAPPY_GROUPS");
-    const int want = ge ? atoi(ge) : 1;  // (default: off until measured)
-    bool ok = b->spec && want > 1 && !b->snappy.empty() && fused && b->level_pages.empty() &&
-              b->level_pages_bw1.empty() && b->ba_chunks.empty() && nc >= 2;
-    for (const auto &hc : b->chunks) ok = ok && hc.col.max_rep == 0 && hc.col.max_def == 0 && !hc.nest;
-    for (const auto &it : b->items) ok = ok && it.kind != WI_DELTA_TILE && it.kind != WI_DLENS;
-    if (ok) b->n_groups = (uint32_t)std::min<int>(std::min<int>(want, pqgpu_batch::kMaxGroups), (int)nc);
-  }
   const uint32_t G = b->n_groups;
   auto grp = [&](uint32_t page) { return G ? b->pages[page].chunk * G / nc : 0u; };
   std::stable_sort(b->items.begin(), b->items.end(), [&](const WorkItem &x, const WorkItem &y) {
@@ -1872,6 +1871,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // group, each followed by an event the group's values work waits for)
   const uint32_t G = b->n_groups;
   if (G) {
+    // flat REQUIRED pages only: k_bases needs no page data, and every group's values follow it
+    HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     for (uint32_t g = 0; g < G; g++) {
       if (!b->ev_snap[g]) HIPCHECK(hipEventCreateWithFlags(&b->ev_snap[g], hipEventDisableTiming), err);
       const uint32_t j0 = b->grp_job[g], j1 = b->grp_job[g + 1];
@@ -1959,7 +1960,6 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
     HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
-    HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else if (b->spec) {

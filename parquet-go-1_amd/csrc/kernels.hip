@@ -3322,7 +3322,10 @@ DEV void snappy_put(SnappyOut &o, const uint8_t *S, uint32_t P, uint32_t len) {
 // kSnappyRing bytes also land in the ring, which must hold the most recent output for later
 // copies), the tail goes through the ring again. Long literals dominate incompressible pages
 // (one literal per 64 KiB encoder fragment).
-constexpr uint32_t kSnappyWaves = 2;
+#ifndef PQ_SNAPPY_WAVES
+#define PQ_SNAPPY_WAVES 2
+#endif
+constexpr uint32_t kSnappyWaves = PQ_SNAPPY_WAVES;
 constexpr uint32_t kSnappyDirect = 2048;  // bytes: shorter literals stay on the ring path
 struct SnappyCmd {                         // LDS: wave 0 -> helper waves
   uint64_t src;                            // literal body source (global address)

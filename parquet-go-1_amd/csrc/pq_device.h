@@ -199,7 +199,10 @@ struct SnappyJob {       // 48 B
                          // without the 64-B pad; no k_values item copies it again (the
                          // decompressed body IS the output, page_v1.go:87-122, type_*.go PLAIN)
 };
-constexpr uint32_t kSnappyRing = 16384;  // LDS window of the most recent output bytes per page
+#ifndef PQ_SNAPPY_RING
+#define PQ_SNAPPY_RING 16384
+#endif
+constexpr uint32_t kSnappyRing = PQ_SNAPPY_RING;  // LDS window of the most recent output bytes per page
 enum : uint32_t { ST_DECOMP = 4 };       // err_key stage of a device decompression error
 
 // On-device page index (pagewalk.hip): readPages' header loop

@@ -460,9 +460,22 @@ def test_gpu_column_groups(gpu_ctx, monkeypatch, groups):
     """The column-group pipeline (host.cpp n_groups: group g's run scan, dictionary tiles and DELTA
     pages start when group g's SNAPPY launch is done) on the 64-column cfg5 replica, with 1 (off) to 8
     groups: every chunk equals the oracle."""
-    import test_gpu_parity as P
+    import pqgpu
     monkeypatch.setenv("PQ_SNAPPY_GROUPS", groups)
     data = pqtest.load("cfg5_small")
-    gpu = P._gpu_decode(gpu_ctx, data)
+    f = pqgpu.File(data)
+    gpu = {}
+    for rg in range(f.num_row_groups):  # one batch per row group: each batch is cut into groups
+        b = pqgpu.Batch(gpu_ctx)
+        b.kernel_timing(True)
+        ids = {col: b.add_file_chunk(f, rg, col)[0] for col in range(f.num_columns)}
+        b.decode()
+        b.sync()
+        # the pipeline really ran: one SNAPPY launch per group
+        assert b.kernel_times()["k_snappy"][1] == min(int(groups), f.num_columns), b.kernel_times()
+        for col, cid in ids.items():
+            e = b.status(cid)
+            gpu[(rg, col)] = e if e is not None else b.result(cid)
+        b.close()
     for rg, col, r in pqtest.oracle_decode(data):
         pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"groups {groups} rg{rg} col{col}")
