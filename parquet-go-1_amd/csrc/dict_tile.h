@@ -14,13 +14,21 @@
 
 namespace pq {
 
-constexpr uint32_t kTileRuns = 1024;      // runs held in LDS (a tile with more reads the run table)
-constexpr uint32_t kTileStageB = 16896;   // staged stream bytes (a wider tile reads global memory)
-
-struct DictTileLDS {
-  HybRun runs[kTileRuns];
+#ifndef PQ_DICT_RUNS
+#define PQ_DICT_RUNS 256
+#endif
+#ifndef PQ_DICT_WPE
+#define PQ_DICT_WPE 8
+#endif
+constexpr uint32_t kTileRuns = 1024;          // runs held in LDS (a tile with more reads the run table)
+constexpr uint32_t kDictRuns = PQ_DICT_RUNS;  // the same for k_values_dict (smaller: 8 workgroups per CU)
+constexpr uint32_t kTileStageB = 16896;       // staged stream bytes (a wider tile reads global memory)
+template <uint32_t NR>
+struct DictTileLDST {
+  HybRun runs[NR];
   uint32_t stage[kTileStageB / 4 + 8];
 };
+using DictTileLDS = DictTileLDST<kTileRuns>;
 
 struct DictTile {
   const uint8_t *s;      // value stream (after the bit-width byte)
@@ -67,17 +75,18 @@ DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   return true;
 }
 
-// Load tile [v0, v1) of page `page`: dict_tile_open, then the runs (up to kTileRuns) and the
+// Load tile [v0, v1) of page `page`: dict_tile_open, then the runs (up to NR) and the
 // stream bytes of the tile's bit-packed values are staged in LDS. Every thread of the workgroup
 // calls it; it ends with a barrier unless it returns false or the bit width is 0 (both
 // workgroup-uniform).
+template <uint32_t NR>
 DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
-                        DictTileLDS &L, DictTile &t) {
+                        DictTileLDST<NR> &L, DictTile &t) {
   uint32_t r0 = 0, r1 = 0;
   if (!dict_tile_open(b, pd, page, v0, v1, nn, t, r0, r1)) return false;
   if (t.bw == 0) return true;
   const HybRun *rg = t.runs;
-  if (t.nr <= kTileRuns) {
+  if (t.nr <= NR) {
     for (uint32_t k = threadIdx.x; k < t.nr; k += blockDim.x) L.runs[k] = rg[k];
     t.runs = L.runs;
   }
@@ -125,7 +134,8 @@ DEV uint32_t dict_tile_seek(const DictTile &t, uint32_t v) {
 
 // Index of value v (v inside [t.v0, t.v1)); `ri` is the lane's run cursor (values visited by a
 // lane must not decrease).
-DEV uint32_t dict_tile_value(const DictTile &t, const DictTileLDS &L, uint32_t &ri, uint32_t v) {
+template <class L_>
+DEV uint32_t dict_tile_value(const DictTile &t, const L_ &L, uint32_t &ri, uint32_t v) {
   if (t.bw == 0) return 0;
   while (ri + 1 < t.nr && t.runs[ri + 1].value_start <= v) ri++;
   const HybRun r = t.runs[ri];

@@ -381,7 +381,7 @@ struct KernelTimer {
 };
 static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
-    "k_ba_emit", "k_records", "k_values[other]", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
+    "k_ba_emit", "k_records", "k_values_dict", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
     "k_values_copy"};
 
@@ -507,6 +507,7 @@ struct pqgpu_batch {
   // PQ_COPY_FUSED=0/1 forces either (set per plan).
   bool copy_fused = false;
   uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
+  uint32_t n_dict_items = 0;      // the WI_DICT items, after the n_delta_items: k_values_dict
   // PQ_COPY_MODE (speculative schedule): where k_values_copy waits — 0 from the start beside
   // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
@@ -520,7 +521,7 @@ struct pqgpu_batch {
   static constexpr int kMaxGroups = 8;
   uint32_t n_groups = 0;
   uint32_t grp_job[kMaxGroups + 1] = {}, grp_scan[kMaxGroups + 1] = {}, grp_item[kMaxGroups + 1] = {},
-           grp_delta[kMaxGroups] = {};
+           grp_delta[kMaxGroups] = {}, grp_dict[kMaxGroups] = {};
   hipEvent_t ev_snap[kMaxGroups] = {};
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
@@ -1449,10 +1450,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   const bool fused = b->copy_fused;
   // ranks: DELTA tiles, DELTA pages, fused PLAIN / BOOLEAN copies (these three are k_values_delta's
   // launch: latency-bound pages first, the bandwidth-bound copies fill the CUs around them), the
-  // LDS-staged kinds (k_values), unfused copies (k_values_copy)
+  // dictionary tiles (k_values_dict), the other LDS-staged kinds (k_values), unfused copies
+  // (k_values_copy)
   auto rank = [fused](uint8_t k) {
     const bool copy = k == WI_PLAIN || k == WI_BOOL;
-    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 4) : 3;
+    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 5) : k == WI_DICT ? 3 : 4;
   };
   const uint32_t G = b->n_groups;
   auto grp = [&](uint32_t page) { return G ? b->pages[page].chunk * G / nc : 0u; };
@@ -1461,22 +1463,25 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     return gx != gy ? gx < gy : rank(x.kind) < rank(y.kind);
   });
   b->n_delta_items = 0;
+  b->n_dict_items = 0;
   b->n_delta_tiles = 0;
   b->n_copy_items = 0;
   for (auto &it : b->items) {
     b->n_delta_items += rank(it.kind) <= 2;  // k_values_delta's launch
+    b->n_dict_items += rank(it.kind) == 3;   // k_values_dict's launch
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
-    b->n_copy_items += rank(it.kind) == 4;
+    b->n_copy_items += rank(it.kind) == 5;
   }
   if (G) {
     for (uint32_t g = 0; g <= G; g++) b->grp_job[g] = b->grp_scan[g] = b->grp_item[g] = 0;
-    for (uint32_t g = 0; g < G; g++) b->grp_delta[g] = 0;
+    for (uint32_t g = 0; g < G; g++) b->grp_delta[g] = b->grp_dict[g] = 0;
     // jobs, scan pages and items are in chunk order: group g's ranges are contiguous
     for (uint32_t j = 0; j < (uint32_t)b->snappy.size(); j++) b->grp_job[b->pages[b->snappy[j].page].chunk * G / nc + 1]++;
     for (uint32_t p : b->scan_pages) b->grp_scan[grp(p) + 1]++;
     for (auto &it : b->items) {
       b->grp_item[grp(it.page) + 1]++;
       b->grp_delta[grp(it.page)] += rank(it.kind) <= 2;
+      b->grp_dict[grp(it.page)] += rank(it.kind) == 3;
     }
     for (uint32_t g = 0; g < G; g++) {
       b->grp_job[g + 1] += b->grp_job[g];
@@ -1891,8 +1896,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // DELTA work items and the other value work items go out as two launches (separately profiled).
   LaunchLists l1 = l, l2 = l;
   l1.n_items = b->n_delta_items;
-  l2.items = l.items + b->n_delta_items;
-  l2.n_items = l.n_items - b->n_delta_items;
+  const WorkItem *dict_items = l.items + b->n_delta_items;
+  const uint32_t n_dict = b->n_dict_items;
+  l2.items = dict_items + n_dict;
+  l2.n_items = l.n_items - b->n_delta_items - n_dict;
   // DELTA_BINARY_PACKED items (the first n_delta_items) go to k_values_delta on the DELTA stream,
   // beside the level kernels, the copies and the other values kinds; the default stream joins it
   hipStream_t ds = b->ctx->delta;
@@ -1947,11 +1954,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       lg.scan_pages = l.scan_pages + b->grp_scan[g];
       lg.n_scan_pages = b->grp_scan[g + 1] - b->grp_scan[g];
       const WorkItem *it0 = l.items + b->grp_item[g];
-      const uint32_t nd = b->grp_delta[g], ni = b->grp_item[g + 1] - b->grp_item[g];
-      lg.items = it0 + nd;
-      lg.n_items = ni - nd;
+      const uint32_t nd = b->grp_delta[g], nk = b->grp_dict[g], ni = b->grp_item[g + 1] - b->grp_item[g];
+      lg.items = it0 + nd + nk;
+      lg.n_items = ni - nd - nk;
       HIPCHECK(hipStreamWaitEvent(v, b->ev_snap[g], 0), err);
       HIPCHECK(timed(b, 2, v, lg.n_scan_pages, [&] { return launch_scan_runs(d, lg, v); }), err);
+      HIPCHECK(timed(b, 8, v, nk, [&] { return launch_values_dict(d, it0 + nd, nk, v); }), err);
       HIPCHECK(timed(b, 9, v, lg.n_items, [&] { return launch_values(d, lg, v); }), err);
       if (nd) {
         HIPCHECK(hipStreamWaitEvent(ds, b->ev_snap[g], 0), err);
@@ -1985,6 +1993,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
     if (b->copy_mode == 6)  // the copies first on the side stream, then the LDS kinds
       HIPCHECK(timed(b, 20, v, l.n_copy_items, [&] { return launch_values_copy(d, l, v); }), err);
+    HIPCHECK(timed(b, 8, v, n_dict, [&] { return launch_values_dict(d, dict_items, n_dict, v); }), err);
     HIPCHECK(timed(b, 9, v, l2.n_items, [&] { return launch_values(d, l2, v); }), err);
     if (b->copy_mode == 1) HIPCHECK(fork_copies(v), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
@@ -2017,6 +2026,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     HIPCHECK(fork_nest(), err);  // on the DELTA stream after its pages
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
+    HIPCHECK(timed(b, 8, s, n_dict, [&] { return launch_values_dict(d, dict_items, n_dict, s); }), err);
     HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
@@ -2133,7 +2143,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->page_nn_out = nn;
   int first = PQ_OK;
   int64_t out_bytes = 0, slots = 0, values = 0, lvl_bytes = 0, val_bytes = 0, dl_bytes = 0, snappy_direct_bytes = 0,
-          cp_bytes = 0;
+          cp_bytes = 0, dict_bytes = 0;
   int64_t kb[PQGPU_TIMER_SLOTS] = {0};  // algorithmic bytes per launch slot
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -2194,6 +2204,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
             !((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values))
           cp_bytes += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_PLAIN_BOOL ? 1 : w);  // the copies' launch
         if (pd.vkind == VK_DICT || pd.vkind == VK_RLE_BOOL) kb[2] += pd.val_len;  // k_scan_runs: index streams
+        if ((pd.vkind == VK_DICT && w > 0) || pd.vkind == VK_RLE_BOOL)
+          dict_bytes += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_RLE_BOOL ? 1 : w);  // k_values_dict
         if (w == 0 && pd.vkind == VK_DICT) {
           if (hc.ba_sync || b->ba_presum) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices
           kb[6] += pd.val_len;
@@ -2249,8 +2261,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   kb[20] = b->copy_fused ? 0 : cp_bytes;            // k_values_copy
   kb[1] = dl_bytes + (b->copy_fused ? cp_bytes : 0);  // k_values_delta: DELTA pages (+ the fused copies)
   val_bytes -= snappy_direct_bytes;
-  kb[9] = val_bytes - cp_bytes - dl_bytes;  // k_values: the LDS kinds other than DELTA (dictionary tiles, ...)
-  kb[8] = val_bytes - dl_bytes;
+  kb[8] = dict_bytes;                                   // k_values_dict: dictionary tiles
+  kb[9] = val_bytes - cp_bytes - dl_bytes - dict_bytes;  // k_values: the other LDS kinds
   kb[11] = b->stats.snappy_kernel_bytes;
   memcpy(b->slot_bytes, kb, sizeof(kb));
   b->stats.levels_kernel_bytes = lvl_bytes;

@@ -1865,7 +1865,7 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 // [w * 1024, (w + 1) * 1024) of the tile in 16 rounds of 64 consecutive values, so every
 // store instruction writes 64 consecutive outputs (256 B for 4-byte values).
 DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
-                 DictTileLDS &lds) {
+                 DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
   if (wi.v0 >= v1) return;
   DictTile t;
@@ -2562,7 +2562,6 @@ struct DeltaPageLDS {
 };
 
 union ValuesLDS {
-  DictTileLDS dict;
   DeltaTileLDS dtile;        // WI_DELTA_TILE
   DeltaPageLDS dpage;        // WI_DELTA_PAGE
 
@@ -3026,7 +3025,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
   switch (wi.kind) {
     case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;  // (only when PQ_COPY_FUSED=1 puts them here)
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
-    case WI_DICT: do_dict(b, wi, pd, cd, nn, lds.dict); break;
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
@@ -3050,6 +3048,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
       break;
     }
   }
+}
+
+// Dictionary tiles (WI_DICT) in a launch of their own: the registers and LDS are do_dict's alone
+// (not the maximum over every work-item kind), so more tiles are resident per CU.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DICT_WPE))) k_values_dict(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
+  __shared__ DictTileLDST<kDictRuns> lds;
+  const WorkItem wi = items[blockIdx.x];
+  const PageDesc &pd = b.pages[wi.page];
+  do_dict(b, wi, pd, b.chunks[pd.chunk], b.page_nn_v[wi.page], lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -3715,6 +3723,11 @@ hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_items) return hipSuccess;
   hipLaunchKernelGGL(k_values, dim3(l.n_items), dim3(256), 0, s, b, l.items);
+  return hipGetLastError();
+}
+hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_values_dict, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();
 }
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {

@@ -61,6 +61,17 @@ def index_pages(bw, rng):
     # 5. payload bytes equal to the run header everywhere (index 127 at bw 8: 0x7f)
     r5 = b"".join(lit(np.full(504, 127 if bw == 8 else 0x7f7f), bw) for _ in range(30))
     pages.append((30 * 504, r5))
+    # 6. short runs: RLE runs of 1-3 values and 1-group literal runs, > 256 runs per 4096-value
+    # tile (k_values_dict keeps 256 runs in LDS and reads a longer tile's runs from global memory)
+    r6, n6 = b"", 0
+    for k in range(4000):
+        if k % 5 == 4:
+            r6 += lit(rng.integers(0, hi, 8), bw)
+            n6 += 8
+        else:
+            r6 += rle(1 + k % 3, (k * 7) % hi, bw)
+            n6 += 1 + k % 3
+    pages.append((n6, r6))
     return pages
 
 
