@@ -1389,9 +1389,24 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) slot_only &= b->pages[p].vkind == VK_DICT;
       cls[c] = slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
     }
+    // A class with fewer than 8 chunks would leave XCDs idle: chunk k of the class (in chunk order)
+    // then gets 8 / n queues and its tiles go round-robin over them, still in block order (tile j
+    // of the chunk at a lower block index than tile j + 1), so the look-back is unchanged.
+    uint32_t ncls[3] = {0, 0, 0};
+    std::vector<uint32_t> qbase(nc, 0), qn(nc, 1), seen(nc, 0);
+    for (uint32_t c : b->ba_chunks) qbase[c] = ncls[cls[c]]++;
+    for (uint32_t c : b->ba_chunks) {
+      const uint32_t n = ncls[cls[c]];
+      if (n < 8) {
+        qn[c] = 8 / n;
+        qbase[c] = qbase[c] * qn[c];
+      } else {
+        qbase[c] = c % 8;
+      }
+    }
     for (uint32_t t = 0; t < (uint32_t)b->ba_tile_page.size(); t++) {
       const uint32_t c = b->pages[b->ba_tile_page[t]].chunk;
-      q[8 * cls[c] + c % 8].push_back(t);
+      q[8 * cls[c] + qbase[c] + seen[c]++ % qn[c]].push_back(t);
     }
     for (uint32_t k = 0; k < 3; k++) {
       size_t m = 0;
