@@ -2999,7 +2999,10 @@ union DeltaLDS {
   DeltaTileLDS dtile;
   DeltaPageLDS dpage;
 };
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_values_delta(BatchDev b_in, const WorkItem *items) {
+#ifndef PQ_DELTA_WPE
+#define PQ_DELTA_WPE 5
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DELTA_WPE))) k_values_delta(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
   __shared__ DeltaLDS lds;
   const WorkItem wi = items[blockIdx.x];
