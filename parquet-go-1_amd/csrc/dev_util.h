@@ -266,6 +266,54 @@ DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, 
   if (tid < tail) dst[head + body + tid] = sp[body + tid];
 }
 
+// The same with U pieces per lane in flight and one load per piece. Per round the workgroup takes
+// nt * U consecutive pieces, wave w the 64 * U of them from w * 64 * U, lane l piece u * 64 + l of
+// those (so every store instruction writes 1 KiB contiguous). A lane's second source block is the
+// next piece: lane l + 1's block (lane 63: lane 0's next block) by one lane shuffle, and only lane
+// 63's last piece loads its own.
+template <uint32_t U>
+DEV void copy_bytes_u(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
+  if (n == 0) return;
+  uintptr_t da = (uintptr_t)dst;
+  uint64_t head = (16 - (da & 15)) & 15;
+  if (head > n) head = n;
+  if (tid < head) dst[tid] = src[tid];
+  const uint64_t body = (n - head) & ~(uint64_t)15;
+  uint4 *d = (uint4 *)(dst + head);
+  const uint8_t *sp = src + head;
+  const uint32_t sa = (uint32_t)((uintptr_t)sp & 15);
+  const uint4 *sb = (const uint4 *)(sp - sa);
+  const uint64_t pieces = body >> 4;
+  const uint32_t lane = tid & 63u, wv = tid >> 6;
+  const int nxt = (int)(((lane + 1) & 63u) * 4);
+  auto shd = [nxt](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)v); };
+  uint64_t r0 = 0;
+  const uint64_t per = (uint64_t)nt * U;
+  for (; r0 + per <= pieces; r0 += per) {
+    const uint64_t i = r0 + (uint64_t)wv * 64 * U + lane;
+    uint4 a[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) a[u] = sb[i + 64 * u];
+    if (sa) {
+      uint4 e = make_uint4(0u, 0u, 0u, 0u);
+      if (lane == 63) e = sb[i + 64 * (U - 1) + 1];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        const uint4 o = (lane == 0 && u + 1 < U) ? a[u + 1] : a[u];  // what lane l - 1 takes from this lane
+        uint4 b = make_uint4(shd(o.x), shd(o.y), shd(o.z), shd(o.w));
+        if (lane == 63 && u + 1 == U) b = e;
+        d[i + 64 * u] = funnel16(a[u], b, sa);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) d[i + 64 * u] = a[u];
+    }
+  }
+  for (uint64_t i = r0 + tid; i < pieces; i += nt) d[i] = sa ? funnel16(sb[i], sb[i + 1], sa) : sb[i];
+  const uint64_t tail = n - head - body;
+  if (tid < tail) dst[head + body + tid] = sp[body + tid];
+}
+
 // Workgroup exclusive scan of one 64-bit value per thread (blockDim.x a multiple of 64;
 // wsum: LDS scratch of blockDim.x / 64 entries). *total = the workgroup sum.
 DEV uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, uint64_t *total) {

@@ -1832,6 +1832,11 @@ DEV uint32_t plain_err(uint64_t have, uint32_t w) { return (have % w) == 0 ? PQ_
 
 
 // PLAIN fixed width (INT32/INT64/FLOAT/DOUBLE/INT96/FLBA): byte copy.
+#ifndef PQ_FUSED_COPY_U
+#define PQ_FUSED_COPY_U 4
+#endif
+// U: pieces per lane in flight (copy_bytes_u); 0: copy_bytes
+template <uint32_t U = 0>
 DEV void do_plain(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
   const uint32_t w = (uint32_t)cd.value_width;
   uint32_t v1 = min(wi.v1, nn);
@@ -1843,7 +1848,8 @@ DEV void do_plain(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   if (e1 <= wi.v0) return;
   const uint8_t *src = gp_u64<const uint8_t>(pd.data) + pd.val_off + (uint64_t)wi.v0 * w;
   uint8_t *dst = gp_u64<uint8_t>(cd.values) + (b.page_vbase[wi.page] + wi.v0) * w;
-  copy_bytes(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
+  if constexpr (U == 0) copy_bytes(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
+  else copy_bytes_u<U>(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
 }
 
 // BOOLEAN PLAIN (type_boolean.go:46-69): bit i of byte i/8, LSB first, one byte read per 8 values.
@@ -3013,7 +3019,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DEL
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
     case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
     case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
-    case WI_PLAIN: do_plain(b, wi, pd, cd, nn); break;  // fused copies (speculative schedule)
+    case WI_PLAIN: do_plain<PQ_FUSED_COPY_U>(b, wi, pd, cd, nn); break;  // fused copies (registers to spare: more in flight)
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
   }
 }
