@@ -229,11 +229,22 @@ __global__ void __launch_bounds__(256) k_ba_scan(BatchDev b_in, const uint32_t *
 // ---------------------------------------------------------------------------
 // k_ba_emit
 // ---------------------------------------------------------------------------
-struct EmitLDS {
-  DictTileLDS tile;
+template <uint32_t NR>
+struct EmitLDST {
+  DictTileLDST<NR> tile;
   uint4 wbuf[kEmitWaves][kWaveVec];
   uint64_t wtot[kEmitWaves];  // the waves' payload bytes
   uint64_t base;              // the tile's payload base
+};
+using EmitLDS = EmitLDST<kTileRuns>;
+// Class 3: a dictionary of at most kLdsSlots 16-B slots (entries of at most 12 bytes) is copied
+// into LDS per tile, so pass A's lengths and pass B's slot pieces are LDS reads instead of random
+// gathers through the texture path (cfg4's 1,024 map keys); 256 runs per tile in LDS keep three
+// workgroups per CU.
+constexpr uint32_t kLdsSlots = 1024;
+struct EmitLDSSlots {
+  EmitLDST<kDictRuns> e;
+  uint4 slots[kLdsSlots];
 };
 
 // The tile of block `blk` in class `cls` (~0u: padding of a shorter queue).
@@ -244,7 +255,8 @@ DEV uint32_t tile_of_block(const BatchDev &b, uint32_t cls, uint32_t blk) {
 // Payload bytes of tile t, computed by one wave without LDS (a look-back that found tile t
 // silent): the same sum tile t's own workgroup publishes (values the run scan did not validate,
 // and dictionary indices out of range, count 0).
-DEV uint64_t tile_aggregate(const BatchDev &b, uint32_t t, const DictTileLDS &unstaged) {
+template <class TL>
+DEV uint64_t tile_aggregate(const BatchDev &b, uint32_t t, const TL &unstaged) {
   const uint32_t p = b.ba_tile_page[t], lane = lane_id();
   const PageDesc &pd = b.pages[p];
   const ChunkDesc &cd = b.chunks[pd.chunk];
@@ -278,8 +290,9 @@ DEV uint64_t tile_aggregate(const BatchDev &b, uint32_t t, const DictTileLDS &un
 // wave reads kLbWin predecessors at a time (the nearest inclusive prefix is usually among
 // them); a predecessor still silent after kHelpSpins polls has its sum computed here, so the
 // wait is bounded whatever the dispatch order.
+template <class TL>
 DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32_t t, uint64_t agg,
-                      const DictTileLDS &lds, Stamps &sp) {
+                      const TL &lds, Stamps &sp) {
   uint64_t *st = b.ba_state;
   const uint32_t lane = lane_id(), j = t - cd.ba_tile0;
   if (j == 0) {
@@ -334,9 +347,10 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // slot table (any slot size: a value loads the 16-B pieces its entry occupies), else bytes are
 // read from their source (dictionaries without slots, PLAIN / DELTA pages). Pass B works in
 // groups of G rounds: the G rounds' loads are issued together.
-template <bool SLOT, uint32_t SV = SLOT ? 4 : 1>
+template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, class EL>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,
-                   uint32_t lo, uint32_t hi, bool is_dict, bool have, DictTile &tl, EmitLDS &L, Stamps &st) {
+                   uint32_t lo, uint32_t hi, bool is_dict, bool have, DictTile &tl, EL &L, Stamps &st,
+                   const uint4 *lslots = nullptr) {
   // SV: uint4 per slot (at most)
   constexpr uint32_t G = 2;              // rounds per load group
   const uint32_t s4 = cd.slot_shift - 4; // SLOT: uint4 per slot = 1 << s4
@@ -376,6 +390,8 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
     if (idx[r] != ~0u) {
       if (PQ_ABLATE(b, 11)) {  // diagnostic: no length loads
         len[r] = 16;
+      } else if (LS) {
+        len[r] = lslots[idx[r]].x;  // LDS copy of the slot table (16-B slots)
       } else if (SLOT) {
         len[r] = ((const uint32_t *)slots)[(uint64_t)idx[r] << (s4 + 2)];
       } else if (is_dict) {
@@ -447,7 +463,8 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         const uint32_t r = g * G + rr;
 #pragma unroll
         for (uint32_t q = 0; q < SV; q++)  // the slot pieces holding bytes of the entry (none: no value)
-          sl[rr][q] = len[r] && len[r] + 4 > 16 * q ? slots[((uint64_t)idx[r] << s4) + q] : make_uint4(0u, 0u, 0u, 0u);
+          sl[rr][q] = len[r] && len[r] + 4 > 16 * q ? (LS ? lslots[idx[r] + q] : slots[((uint64_t)idx[r] << s4) + q])
+                                                    : make_uint4(0u, 0u, 0u, 0u);
       }
     }
 #pragma unroll
@@ -509,9 +526,10 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
 }
 
 // Classes: chunks whose pages are all dictionary pages with a slot table of 16/32-byte (class 0)
-// or 64-byte slots (class 1), compiled without the source path; class 2: any page.
-template <uint32_t CLS>
-DEV void ba_emit(const BatchDev &b, EmitLDS &L) {
+// or 64-byte slots (class 1), compiled without the source path; class 2: any page; class 3: as
+// class 0 with 16-B slots and at most kLdsSlots entries, the slot table read from LDS.
+template <uint32_t CLS, class EL>
+DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   PQ_STAMPS(st, b.dbg);
   st.begin();
   const uint32_t t = tile_of_block(b, CLS, blockIdx.x);
@@ -532,7 +550,8 @@ DEV void ba_emit(const BatchDev &b, EmitLDS &L) {
     hi = tl.v1;
   }
   st.lap(0);
-  if (CLS == 0) emit_tile<true, 2>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
+  if (CLS == 3) emit_tile<true, 1, true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st, lslots);
+  else if (CLS == 0) emit_tile<true, 2>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else if (CLS == 1 || (is_dict && cd.slot_shift)) emit_tile<true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else emit_tile<false>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   st.count(7);
@@ -555,6 +574,17 @@ __global__ void __launch_bounds__(64 * kEmitWaves) k_ba_emit(BatchDev b_in) {
   __shared__ EmitLDS L;
   ba_emit<2>(b, L);
 }
+__global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(6))) k_ba_emit_lds(BatchDev b_in) {
+  const BatchDev b = global_view(b_in);
+  __shared__ EmitLDSSlots L;
+  const uint32_t t = tile_of_block(b, 3, blockIdx.x);
+  if (t == ~0u) return;  // queue padding (workgroup-uniform)
+  const ChunkDesc &cd = b.chunks[b.pages[b.ba_tile_page[t]].chunk];
+  const uint4 *gs = gp_u64<const uint4>(cd.dict_slots);
+  for (uint32_t k = threadIdx.x; k < cd.dict_count; k += blockDim.x) L.slots[k] = gs[k];
+  wg_barrier();
+  ba_emit<3>(b, L.e, L.slots);
+}
 
 hipError_t launch_dict_slots(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_slot_chunks) return hipSuccess;
@@ -576,6 +606,7 @@ hipError_t launch_ba_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s
   if (l.n_ba_class[0]) hipLaunchKernelGGL(k_ba_emit_slots, dim3(l.n_ba_class[0]), dim3(64 * kEmitWaves), 0, s, b);
   if (l.n_ba_class[1]) hipLaunchKernelGGL(k_ba_emit_slots64, dim3(l.n_ba_class[1]), dim3(64 * kEmitWaves), 0, s, b);
   if (l.n_ba_class[2]) hipLaunchKernelGGL(k_ba_emit, dim3(l.n_ba_class[2]), dim3(64 * kEmitWaves), 0, s, b);
+  if (l.n_ba_class[3]) hipLaunchKernelGGL(k_ba_emit_lds, dim3(l.n_ba_class[3]), dim3(64 * kEmitWaves), 0, s, b);
   return hipGetLastError();
 }
 

@@ -526,7 +526,7 @@ struct pqgpu_batch {
   std::vector<uint32_t> ba_tile_page;  // byte-array tile -> page
   std::vector<uint32_t> ba_tile_order; // tiles in 8 per-XCD queues (chunk c in queue c mod 8)
   uint32_t ba_class_off[4] = {0, 0, 0, 0};  // class k's blocks in ba_tile_order
-  uint32_t n_ba_class[3] = {0, 0, 0};  // tiles per k_ba_emit class
+  uint32_t n_ba_class[4] = {0, 0, 0, 0};  // tiles per k_ba_emit class
   std::vector<uint32_t> slot_chunks;   // byte-array dictionaries materialised in slots
   uint32_t slot_grid_x = 0;
   bool any_ba_sync = false;
@@ -1379,20 +1379,24 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // tiles (in order) go to queue c mod 8 and block b takes tile b / 8 of queue b mod 8: blocks
   // are dispatched round-robin over the 8 XCDs, so the chunk's dictionary, slot table and index
   // streams stay in one XCD's L2, and a tile's predecessors have lower block indices.
-  b->n_ba_class[0] = b->n_ba_class[1] = b->n_ba_class[2] = 0;
+  b->n_ba_class[0] = b->n_ba_class[1] = b->n_ba_class[2] = b->n_ba_class[3] = 0;
   if (!b->ba_tile_page.empty()) {
-    std::vector<std::vector<uint32_t>> q(24);
+    std::vector<std::vector<uint32_t>> q(32);
     std::vector<int8_t> cls(nc, -1);
+    const char *lsv = getenv("PQ_BA_LDS_SLOTS");  // 0: no LDS slot class (comparison runs)
+    const bool lds_ok = !lsv || atoi(lsv) != 0;
     for (uint32_t c : b->ba_chunks) {
       const HostChunk &hc = b->chunks[c];
       bool slot_only = hc.slot_shift != 0 && !hc.ba_sync;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) slot_only &= b->pages[p].vkind == VK_DICT;
-      cls[c] = slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
+      // class 3: 16-B slots of a dictionary small enough for LDS (bytearray.hip k_ba_emit_lds)
+      const bool lds = lds_ok && slot_only && hc.slot_shift == 4 && hc.dict_count <= 1024;
+      cls[c] = lds ? 3 : slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
     }
     // A class with fewer than 8 chunks would leave XCDs idle: chunk k of the class (in chunk order)
     // then gets 8 / n queues and its tiles go round-robin over them, still in block order (tile j
     // of the chunk at a lower block index than tile j + 1), so the look-back is unchanged.
-    uint32_t ncls[3] = {0, 0, 0};
+    uint32_t ncls[4] = {0, 0, 0, 0};
     std::vector<uint32_t> qbase(nc, 0), qn(nc, 1), seen(nc, 0);
     for (uint32_t c : b->ba_chunks) qbase[c] = ncls[cls[c]]++;
     for (uint32_t c : b->ba_chunks) {
@@ -1408,7 +1412,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       const uint32_t c = b->pages[b->ba_tile_page[t]].chunk;
       q[8 * cls[c] + qbase[c] + seen[c]++ % qn[c]].push_back(t);
     }
-    for (uint32_t k = 0; k < 3; k++) {
+    for (uint32_t k = 0; k < 4; k++) {
       size_t m = 0;
       for (uint32_t x = 0; x < 8; x++) m = std::max(m, q[8 * k + x].size());
       b->ba_class_off[k] = (uint32_t)b->ba_tile_order.size();
@@ -1834,7 +1838,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.ba_chunks = (const uint32_t *)(A + b->l_ba);
   l.n_ba_chunks = (uint32_t)b->ba_chunks.size();
   l.n_ba_tiles = (uint32_t)b->ba_tile_page.size();
-  for (int k = 0; k < 3; k++) l.n_ba_class[k] = b->n_ba_class[k];
+  for (int k = 0; k < 4; k++) l.n_ba_class[k] = b->n_ba_class[k];
   l.slot_chunks = (const uint32_t *)(A + b->l_slot);
   l.n_slot_chunks = (uint32_t)b->slot_chunks.size();
   l.slot_grid_x = b->slot_grid_x;

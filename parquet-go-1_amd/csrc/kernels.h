@@ -72,7 +72,7 @@ struct LaunchLists {
   const WorkItem *copy_items; uint32_t n_copy_items;     // PLAIN / BOOLEAN copies (k_values_copy, no LDS)
   const uint32_t *ba_chunks; uint32_t n_ba_chunks;       // chunks with byte-array output
   uint32_t n_ba_tiles;
-  uint32_t n_ba_class[3];  // k_ba_emit tiles per class (bytearray.hip ba_emit)                                   // byte-array tiles (BatchDev::ba_tile_page)
+  uint32_t n_ba_class[4];  // k_ba_emit tiles per class (bytearray.hip ba_emit)                                   // byte-array tiles (BatchDev::ba_tile_page)
   const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
   uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
