@@ -237,10 +237,11 @@ struct EmitLDST {
   uint64_t base;              // the tile's payload base
 };
 using EmitLDS = EmitLDST<kTileRuns>;
-// Class 3: a dictionary of at most kLdsSlots 16-B slots (entries of at most 12 bytes) is copied
-// into LDS per tile, so pass A's lengths and pass B's slot pieces are LDS reads instead of random
-// gathers through the texture path (cfg4's 1,024 map keys); 256 runs per tile in LDS keep three
-// workgroups per CU.
+// Class 3: the first 16-B piece of every slot (length and the first 12 bytes) of a dictionary of at
+// most kLdsSlots entries in 16- or 32-B slots is copied into LDS per tile, so pass A's lengths and
+// pass B's first pieces are LDS reads instead of random gathers through the texture path (cfg4's
+// 1,024 map keys of 6-14 bytes); only entries longer than 12 bytes load their second piece. 256
+// runs per tile in LDS keep three workgroups per CU.
 constexpr uint32_t kLdsSlots = 1024;
 struct EmitLDSSlots {
   EmitLDST<kDictRuns> e;
@@ -463,8 +464,9 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         const uint32_t r = g * G + rr;
 #pragma unroll
         for (uint32_t q = 0; q < SV; q++)  // the slot pieces holding bytes of the entry (none: no value)
-          sl[rr][q] = len[r] && len[r] + 4 > 16 * q ? (LS ? lslots[idx[r] + q] : slots[((uint64_t)idx[r] << s4) + q])
-                                                    : make_uint4(0u, 0u, 0u, 0u);
+          sl[rr][q] = len[r] && len[r] + 4 > 16 * q
+                          ? ((LS && q == 0) ? lslots[idx[r]] : slots[((uint64_t)idx[r] << s4) + q])
+                          : make_uint4(0u, 0u, 0u, 0u);
       }
     }
 #pragma unroll
@@ -527,7 +529,7 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
 
 // Classes: chunks whose pages are all dictionary pages with a slot table of 16/32-byte (class 0)
 // or 64-byte slots (class 1), compiled without the source path; class 2: any page; class 3: as
-// class 0 with 16-B slots and at most kLdsSlots entries, the slot table read from LDS.
+// class 0 with at most kLdsSlots entries, their first slot pieces read from LDS.
 template <uint32_t CLS, class EL>
 DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   PQ_STAMPS(st, b.dbg);
@@ -550,7 +552,7 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
     hi = tl.v1;
   }
   st.lap(0);
-  if (CLS == 3) emit_tile<true, 1, true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st, lslots);
+  if (CLS == 3) emit_tile<true, 2, true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st, lslots);
   else if (CLS == 0) emit_tile<true, 2>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else if (CLS == 1 || (is_dict && cd.slot_shift)) emit_tile<true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else emit_tile<false>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
@@ -581,7 +583,8 @@ __global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_p
   if (t == ~0u) return;  // queue padding (workgroup-uniform)
   const ChunkDesc &cd = b.chunks[b.pages[b.ba_tile_page[t]].chunk];
   const uint4 *gs = gp_u64<const uint4>(cd.dict_slots);
-  for (uint32_t k = threadIdx.x; k < cd.dict_count; k += blockDim.x) L.slots[k] = gs[k];
+  const uint32_t s4 = cd.slot_shift - 4;
+  for (uint32_t k = threadIdx.x; k < cd.dict_count; k += blockDim.x) L.slots[k] = gs[(uint64_t)k << s4];
   wg_barrier();
   ba_emit<3>(b, L.e, L.slots);
 }

@@ -1389,8 +1389,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       const HostChunk &hc = b->chunks[c];
       bool slot_only = hc.slot_shift != 0 && !hc.ba_sync;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) slot_only &= b->pages[p].vkind == VK_DICT;
-      // class 3: 16-B slots of a dictionary small enough for LDS (bytearray.hip k_ba_emit_lds)
-      const bool lds = lds_ok && slot_only && hc.slot_shift == 4 && hc.dict_count <= 1024;
+      // class 3: 16- / 32-B slots of a dictionary whose first slot pieces fit in LDS
+      // (bytearray.hip k_ba_emit_lds)
+      const bool lds = lds_ok && slot_only && hc.slot_shift <= 5 && hc.dict_count <= 1024;
       cls[c] = lds ? 3 : slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
     }
     // A class with fewer than 8 chunks would leave XCDs idle: chunk k of the class (in chunk order)
