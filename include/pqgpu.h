@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 7
+#define PQGPU_ABI_VERSION 8
 
 /* Error classes (Go error value the reference returns in the same case). */
 enum pqgpu_status {
@@ -272,10 +272,12 @@ int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, 
 double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix);
 /* How the build went: result read-backs beyond the first (some chunk's completion marker, a
  * per-build generation, was not yet visible), chunks that never reported (walked by the host),
- * chunks that fell back for any reason, and 1 when the header table overflowed its largest size
- * (every chunk then falls back). */
+ * chunks that fell back for any reason, 1 when the header table overflowed its largest size
+ * (every chunk then falls back), and table entries dropped because they carry another build's
+ * generation stamp (left in reused scratch; their chunk's count no longer adds up, so the host
+ * walks it). Any pointer may be NULL. */
 int pqgpu_page_index_stats(const pqgpu_page_index *ix, int32_t *polls, int32_t *unreported, int32_t *fallback_chunks,
-                           int32_t *overflowed);
+                           int32_t *overflowed, int32_t *stale_entries);
 void pqgpu_page_index_destroy(pqgpu_page_index *ix);
 /* The host's PageHeader decode (the same fields), for comparison. */
 int pqgpu_parse_page_header(const uint8_t *buf, size_t len, pqgpu_page_header *out, int64_t *consumed);
@@ -357,7 +359,7 @@ int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
 int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
 /* The same for every timed launch slot (0 <= slot < PQGPU_TIMER_SLOTS); PQ_ERR_ARG past the end. */
-#define PQGPU_TIMER_SLOTS 21
+#define PQGPU_TIMER_SLOTS 22
 int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
                             size_t name_len);
 /* Algorithmic bytes (sections read + outputs written, counted once) of one launch
@@ -403,8 +405,8 @@ typedef struct {
   double decode_ms;        /* GPU: decode launches .. done, summed over row groups */
   double index_ms;         /* device_index: byte-range copy + device page walk, summed (part of plan_ms) */
   /* device_index builds (pqgpu_page_index_stats summed): result re-reads, chunks whose walk never
-   * reported (walked by the host), chunks the host walked for any reason */
-  int64_t ix_polls, ix_unreported, ix_fallback_chunks;
+   * reported (walked by the host), chunks the host walked for any reason, stale table entries dropped */
+  int64_t ix_polls, ix_unreported, ix_fallback_chunks, ix_stale_entries;
 } pqgpu_pipeline_stats;
 /* rgs / cols may be NULL for all row groups / all columns. */
 int pqgpu_pipeline_create(pqgpu_ctx *ctx, const pqgpu_file *f, const int32_t *rgs, int32_t n_rgs, const int32_t *cols,

@@ -63,7 +63,7 @@ DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   if (t.bw == 0) return v0 < v1;  // bit width 0: every index is 0 and no stream is read
   const uint64_t di = 2 * ((uint64_t)pd.dict_tile0 + v0 / kDictTile);
   const uint4 D = b.tile_desc[di], E = b.tile_desc[di + 1];
-  if (!E.y) return false;
+  if (E.y != 1u) return false;  // 1 = written valid by this decode's k_scan_runs (the region is 0xff-filled)
   r0 = D.x;
   r1 = D.y;
   t.v1 = min(v1, E.x);  // values covered by valid runs

@@ -383,7 +383,7 @@ static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values_dict", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
-    "k_values_copy"};
+    "k_values_copy", "k_group_flat"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -821,6 +821,8 @@ struct pqgpu_page_index {
   int32_t polls = 0;                 // result read-backs beyond the first (a chunk's marker was missing)
   int32_t unreported = 0;            // chunks whose walk never reported (kept with the host walk)
   int32_t overflowed = 0;            // 1: the table could not hold every header (every chunk falls back)
+  int32_t stale = 0;                 // entries read back with another build's generation (dropped)
+  uint32_t gen = 0;                  // generation of the build whose table was read
 };
 
 static void to_public(const PageIxEntry &x, pqgpu_page_header *o) {
@@ -1443,12 +1445,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       base += nn;
     }
   }
-  // Region set to 0xff before every decode: chunk error keys, dictionary tile table.
+  // Region set to 0xff before every decode: chunk error keys, dictionary tile table and descriptors.
   b->o_err = take((uint64_t)nc * 8);
   b->f_begin = b->o_err;
   b->o_tile_first = take(b->tile_total * 4);
+  b->o_tile_desc = take(b->tile_total * 32);  // (filled too: a descriptor k_scan_runs did not write reads invalid)
   b->f_end = a;
-  b->o_tile_desc = take(b->tile_total * 32);
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
   // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
@@ -1946,7 +1948,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (e == hipSuccess) e = hipStreamWaitEvent(ds, b->ev_levels, 0);
     if (e == hipSuccess) e = timed(b, 16, ds, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, ds); });
     if (e == hipSuccess) e = timed(b, 14, ds, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, ds); });
-    if (e == hipSuccess) e = timed(b, 14, ds, l.n_grp_tiles, [&] { return launch_group_flat(d, l, ds); });  // flat leaves
+    if (e == hipSuccess) e = timed(b, 21, ds, l.n_grp_tiles, [&] { return launch_group_flat(d, l, ds); });  // flat leaves
     if (e == hipSuccess) e = hipEventRecord(b->ev_nest_join, ds);
     return e;
   };
@@ -2273,7 +2275,9 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         const int j = hc.col.group_depth[g];
         const int64_t ent = hc.col.max_rep == 0 ? (int64_t)hc.num_slots : (j < hc.col.max_rep ? hc.num_lists[j] : hc.num_elems);
         out_bytes += (ent + 7) / 8;
-        kb[14] += (ent + 7) / 8 + (hc.col.max_rep == 0 ? (int64_t)hc.num_slots : 0);  // flat: + the u8 levels read
+        // repeated leaves: k_nest_emit writes it; flat leaves: k_group_flat (+ the u8 levels it reads)
+        if (hc.col.max_rep == 0) kb[21] += (ent + 7) / 8 + (int64_t)hc.num_slots;
+        else kb[14] += (ent + 7) / 8;
       }
     }
   }
@@ -2464,6 +2468,7 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   (void)hipStreamSynchronize(b->ctx->stream);
   (void)hipStreamSynchronize(b->ctx->side);
   (void)hipStreamSynchronize(b->ctx->copy);
+  (void)hipStreamSynchronize(b->ctx->delta);  // an error return inside decode_impl can leave forked work here
   free_payloads(b);
   if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
@@ -2484,6 +2489,9 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
 int pqgpu_batch_reset(pqgpu_batch *b) {
   if (b->ctx) {
     (void)hipStreamSynchronize(b->ctx->stream);
+    (void)hipStreamSynchronize(b->ctx->side);  // forked work of a decode that returned early
+    (void)hipStreamSynchronize(b->ctx->copy);
+    (void)hipStreamSynchronize(b->ctx->delta);
     if (b->last_stream) (void)hipStreamSynchronize(b->last_stream);  // an H2D copy may still read the stage
     free_payloads(b);
   }
@@ -2612,6 +2620,7 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     uint4 *d_res = (uint4 *)(D + 256);
     PageIxEntry *d_tab = (PageIxEntry *)(D + 256 + res_bytes);
     const uint32_t gen = ctx->next_ix_gen();
+    ix->gen = gen;
     hipError_t he = launch_page_walk((const uint8_t *)dev_bytes, len, file_offset, ix->chunks.data(), (uint32_t)n_chunks,
                                      d_res, d_tab, d_n, (uint32_t)cap, validate_crc, gen, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -2672,10 +2681,17 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     for (const auto &x : ix->entries)
       fprintf(stderr, "[ix]   e chunk %u seq %u off %lld type %d cs %d\n", x.chunk, x.seq, (long long)x.hdr_off, x.type, x.csize);
   }
-  // entries of a chunk id outside the build cannot come from a completed walk: dropped
-  ix->entries.erase(std::remove_if(ix->entries.begin(), ix->entries.end(),
-                                   [&](const PageIxEntry &x) { return x.chunk >= (uint32_t)n_chunks; }),
-                    ix->entries.end());
+  // entries stamped by another build (scratch reused: a slot this build reserved but whose store
+  // never landed) or of a chunk id outside the build cannot come from this build's walk: dropped.
+  // The per-chunk count check below then sends such a chunk to the host walk.
+  {
+    const uint32_t gen_ok = ix->gen;
+    const size_t before = ix->entries.size();
+    ix->entries.erase(std::remove_if(ix->entries.begin(), ix->entries.end(),
+                                     [&](const PageIxEntry &x) { return x.gen != gen_ok || x.chunk >= (uint32_t)n_chunks; }),
+                      ix->entries.end());
+    ix->stale = (int32_t)(before - ix->entries.size());
+  }
   // group by chunk in page order (a chunk's entries were reserved in increasing order)
   std::vector<PageIxEntry> &e = ix->entries;
   std::stable_sort(e.begin(), e.end(), [](const PageIxEntry &a, const PageIxEntry &b) {
@@ -2710,8 +2726,9 @@ int pqgpu_page_index_page(const pqgpu_page_index *ix, int32_t chunk, int32_t k, 
 double pqgpu_page_index_walk_ms(const pqgpu_page_index *ix) { return ix ? ix->walk_ms : 0.0; }
 
 int pqgpu_page_index_stats(const pqgpu_page_index *ix, int32_t *polls, int32_t *unreported, int32_t *fallback_chunks,
-                           int32_t *overflowed) {
+                           int32_t *overflowed, int32_t *stale_entries) {
   if (!ix) return PQ_ERR_ARG;
+  if (stale_entries) *stale_entries = ix->stale;
   int32_t fb = 0;
   for (const auto &k : ix->chunks) fb += k.status != IX_OK;
   if (polls) *polls = ix->polls;
@@ -2926,6 +2943,10 @@ static std::vector<std::string> path_parts(const char *p) {
 int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t *equal, pqgpu_error *err) {
   clear_err(err);
   if (equal) *equal = 0;
+  if (ia == ib) {
+    set_err(err, PQ_ERR_ARG, ib, -1, "a leaf cannot share ancestors with itself");
+    return PQ_ERR_ARG;
+  }
   pqgpu_chunk_result ra, rb;
   int e = pqgpu_batch_chunk_result(b, ia, &ra, err);
   if (!e) e = pqgpu_batch_chunk_result(b, ib, &rb, err);
@@ -2985,7 +3006,16 @@ int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t 
     same = h == 0;
   }
   if (same) {
-    hb.share_from = ia;
+    // link to the root of ia's sharing chain, never to a chunk that already follows ib: the links
+    // stay acyclic, so chunk_result's walk along share_from ends
+    int32_t root = ia;
+    for (int32_t hops = 0; b->chunks[(size_t)root].share_from >= 0 && hops <= (int32_t)b->chunks.size(); hops++)
+      root = b->chunks[(size_t)root].share_from;
+    if (root == ib) {  // ia already takes its arrays from ib: nothing to link
+      if (equal) *equal = 1;
+      return PQ_OK;
+    }
+    hb.share_from = root;
     hb.share_lists = (uint32_t)La;
     hb.share_groups = (uint32_t)Ga;
     if (equal) *equal = 1;

@@ -269,7 +269,7 @@ struct IxChunkArgs {
 __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t len, int64_t file_off,
                                                   const IxChunkArgs args, uint32_t chunk0, uint4 *res_in,
                                                   PageIxEntry *table_in, uint32_t *table_n, uint32_t table_cap,
-                                                  uint32_t gen, uint32_t sys_fence) {
+                                                  uint32_t gen, uint32_t sys_fence, uint32_t test_skip) {
   __shared__ TFrame stk[kIxDepth];
   const uint8_t *buf = gp(buf_in);
   PageIxEntry *table = gp(table_in);
@@ -294,7 +294,9 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     if (lane == 0) at = atomicAdd(table_n, n);
     at = sgpr(__shfl(at, 0));
     if ((uint64_t)at + n > table_cap) return false;
-    if (lane < n) table[at + lane] = mine;
+    // test_skip (PQ_IX_TEST_SKIP_STORE, tests only): chunk test_skip reserves its slots but stores
+    // nothing, as if its stores were lost; the host must not trust what the slots hold
+    if (lane < n && c != test_skip) table[at + lane] = mine;
     return true;
   };
   while (ch.total - count > 0) {
@@ -313,7 +315,8 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     h.hdr_len = (int32_t)hl;
     h.chunk = c;
     h.seq = seq;
-    h.pad[0] = h.pad[1] = 0;
+    h.gen = gen;
+    h.pad = 0;
     if (lane == (seq & 63)) mine = h;
     off += h.csize;
     count += h.csize;
@@ -467,13 +470,15 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
                             int validate_crc, uint32_t gen, hipStream_t s) {
   if (!nchunks) return hipSuccess;
   const uint32_t sys_fence = getenv("PQ_IX_FENCE") && atoi(getenv("PQ_IX_FENCE")) == 1;
+  const char *skip_env = getenv("PQ_IX_TEST_SKIP_STORE");  // tests: one chunk's table stores are dropped
+  const uint32_t test_skip = skip_env ? (uint32_t)atoi(skip_env) : 0xffffffffu;
   hipLaunchKernelGGL(k_page_walk_init, dim3((nchunks + 255) / 256), dim3(256), 0, s, table_n, res, nchunks);
   for (uint32_t c0 = 0; c0 < nchunks; c0 += kIxArgChunks) {
     const uint32_t n = std::min<uint32_t>(kIxArgChunks, nchunks - c0);
     IxChunkArgs a;
     memset(&a, 0, sizeof(a));
     memcpy(a.c, chunks + c0, n * sizeof(PageIxChunk));
-    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap, gen, sys_fence);
+    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap, gen, sys_fence, test_skip);
   }
   if (validate_crc)
     hipLaunchKernelGGL(k_page_crc, dim3(2048), dim3(kCrcThreads), 0, s, buf, len, file_off, table,

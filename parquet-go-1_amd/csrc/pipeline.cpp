@@ -139,8 +139,8 @@ static void worker(pqgpu_pipeline *p) {
     const int32_t rg = p->rgs[(size_t)i];
     pqgpu_page_index *ix = p->device_index ? index_row_group(p, sl, rg) : nullptr;
     const double ixms = ix ? ms_since(tp) : 0.0;
-    int32_t ix_polls = 0, ix_unrep = 0, ix_fb = 0;
-    if (ix) (void)pqgpu_page_index_stats(ix, &ix_polls, &ix_unrep, &ix_fb, nullptr);
+    int32_t ix_polls = 0, ix_unrep = 0, ix_fb = 0, ix_stale = 0;
+    if (ix) (void)pqgpu_page_index_stats(ix, &ix_polls, &ix_unrep, &ix_fb, nullptr, &ix_stale);
     for (size_t k = 0; k < p->cols.size(); k++) {
       int32_t id;
       pqgpu_error e;
@@ -167,6 +167,7 @@ static void worker(pqgpu_pipeline *p) {
       p->st.ix_polls += ix_polls;
       p->st.ix_unreported += ix_unrep;
       p->st.ix_fallback_chunks += ix_fb;
+      p->st.ix_stale_entries += ix_stale;
       p->st.upload_ms += up;
     }
     p->cv.notify_all();

@@ -235,7 +235,9 @@ struct PageIxEntry {     // 96 B: one PageHeader (format.h) and where it lies
   int32_t dict[2];       // DictionaryPageHeader: num_values, encoding
   int32_t dph2[6];       // DataPageHeaderV2: num_values, num_nulls, num_rows, encoding, def_len, rep_len
   uint32_t chunk, seq;   // walk input chunk, page position in its chunk (dictionary page included)
-  uint32_t pad[2];
+  uint32_t gen;          // the build's generation (ctx next_ix_gen): an entry left in reused scratch by
+                         // an earlier build carries another and is dropped by the host
+  uint32_t pad;
 };
 // Device-to-device copy of an UNCOMPRESSED page body from the resident file bytes into the
 // batch's page region (16-B aligned, 64 zero bytes after it), done once at upload.

@@ -111,15 +111,16 @@ class PipelineStats(ctypes.Structure):
                 ("failed_chunks", ctypes.c_int64), ("input_bytes", ctypes.c_int64), ("output_bytes", ctypes.c_int64),
                 ("wall_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
                 ("h2d_ms", ctypes.c_double), ("decode_ms", ctypes.c_double), ("index_ms", ctypes.c_double),
-                ("ix_polls", ctypes.c_int64), ("ix_unreported", ctypes.c_int64), ("ix_fallback_chunks", ctypes.c_int64)]
+                ("ix_polls", ctypes.c_int64), ("ix_unreported", ctypes.c_int64), ("ix_fallback_chunks", ctypes.c_int64),
+                ("ix_stale_entries", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _LIB = None
-TIMER_SLOTS = 21  # PQGPU_TIMER_SLOTS
-ABI_VERSION = 7  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
+TIMER_SLOTS = 22  # PQGPU_TIMER_SLOTS
+ABI_VERSION = 8  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
@@ -197,7 +198,7 @@ def lib():
                                    ctypes.c_int),
         "pqgpu_page_index_page": ([P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(PageHeader)], ctypes.c_int),
         "pqgpu_page_index_walk_ms": ([P], ctypes.c_double),
-        "pqgpu_page_index_stats": ([P] + [ctypes.POINTER(ctypes.c_int32)] * 4, ctypes.c_int),
+        "pqgpu_page_index_stats": ([P] + [ctypes.POINTER(ctypes.c_int32)] * 5, ctypes.c_int),
         "pqgpu_page_index_destroy": ([P], None),
         "pqgpu_parse_page_header": ([P, ctypes.c_size_t, ctypes.POINTER(PageHeader), ctypes.POINTER(ctypes.c_int64)],
                                     ctypes.c_int),
@@ -712,10 +713,10 @@ class PageIndex:
         return lib().pqgpu_page_index_walk_ms(self._h)
 
     def stats(self):
-        """{polls, unreported, fallback_chunks, overflowed} of the build (pqgpu_page_index_stats)."""
-        v = [ctypes.c_int32() for _ in range(4)]
+        """{polls, unreported, fallback_chunks, overflowed, stale_entries} of the build (pqgpu_page_index_stats)."""
+        v = [ctypes.c_int32() for _ in range(5)]
         lib().pqgpu_page_index_stats(self._h, *[ctypes.byref(x) for x in v])
-        return dict(zip(("polls", "unreported", "fallback_chunks", "overflowed"), (x.value for x in v)))
+        return dict(zip(("polls", "unreported", "fallback_chunks", "overflowed", "stale_entries"), (x.value for x in v)))
 
     def close(self):
         if self._h:

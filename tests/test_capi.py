@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), s
     assert set(pqgpu._EXPORTS) <= set(syms)
-    assert L.pqgpu_abi_version() == pqgpu.ABI_VERSION == 7
+    assert L.pqgpu_abi_version() == pqgpu.ABI_VERSION == 8
 
 
 def test_status_strings():

@@ -359,4 +359,37 @@ def test_build_stats_clean(gpu_ctx, name):
         ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, _all_chunks(f), whole_file=True)
         st = ix.stats()
         ix.close()
-        assert st == {"polls": 0, "unreported": 0, "fallback_chunks": 0, "overflowed": 0}, (name, st)
+        assert st == {"polls": 0, "unreported": 0, "fallback_chunks": 0, "overflowed": 0, "stale_entries": 0}, (name, st)
+
+
+@pytest.mark.parametrize("name", ["edge_tiny_pages", "cfg2_v2_small"])
+def test_stale_entries_dropped(gpu_ctx, monkeypatch, name):
+    """Table entries carry the build's generation stamp. A chunk whose walk reports success with the
+    right page count but whose table stores never landed (PQ_IX_TEST_SKIP_STORE: its slots are
+    reserved and left as they were — here holding the previous build's entries for the same chunk,
+    same slots, same count) must not be trusted: its entries are dropped as stale, the count no
+    longer adds up, the chunk falls back to the host walk, and the decode still equals the oracle."""
+    data = pqtest.load(name)
+    f = pqgpu.File(data)
+    chunks = _all_chunks(f)
+    k = len(chunks) - 1  # the chunk whose stores are dropped
+    mine = [chunks[k]]
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, mine, whole_file=True)  # fills the scratch table
+    pages, status = ix.chunk(0)
+    assert status == pqgpu.IX_OK and pages > 0
+    ix.close()
+    monkeypatch.setenv("PQ_IX_TEST_SKIP_STORE", "0")
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, mine, whole_file=True)
+    st = ix.stats()
+    assert ix.chunk(0) == (0, pqgpu.IX_FALLBACK), (name, st)
+    assert st["stale_entries"] == pages and st["fallback_chunks"] == 1 and st["unreported"] == 0, (name, st)
+    ix.close()
+    # the whole file with one chunk's stores dropped: that chunk is walked by the host, the others
+    # by the device, and every result equals the oracle's
+    monkeypatch.setenv("PQ_IX_TEST_SKIP_STORE", str(k))
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, chunks, whole_file=True)
+    st = ix.stats()
+    assert st["fallback_chunks"] == 1 and st["stale_entries"] >= 0, st
+    assert ix.chunk(k)[1] == pqgpu.IX_FALLBACK and all(ix.chunk(j)[1] == pqgpu.IX_OK for j in range(k))
+    ix.close()
+    _check_against_oracle(name, data, _decode_indexed(gpu_ctx, data))

@@ -19,6 +19,8 @@ import io
 import numpy as np
 import pytest
 
+import pqgpu
+
 import pqtest
 import py_oracle as O
 import test_ref_goldens as G
@@ -227,4 +229,25 @@ def test_gpu_share_ancestors_detects_mismatch(gpu_ctx):
     r = b.result(ids[(0, va)], copy=False)
     rk = b.result(ids[(0, ka)], copy=False)
     assert r.lvl_offsets[0] != rk.lvl_offsets[0]
+    b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_share_ancestors_no_cycles(gpu_ctx):
+    """Sharing links stay acyclic: a leaf cannot share with itself (an argument error), sharing a
+    pair in both directions leaves every result readable with the same
+    contents (chunk_result follows share_from to a root; host.cpp links to the root)."""
+    data = pqtest.load("cfg4_small")
+    f, b, ids = _decode_all(gpu_ctx, data)
+    paths = f.column_paths()
+    ka, va = ids[(0, paths.index("m.key_value.key"))], ids[(0, paths.index("m.key_value.value"))]
+    with pytest.raises(pqgpu.DecodeError):
+        b.share_ancestors(ka, ka)
+    before_k, before_v = b.result(ka), b.result(va)
+    assert b.share_ancestors(ka, va)
+    assert b.share_ancestors(va, ka)  # already shared the other way: no link back
+    for r0, r1 in ((before_k, b.result(ka)), (before_v, b.result(va))):
+        for (o1, v1), (o2, v2) in zip(r0.nested, r1.nested):
+            np.testing.assert_array_equal(o1, o2)
+            np.testing.assert_array_equal(v1, v2)
     b.close()
