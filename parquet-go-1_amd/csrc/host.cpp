@@ -473,7 +473,8 @@ struct pqgpu_batch {
   uint64_t l_pba_pages = 0, l_pba_seg0 = 0, l_pba_seg_page = 0, o_pba_segs = 0, o_pba_limit = 0;
   uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
-  std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: the byte-parallel level kernel
+  std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: k_levels_seg's first, then the others
+  uint32_t n_level_seg = 0;
   std::vector<uint32_t> delta_pages;      // tiled DELTA pages
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
@@ -1273,7 +1274,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       PageDesc &pd = b->pages[p];
       in_bytes += pd.rep_len + pd.def_len + pd.val_len;
       if (hc.col.max_def == 1 && hc.col.max_rep == 0) {
-        b->level_pages_bw1.push_back(p);
+        b->level_pages_bw1.push_back(p);  // (ordered below: pages for k_levels_seg first)
       } else if (hc.col.max_def > 0 || hc.col.max_rep > 0) {
         // generic: one k_levels workgroup per stream (page << 1 | 0 rep, 1 def) writing a run
         // table of at most one entry per two stream bytes; k_level_fill tiles expand them
@@ -1549,6 +1550,14 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_dblk_n = take((uint64_t)np * 4);
   b->l_delta = take(b->delta_pages.size() * 4);
   b->l_level = take(b->level_pages.size() * 4);
+  {  // k_levels_seg takes the pages whose definition stream fits its LDS stage (+ 16 B alignment slack)
+    const char *lsg = getenv("PQ_LV_SEG");
+    const bool seg = !(lsg && atoi(lsg) == 0);
+    auto fits = [&](uint32_t p) { return seg && (uint64_t)b->pages[p].def_len + 24 <= kSgStageHost; };
+    std::stable_partition(b->level_pages_bw1.begin(), b->level_pages_bw1.end(), fits);
+    b->n_level_seg = 0;
+    for (uint32_t p : b->level_pages_bw1) b->n_level_seg += fits(p);
+  }
   b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
   b->l_base = take(b->base_chunks.size() * 4);
@@ -1827,6 +1836,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_level_pages = (uint32_t)b->level_pages.size();
   l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
+  l.n_level_pages_seg = b->n_level_seg;
   l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
   l.n_lv_tiles = (uint32_t)b->lv_tiles.size();
   l.n_ba_delta = (uint32_t)b->ba_delta.size();

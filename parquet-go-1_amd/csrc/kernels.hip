@@ -1245,6 +1245,372 @@ __global__ void __launch_bounds__(64) k_levels_bw1w(BatchDev b_in, const uint32_
   if (lane == 0) b.page_nn[pi] = cnt;
 }
 
+// ---------------------------------------------------------------------------
+// k_levels_seg: flat OPTIONAL pages (bit width 1 definition levels -> validity bitmap and non-null
+// count; hybrid_decoder.go:81-165 through decodePackedArray helpers.go:133-149), ONE wavefront per
+// page, by verified speculation over stream segments (no workgroup barrier, no list ranking).
+//
+// The run-header chain is serial: run k+1 starts where run k ends. The stream (staged in LDS) is
+// cut into 64 segments [lo_i, hi_i), one per lane. Lane i starts kSgMargin bytes before its
+// segment at an arbitrary byte and walks run headers speculatively (a header that is not a
+// well-formed run, or one that would jump more than kSgCap bytes, moves it one byte on); a chain
+// started anywhere joins the true chain within a few runs (measured on pyarrow's def-level
+// streams: 99.5 % within 128 bytes, 99.997 % within 256, once jumps are capped — garbage varints
+// otherwise jump kilobytes and never rejoin). Its first position at or past lo_i is its ENTRY;
+// from there it walks exactly (every fast run is taken, whatever its length) up to the first
+// position at or past hi_i, its EXIT, counting the values of the runs it passed.
+// Verification is exact: lane 0 starts at stream position 0; lane i's chain IS the true chain from
+// its entry on iff entry_i == exit_(i-1) and lane i-1 is verified (chains are deterministic
+// functions of a position). The first lane that fails (or stopped at a header the fast decoder does
+// not take: a varint over 4 bytes, a run cut by EOF, an error) is re-walked from its predecessor's
+// exit with the reference's full header semantics (decode_hdr), uniformly by the wave; then the
+// next one, in lane order. A long run that jumps over whole segments leaves them empty.
+// Then a wave scan of the lanes' value counts gives every run its first value index, and each lane
+// walks its verified range again (32 values per step) and writes its values' validity bits
+// straight to the chunk bitmap
+// (pre-zeroed every decode): a lane's values are one contiguous bit range, assembled in a 64-bit
+// register accumulator; words inside the range are plain stores, the range's first and last words
+// (shared with the neighbouring lanes or pages) atomic ORs; null runs only move the cursor. Runs of
+// more than kSgLong values go to the whole wave. Runs past the one that reaches num_values are never
+// read; an error is the page's only if the reference's next() meets it before num_values (same
+// class, same value position as decodePackedArray), and a failing page writes nothing.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSgStage = kSgStageHost;  // LDS stage; pages whose stream does not fit take k_levels_bw1
+constexpr uint32_t kSgSlack = 128;    // zero bytes after the stage (reads of lanes past their range)
+constexpr uint32_t kSgMargin = 128;   // bytes a lane walks speculatively before its segment
+constexpr uint32_t kSgCap = 72;       // a speculative hop longer than this is not taken
+constexpr uint32_t kSgLong = 1024;    // runs of more values (not null runs) expand with the whole wave
+constexpr uint32_t kSgQueue = 64;
+enum : uint32_t { SG_OK = 0, SG_STOP = 1, SG_ERR = 2, SG_TRUNC = 3 };
+struct LevelSegLDS {
+  uint32_t stage[(kSgStage + kSgSlack) / 4];  // stream bytes from the 16-B aligned address below s
+  uint32_t qg[kSgQueue], qc[kSgQueue], qv[kSgQueue], nq;  // long runs: first value, count, bp | payload / 1
+};
+
+// Bytes [p, p + 8) of the staged stream (stage byte o = stream byte o - sa; zero past the stream).
+DEV uint64_t sg_bytes8(const uint32_t *stage, uint32_t o) {
+  const uint32_t a = o >> 2, sh = o & 3;
+  const uint32_t w0 = stage[a], w1 = stage[a + 1], w2 = stage[a + 2];
+  return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+
+// The fast form of the header whose 8 bytes are x, at stream position p (bit width 1): a varint of
+// at most 4 bytes announcing a well formed run complete inside the stream (RLE value 0 or 1; a
+// bit-packed run of k groups has k payload bytes). adv == 0: not a fast header (decode_hdr decides).
+struct SgHop { uint32_t adv, nv, bp, val, L; };
+DEV SgHop sg_decode(uint64_t x, uint32_t p, uint32_t n) {
+  const uint32_t u0 = (uint32_t)x;
+  const uint32_t t = ~u0 & 0x80808080u;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+  const uint32_t y = (L >= 4 ? u0 : (u0 & ((1u << (8 * L)) - 1u))) & 0x7f7f7f7fu;
+  const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+  const uint32_t cnt = h >> 1, bp = h & 1u;
+  const uint32_t adv = bp ? L + cnt : L + 1;
+  const uint32_t v = (uint32_t)(x >> (8 * L)) & 0xffu;
+  const bool ok = t != 0 && cnt != 0 && (uint64_t)p + adv <= n && (bp || v <= 1);
+  SgHop r;
+  r.adv = ok ? adv : 0u;
+  r.nv = bp ? cnt * 8 : cnt;  // cnt < 2^27
+  r.bp = bp;
+  r.val = bp ? p + L : v;
+  r.L = L;
+  return r;
+}
+
+// A lane's validity bits, in value order, into the chunk bitmap `vb` (pre-zeroed): bits gather in
+// a 64-bit accumulator; a finished word is stored plainly unless it is the first word of a range
+// (shared with whoever wrote the bits before it: atomic OR); the last, unfinished word is OR-ed.
+struct SgOut {
+  uint32_t *vb;
+  uint64_t acc;
+  uint32_t W, o;  // word of the accumulator's bit 0, bits in use
+  bool first;
+  uint32_t ones;
+  bool nostore;  // diagnostic build: PQ_ABLATE bit 20 (no bitmap stores)
+  DEV void start(uint64_t g) { W = (uint32_t)(g >> 5); o = (uint32_t)(g & 31); acc = 0; first = true; }
+  DEV void put(uint32_t x) {
+    if (!nostore) {
+      if (first) { if (x) atomicOr(&vb[W], x); }
+      else vb[W] = x;
+    }
+    first = false;
+  }
+  DEV void app(uint32_t x, uint32_t k) {  // k <= 32 bits (x has no bits above k)
+    ones += __popc(x);
+    acc |= (uint64_t)x << o;
+    o += k;
+    if (o >= 32) { put((uint32_t)acc); acc >>= 32; W++; o -= 32; }
+  }
+  DEV void zeros(uint32_t c) {  // c null values: the bitmap already holds zeros
+    const uint32_t t = o + c;
+    if (t < 32) { o = t; return; }
+    put((uint32_t)acc);
+    acc = 0;
+    W += t >> 5;
+    o = t & 31;
+  }
+  DEV void end() {  // the range's last word, shared with whoever writes the bits after it
+    if (o && acc && !nostore) atomicOr(&vb[W], (uint32_t)acc);
+    o = 0;
+  }
+};
+
+// One long run (values [g, g + c) of the chunk bitmap) by the whole wave: output word w takes run
+// bits [32 w - g, +32); words inside the run are plain stores, the two edge words atomic ORs.
+// Returns this lane's count of ones.
+DEV uint32_t sg_run_wave(uint32_t *vb, const uint32_t *stage, uint32_t sa, uint64_t g, uint32_t c, bool bp,
+                         uint32_t pay) {
+  const uint32_t lane = lane_id();
+  const uint64_t w0 = g >> 5, w1 = (g + c - 1) >> 5;
+  uint32_t ones = 0;
+  for (uint64_t w = w0 + lane; w <= w1; w += 64) {
+    const int64_t r = (int64_t)(w * 32) - (int64_t)g;  // run bit at the word's bit 0 (negative: first word)
+    const uint32_t lo = r < 0 ? (uint32_t)(-r) : 0u;    // word bits before the run
+    const uint64_t rb = r > 0 ? (uint64_t)r : 0u;       // the word's first run bit
+    const uint32_t nb = (uint32_t)min<uint64_t>(32 - lo, (uint64_t)c - rb);
+    uint32_t x = bp ? (uint32_t)(sg_bytes8(stage, pay + sa + (uint32_t)(rb >> 3)) >> (rb & 7)) : ~0u;
+    x &= nb == 32 ? ~0u : ((1u << nb) - 1u);
+    x <<= lo;
+    ones += __popc(x);
+    if (lo || nb + lo < 32) { if (x) atomicOr(&vb[w], x); }
+    else vb[w] = x;
+  }
+  return ones;
+}
+
+__global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelSegLDS L;
+  const uint32_t pi = pages[blockIdx.x], lane = lane_id();
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t ns = pd.num_slots;
+  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.def_off;
+  const uint32_t n = pd.def_len;  // n + 24 <= kSgStage (host)
+  // diagnostic build: 0 stage, 1 A, 2 B, 3 C+D; 5 B iterations, 6 A steps, 7 D steps
+  PQ_STAMPS(stp, b.dbg);
+  stp.begin();
+  // ---- stage: the stream from the 16-B aligned address at or below s, zero at and past its end
+  // (a short final group zero-fills; lanes past their range read zeros)
+  const uint32_t sa = (uint32_t)((uintptr_t)s & 15u);
+  {
+    const uint4 *g = (const uint4 *)(s - sa);
+    const uint32_t lim = n + sa;
+    const uint32_t nv = (lim + 15) / 16;
+    for (uint32_t k = lane; k < (kSgStage + kSgSlack) / 16; k += 64) {
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      if (k < nv) {
+        x = g[k];
+        const int32_t rel = (int32_t)(lim - 16 * k);
+        if (rel < 16) {
+          uint32_t q[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int32_t r = rel - 4 * i;
+            q[i] = r >= 4 ? q[i] : (r <= 0 ? 0u : (q[i] & ((1u << (8 * r)) - 1u)));
+          }
+          x = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+      }
+      *(uint4 *)&L.stage[4 * k] = x;
+    }
+    if (lane == 0) L.nq = 0;
+  }
+  uint32_t err_pos = 0, err = 0, ones = 0;
+  wave_lds_sync();
+  stp.lap(0);
+  const uint32_t need = ns;
+  const uint32_t sa4 = (uint32_t)((uintptr_t)s & 3u);
+  const uint32_t *s4 = (const uint32_t *)(s - sa4);  // decode_hdr's view: global memory
+  if (!(pd.flags & PF_DEF)) {
+    if (ns) err = PQ_ERR_INVALID;  // "reader is not initialized"
+  } else if (ns) {
+    // ---- A. speculative walks: segment [lo, hi) of lane i (branch-free body: every lane runs the
+    // same instructions; a lane past its range only reads)
+    const uint32_t S = max((n + 63) / 64, 16u);
+    const uint32_t lo = lane * S, hi = lo + S;
+    const uint32_t lim = lo < n ? min(hi, n) : 0u;
+    uint32_t p = (lane == 0 || lo <= kSgMargin || lo >= n) ? 0u : lo - kSgMargin;
+    uint32_t entry = lo < n ? (p >= lo ? p : ~0u) : n, cnt = 0, st = SG_OK;
+    for (;;) {
+      const bool act = st == SG_OK && p < lim;
+      if (!__ballot(act)) break;
+      stp.count(6);
+      const SgHop h = sg_decode(sg_bytes8(L.stage, p + sa), p, n);
+      const bool spec = p < lo;
+      const bool take = h.adv != 0 && (!spec || h.adv <= kSgCap);
+      const uint32_t np = take ? p + h.adv : p + 1u;  // (a stop does not move: st ends the walk)
+      if (act && !spec) {
+        cnt += take ? h.nv : 0u;
+        st = take ? SG_OK : SG_STOP;
+      }
+      if (act && spec && np >= lo) entry = np;
+      if (act && (take || spec)) p = np;
+    }
+    uint32_t exit = lo < n ? p : n;
+    if (lo < n && entry == ~0u) entry = p;  // (cannot stay unset: the loop runs until p >= lo)
+    stp.lap(1);
+    // ---- B. verification in lane order; the first failing lane is re-walked exactly from its
+    // predecessor's (verified) exit, uniformly by the wave
+    uint32_t err_code = 0;
+    auto bad_mask = [&]() {
+      const uint32_t prev = __shfl_up(exit, 1, 64);
+      const bool ok = st == SG_OK && (lane == 0 ? entry == 0 : entry == prev);
+      return __ballot(!ok);
+    };
+    uint64_t bad = bad_mask();
+    uint32_t f_dead = 64;  // lanes from here on hold no runs (the chain ended before them)
+    while (bad) {
+      const uint32_t f = (uint32_t)__builtin_ctzll(bad);
+      stp.count(5);
+      // values of the verified lanes before f: once they reach num_values, nothing after matters
+      const uint32_t before = (uint32_t)wave_sum64(lane < f ? cnt : 0u);
+      if (before >= need) { f_dead = f; break; }
+      uint32_t P = f ? rdlane(exit, f - 1) : 0u;
+      const uint32_t fhi = f * S + S;
+      uint32_t c = 0, fst = SG_OK, fcode = 0;
+      const uint32_t fentry = P;
+      while (P < fhi && P < n && before + c < need) {
+        const SgHop h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
+        if (h.adv) { c += h.nv; P += h.adv; continue; }
+        // the reference's full header semantics
+        const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+        if (eh.err) {
+          fst = SG_ERR;
+          fcode = eh.err == kErrLongVarint ? resolve_long_varint(s, P, n) : eh.err;
+          break;
+        }
+        const uint32_t okv = min(eh.nvals, eh.okvals);
+        if (okv < eh.nvals) {  // a bit-packed run cut by EOF: next() fails after its groups
+          c += okv;
+          fst = SG_TRUNC;
+          fcode = PQ_ERR_EOF;
+          break;
+        }
+        c += eh.nvals;
+        P += eh.adv;
+      }
+      if (lane == f) {
+        entry = fentry;
+        exit = P;
+        cnt = c;
+        st = fst;
+        err_code = fcode;
+      }
+      if (fst != SG_OK || P >= n || before + c >= need) {
+        f_dead = f + 1;  // the chain ends in lane f (error, EOF, stream end or num_values)
+        break;
+      }
+      bad = bad_mask() & ~((2ull << f) - 1ull);  // lanes <= f are verified now
+    }
+    if (lane >= f_dead) { cnt = 0; st = SG_OK; }
+    stp.lap(2);
+    // ---- C. value bases; the reference's first failure before num_values
+    const uint32_t base = wave_excl_scan(cnt);
+    const uint32_t total = (uint32_t)wave_sum64(cnt);
+    {
+      const uint64_t em = __ballot((st == SG_ERR || st == SG_TRUNC) && base + cnt < need);
+      if (em) {
+        const uint32_t e = (uint32_t)__builtin_ctzll(em);
+        err_pos = rdlane(base + cnt, e);
+        err = rdlane(err_code, e);
+      } else if (total < need) {
+        err_pos = total;  // the chain ended at the stream end: next() reads a header at EOF
+        err = PQ_ERR_EOF;
+      }
+    }
+    // ---- D. every verified lane writes its values' validity bits (a failing page writes nothing):
+    // one step = the next header when the current run is done, then up to 32 of the run's values
+    if (!err && !PQ_ABLATE(b, 21)) {  // (diagnostic: bit 21 skips D)
+      uint32_t P = entry, v = base;
+      const bool mine = cnt > 0 && base < need;
+      const uint32_t vend = min(base + cnt, need);
+      SgOut out;
+      out.vb = vbits;
+      out.ones = 0;
+      out.nostore = PQ_ABLATE(b, 20);
+      out.start(pd.slot_base + base);
+      uint32_t rem = 0, rbp = 0, rval = 0;  // the current run: values left, kind, RLE value / payload byte
+      for (;;) {
+        const bool act = mine && (rem > 0 || (P < exit && v < vend));
+        if (!__ballot(act)) break;
+        stp.count(7);
+        if (act && rem == 0) {
+          SgHop h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
+          if (!h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
+            const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+            h.adv = eh.adv;
+            h.nv = eh.nvals;
+            h.bp = eh.bp;
+            h.val = eh.value;
+          }
+          rem = min(h.nv, vend - v);
+          rbp = h.bp;
+          rval = h.val;
+          P += h.adv;
+          if (rem > kSgLong && (rbp || rval)) {  // long: the whole wave (the accumulator restarts after it)
+            const uint32_t q = atomicAdd(&L.nq, 1u);
+            if (q < kSgQueue) {
+              out.end();
+              L.qg[q] = v;
+              L.qc[q] = rem;
+              L.qv[q] = rbp ? 0x80000000u | rval : 1u;
+              v += rem;
+              rem = 0;
+              out.start(pd.slot_base + v);
+            }
+          }
+        }
+        if (PQ_ABLATE(b, 22) && act) { v += rem; rem = 0; }  // diagnostic: walk only, no emission
+        if (act && rem) {
+          if (!rbp && !rval) {  // nulls: the cursor moves
+            out.zeros(rem);
+            v += rem;
+            rem = 0;
+          } else {
+            const uint32_t k = min(32u, rem);
+            const uint32_t m = k == 32 ? ~0u : ((1u << k) - 1u);
+            const uint32_t x = rbp && !PQ_ABLATE(b, 23) ? (uint32_t)sg_bytes8(L.stage, rval + sa) & m : m;
+            out.app(x, k);
+            rval += rbp ? 4u : 0u;
+            v += k;
+            rem -= k;
+          }
+        }
+      }
+      // a bit-packed run cut by EOF ends the last lane's range: its readable values (zero filled)
+      if (mine && st == SG_TRUNC && v < need) {
+        const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+        uint32_t c = min(min(eh.okvals, eh.nvals), need - v), pay = eh.value;
+        for (uint32_t q = 0; q < c; q += 32, pay += 4) {
+          const uint32_t k = min(32u, c - q);
+          out.app((uint32_t)sg_bytes8(L.stage, pay + sa) & (k == 32 ? ~0u : ((1u << k) - 1u)), k);
+        }
+      }
+      if (mine) out.end();
+      ones = out.ones;
+      wave_lds_sync();
+      const uint32_t nq = min(L.nq, kSgQueue);
+      for (uint32_t q = 0; q < nq; q++) {
+        const uint32_t qv = L.qv[q];
+        ones += sg_run_wave(vbits, L.stage, sa, pd.slot_base + L.qg[q], L.qc[q], (qv >> 31) != 0, qv & 0x7fffffffu);
+      }
+    }
+    stp.lap(3);
+  }
+  const uint32_t cntv = (uint32_t)wave_sum64(ones);
+  if (lane == 0) {
+    if (err) {  // the reference fails the page at the first level error
+      report(b, pd.chunk, 1, pd.page_in_chunk, ST_DEF, err_pos, err);
+      b.page_nn[pi] = 0;
+    } else {
+      b.page_nn[pi] = cntv;
+    }
+  }
+  stp.flush(16);
+}
+
 // The same walk for the generic level streams (repetition levels, definition levels of max > 1):
 // one wavefront per (page, stream) writes the stream's run table (first value index; bit-packed
 // flag | payload position, or the RLE value) and the run of every k_level_fill tile's first value,
@@ -3703,9 +4069,16 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
 }
 hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (l.n_level_pages_bw1) {
-    const char *lw = getenv("PQ_LV_WAVE");  // 1: one wavefront per page (slower: DESIGN.md §5)
-    if (lw && atoi(lw) == 1) hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
-    else hipLaunchKernelGGL(k_levels_bw1, dim3(l.n_level_pages_bw1), dim3(kLvThreads), 0, s, b, l.level_pages_bw1);
+    // default: verified segment speculation (k_levels_seg); PQ_LV_SEG=0: the list-ranking workgroup
+    // kernel; PQ_LV_WAVE=1: the lane-to-lane wave walk (both slower: DESIGN.md §5)
+    const char *lw = getenv("PQ_LV_WAVE");
+    if (lw && atoi(lw) == 1) {
+      hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
+    } else {
+      const uint32_t nseg = l.n_level_pages_seg, nrest = l.n_level_pages_bw1 - nseg;
+      if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(nseg), dim3(64), 0, s, b, l.level_pages_bw1);
+      if (nrest) hipLaunchKernelGGL(k_levels_bw1, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages_bw1 + nseg);
+    }
   }
   if (l.n_level_pages) {
     const char *lw = getenv("PQ_LV_WAVE");

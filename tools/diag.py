@@ -35,9 +35,9 @@ names = ["stage", "P1_links", "P2_doubling", "P3_ckp", "P4_walkers", "P5_P6", "t
 for k, n in enumerate(names):
     v = int(d[k])
     print(f"levels {n:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
-for k, nm in enumerate(["p3_mask", "p3_desc_scan", "p3_rle", "p3_owner_shfl", "p3_emit", "p3_tail"]):
+for k, nm in enumerate(["seg_stage", "seg_A", "seg_B", "seg_CD", "seg_flush", "seg_B_iters", "seg_A_steps", "seg_D_steps"]):
     v = int(d[16 + k])
-    print(f"levels {nm:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
+    print(f"levels {nm:12s} total {v:>14d}  per page(wave) {v / pages:>12.1f}")
 for k, nm in enumerate(["w_first", "w_fetch_issue", "w_walk", "w_bar1", "w_store", "w_bar2", "w_reloads#", "w_windows#"]):
     v = int(d[24 + k])
     print(f"dwalk  {nm:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
