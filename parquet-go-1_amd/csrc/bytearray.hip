@@ -348,7 +348,12 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // slot table (any slot size: a value loads the 16-B pieces its entry occupies), else bytes are
 // read from their source (dictionaries without slots, PLAIN / DELTA pages). Pass B works in
 // groups of G rounds: the G rounds' loads are issued together.
-template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, class EL>
+// P0: pass A loads every value's whole first slot piece (its length and first 12 bytes: one request
+// per value of at most 12 bytes) and keeps it in registers for pass B instead of loading it again.
+#ifndef PQ_BA_P0
+#define PQ_BA_P0 1
+#endif
+template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool P0 = false, class EL>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,
                    uint32_t lo, uint32_t hi, bool is_dict, bool have, DictTile &tl, EL &L, Stamps &st,
                    const uint4 *lslots = nullptr) {
@@ -384,13 +389,18 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   }
   uint32_t pos[R];  // S == 0 dictionaries: the entry's position in the dictionary page
   uint32_t len[R];
+  uint4 p0[P0 ? R : 1];  // P0: the first slot pieces
 #pragma unroll
   for (uint32_t r = 0; r < R; r++) {
     pos[r] = 0;
     len[r] = 0;
+    if (P0) p0[r] = make_uint4(0u, 0u, 0u, 0u);
     if (idx[r] != ~0u) {
       if (PQ_ABLATE(b, 11)) {  // diagnostic: no length loads
         len[r] = 16;
+      } else if (P0) {
+        p0[r] = slots[(uint64_t)idx[r] << s4];
+        len[r] = p0[r].x;
       } else if (LS) {
         len[r] = lslots[idx[r]].x;  // LDS copy of the slot table (16-B slots)
       } else if (SLOT) {
@@ -464,7 +474,8 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         const uint32_t r = g * G + rr;
 #pragma unroll
         for (uint32_t q = 0; q < SV; q++)  // the slot pieces holding bytes of the entry (none: no value)
-          sl[rr][q] = len[r] && len[r] + 4 > 16 * q
+          sl[rr][q] = (P0 && q == 0) ? p0[r]
+                      : len[r] && len[r] + 4 > 16 * q
                           ? ((LS && q == 0) ? lslots[idx[r]] : slots[((uint64_t)idx[r] << s4) + q])
                           : make_uint4(0u, 0u, 0u, 0u);
       }
@@ -553,15 +564,16 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   }
   st.lap(0);
   if (CLS == 3) emit_tile<true, 2, true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st, lslots);
-  else if (CLS == 0) emit_tile<true, 2>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
+  else if (CLS == 0) emit_tile<true, 2, false, PQ_BA_P0 != 0>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else if (CLS == 1 || (is_dict && cd.slot_shift)) emit_tile<true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else emit_tile<false>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   st.count(7);
   st.flush(40);
 }
 
-// class 0 at 6 waves per SIMD (three 8-wave workgroups per CU: <= 80 VGPRs, 46 KB LDS each)
-__global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(6))) k_ba_emit_slots(BatchDev b_in) {
+// class 0 at 6 waves per SIMD (three 8-wave workgroups per CU: <= 80 VGPRs, 46 KB LDS each); with
+// the first pieces kept in registers (PQ_BA_P0) 4 waves per SIMD (<= 128 VGPRs)
+__global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(PQ_BA_P0 ? 4 : 6))) k_ba_emit_slots(BatchDev b_in) {
   const BatchDev b = global_view(b_in);
   __shared__ EmitLDS L;
   ba_emit<0>(b, L);

@@ -1266,8 +1266,7 @@ __global__ void __launch_bounds__(64) k_levels_bw1w(BatchDev b_in, const uint32_
 // exit with the reference's full header semantics (decode_hdr), uniformly by the wave; then the
 // next one, in lane order. A long run that jumps over whole segments leaves them empty.
 // Then a wave scan of the lanes' value counts gives every run its first value index, and each lane
-// walks its verified range again (32 values per step) and writes its values' validity bits
-// straight to the chunk bitmap
+// walks its verified range again and writes its values' validity bits straight to the chunk bitmap
 // (pre-zeroed every decode): a lane's values are one contiguous bit range, assembled in a 64-bit
 // register accumulator; words inside the range are plain stores, the range's first and last words
 // (shared with the neighbouring lanes or pages) atomic ORs; null runs only move the cursor. Runs of
@@ -1437,16 +1436,25 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
       const bool act = st == SG_OK && p < lim;
       if (!__ballot(act)) break;
       stp.count(6);
-      const SgHop h = sg_decode(sg_bytes8(L.stage, p + sa), p, n);
+      // up to two hops per 8-byte read: the second header is decoded from the same bytes when the
+      // first run took at most 3 of them (5 left: a 4-byte varint and an RLE value byte)
+      const uint64_t x = sg_bytes8(L.stage, p + sa);
+      const SgHop h = sg_decode(x, p, n);
       const bool spec = p < lo;
       const bool take = h.adv != 0 && (!spec || h.adv <= kSgCap);
       const uint32_t np = take ? p + h.adv : p + 1u;  // (a stop does not move: st ends the walk)
+      const SgHop h2 = sg_decode(x >> (8 * min(h.adv, 3u)), np, n);
+      const bool spec2 = np < lo;
+      const bool take2 = take && h.adv <= 3 && np < lim && h2.adv != 0 && (!spec2 || h2.adv <= kSgCap);
+      const uint32_t np2 = take2 ? np + h2.adv : np;
       if (act && !spec) {
         cnt += take ? h.nv : 0u;
         st = take ? SG_OK : SG_STOP;
       }
+      if (act && take2 && !spec2) cnt += h2.nv;
       if (act && spec && np >= lo) entry = np;
-      if (act && (take || spec)) p = np;
+      if (act && take2 && spec2 && np2 >= lo) entry = np2;
+      if (act && (take || spec)) p = np2;
     }
     uint32_t exit = lo < n ? p : n;
     if (lo < n && entry == ~0u) entry = p;  // (cannot stay unset: the loop runs until p >= lo)
@@ -1521,7 +1529,7 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
       }
     }
     // ---- D. every verified lane writes its values' validity bits (a failing page writes nothing):
-    // one step = the next header when the current run is done, then up to 32 of the run's values
+    // one run per step, a short bit-packed run's payload taken from its header's 8 bytes
     if (!err && !PQ_ABLATE(b, 21)) {  // (diagnostic: bit 21 skips D)
       uint32_t P = entry, v = base;
       const bool mine = cnt > 0 && base < need;
@@ -1531,52 +1539,52 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
       out.ones = 0;
       out.nostore = PQ_ABLATE(b, 20);
       out.start(pd.slot_base + base);
-      uint32_t rem = 0, rbp = 0, rval = 0;  // the current run: values left, kind, RLE value / payload byte
       for (;;) {
-        const bool act = mine && (rem > 0 || (P < exit && v < vend));
+        const bool act = mine && P < exit && v < vend;
         if (!__ballot(act)) break;
         stp.count(7);
-        if (act && rem == 0) {
-          SgHop h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
-          if (!h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
-            const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
-            h.adv = eh.adv;
-            h.nv = eh.nvals;
-            h.bp = eh.bp;
-            h.val = eh.value;
-          }
-          rem = min(h.nv, vend - v);
-          rbp = h.bp;
-          rval = h.val;
-          P += h.adv;
-          if (rem > kSgLong && (rbp || rval)) {  // long: the whole wave (the accumulator restarts after it)
+        const uint64_t x = sg_bytes8(L.stage, P + sa);
+        SgHop h = sg_decode(x, P, n);
+        bool slow = false;
+        if (act && !h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
+          const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+          h.adv = eh.adv;
+          h.nv = eh.nvals;
+          h.bp = eh.bp;
+          h.val = eh.value;
+          slow = true;
+        }
+        if (act) {
+          const uint32_t c = min(h.nv, vend - v);
+          bool done = false;
+          if (c > kSgLong && (h.bp || h.val)) {  // long: the whole wave (the accumulator restarts after it)
             const uint32_t q = atomicAdd(&L.nq, 1u);
             if (q < kSgQueue) {
               out.end();
               L.qg[q] = v;
-              L.qc[q] = rem;
-              L.qv[q] = rbp ? 0x80000000u | rval : 1u;
-              v += rem;
-              rem = 0;
-              out.start(pd.slot_base + v);
+              L.qc[q] = c;
+              L.qv[q] = h.bp ? 0x80000000u | h.val : 1u;
+              out.start(pd.slot_base + v + c);
+              done = true;
             }
           }
-        }
-        if (PQ_ABLATE(b, 22) && act) { v += rem; rem = 0; }  // diagnostic: walk only, no emission
-        if (act && rem) {
-          if (!rbp && !rval) {  // nulls: the cursor moves
-            out.zeros(rem);
-            v += rem;
-            rem = 0;
+          if (done || PQ_ABLATE(b, 22)) {
+          } else if (!h.bp && !h.val) {
+            out.zeros(c);  // nulls: the cursor moves
+          } else if (h.bp && !slow && h.L + ((c + 7) >> 3) <= 8) {  // payload inside the header's 8 bytes
+            const uint64_t pb = x >> (8 * h.L);
+            const uint32_t k1 = min(c, 32u);
+            out.app((uint32_t)pb & (k1 == 32 ? ~0u : ((1u << k1) - 1u)), k1);
+            if (c > 32) out.app((uint32_t)(pb >> 32) & ((1u << (c - 32)) - 1u), c - 32);
           } else {
-            const uint32_t k = min(32u, rem);
-            const uint32_t m = k == 32 ? ~0u : ((1u << k) - 1u);
-            const uint32_t x = rbp && !PQ_ABLATE(b, 23) ? (uint32_t)sg_bytes8(L.stage, rval + sa) & m : m;
-            out.app(x, k);
-            rval += rbp ? 4u : 0u;
-            v += k;
-            rem -= k;
+            for (uint32_t q = 0; q < c; q += 32) {
+              const uint32_t k = min(32u, c - q);
+              const uint32_t m = k == 32 ? ~0u : ((1u << k) - 1u);
+              out.app(h.bp ? (uint32_t)sg_bytes8(L.stage, h.val + sa + (q >> 3)) & m : m, k);
+            }
           }
+          v += c;
+          P += h.adv;
         }
       }
       // a bit-packed run cut by EOF ends the last lane's range: its readable values (zero filled)
@@ -2236,6 +2244,9 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 // The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
 // [w * 1024, (w + 1) * 1024) of the tile in 16 rounds of 64 consecutive values, so every
 // store instruction writes 64 consecutive outputs (256 B for 4-byte values).
+#ifndef PQ_DICT_LDS
+#define PQ_DICT_LDS 1
+#endif
 DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                  DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
@@ -2263,17 +2274,26 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
         else first_err = min(first_err, v);
       }
     }
+    // a dictionary that fits the stage is gathered from LDS: once every wave has its indices, the
+    // stage's stream bytes are dead and the dictionary takes their place (PQ_DICT_LDS=0: global)
+    const bool ldict = PQ_DICT_LDS && (uint64_t)dcount * w <= kTileStageB;  // workgroup-uniform
+    if (ldict) {
+      wg_barrier();  // every wave's reads of the staged stream are done
+      const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
+      for (uint32_t k = threadIdx.x; k < dcount * (w / 4); k += blockDim.x) lds.stage[k] = src[k];
+      wg_barrier();
+    }
     if (w == 4) {
-      const uint32_t *dv = gp_u64<const uint32_t>(cd.dict_values);
+      const uint32_t *dv = ldict ? lds.stage : gp_u64<const uint32_t>(cd.dict_values);
       uint32_t *out = gp_u64<uint32_t>(cd.values) + vb + seg0 + lane;
       uint32_t val[16];
 #pragma unroll
-      for (uint32_t r = 0; r < 16; r++) val[r] = idx[r] != ~0u ? dv[idx[r]] : 0u;
+      for (uint32_t r = 0; r < 16; r++) val[r] = idx[r] != ~0u ? (PQ_ABLATE(b, 24) ? idx[r] : dv[idx[r]]) : 0u;
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++)
         if (idx[r] != ~0u) out[r * 64] = val[r];
     } else {
-      const uint64_t *dv = gp_u64<const uint64_t>(cd.dict_values);
+      const uint64_t *dv = ldict ? (const uint64_t *)lds.stage : gp_u64<const uint64_t>(cd.dict_values);
       uint64_t *out = gp_u64<uint64_t>(cd.values) + vb + seg0 + lane;
 #pragma unroll
       for (uint32_t h = 0; h < 16; h += 8) {
