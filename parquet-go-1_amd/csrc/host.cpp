@@ -474,7 +474,7 @@ struct pqgpu_batch {
   uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: k_levels_seg's first, then the others
-  uint32_t n_level_seg = 0;
+  uint32_t n_level_seg = 0, n_level_units_seg = 0;
   std::vector<uint32_t> delta_pages;      // tiled DELTA pages
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
@@ -1558,6 +1558,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->n_level_seg = 0;
     for (uint32_t p : b->level_pages_bw1) b->n_level_seg += fits(p);
   }
+  {  // generic level streams: k_levels_segw takes the units whose stream fits its LDS stage
+    const char *lsg = getenv("PQ_LV_SEG");
+    const bool seg = !(lsg && atoi(lsg) == 0);
+    auto fits = [&](uint32_t u) {
+      const PageDesc &pd = b->pages[u >> 1];
+      return seg && (uint64_t)((u & 1) ? pd.def_len : pd.rep_len) + 24 <= kSgwStageHost;
+    };
+    std::stable_partition(b->level_pages.begin(), b->level_pages.end(), fits);
+    b->n_level_units_seg = 0;
+    for (uint32_t u : b->level_pages) b->n_level_units_seg += fits(u);
+  }
   b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
   b->l_base = take(b->base_chunks.size() * 4);
@@ -1837,6 +1848,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
   l.n_level_pages_seg = b->n_level_seg;
+  l.n_level_units_seg = b->n_level_units_seg;
   l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
   l.n_lv_tiles = (uint32_t)b->lv_tiles.size();
   l.n_ba_delta = (uint32_t)b->ba_delta.size();

@@ -66,6 +66,7 @@ struct LaunchLists {
   const uint32_t *lv_tiles; uint32_t n_lv_tiles;         // page of every k_level_fill tile
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   uint32_t n_level_pages_seg;  // the first n of them go to k_levels_seg (def stream fits its LDS stage)
+  uint32_t n_level_units_seg;  // the first n level_pages units go to k_levels_segw (stream fits its stage)
   uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases
@@ -89,6 +90,7 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
 hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // generic level run tables
 constexpr uint32_t kLfTileHost = 8192;  // k_level_fill tile (kernels.hip kLfTile)
 constexpr uint32_t kSgStageHost = 10240;  // k_levels_seg's LDS stage (kernels.hip kSgStage)
+constexpr uint32_t kSgwStageHost = 57344; // k_levels_segw's LDS stage (kernels.hip kSgwStage)
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);

@@ -1619,6 +1619,280 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
   stp.flush(16);
 }
 
+// ---------------------------------------------------------------------------
+// k_levels_segw: generic level streams (repetition levels; definition levels with max_def > 1) by
+// the same verified segment speculation as k_levels_seg, one 512-thread workgroup per (page,
+// stream) whose stream fits the LDS stage (kSgwStage; the rest take k_levels): 512 lanes walk
+// 512 segments, verification runs in lane order across the waves (lane 0 of wave w checks against
+// lane 63 of wave w - 1 through LDS), a failing lane is re-walked by wave 0 with decode_hdr's full
+// semantics while the others wait, a workgroup scan gives every lane its first value and first run
+// index, and each lane writes its runs to the stream's run table (first value; bit-packed flag |
+// payload position, or the RLE value) together with the run of every k_level_fill tile whose first
+// value it holds — the same table and markers k_levels writes, expanded chip-wide by k_level_fill.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSgwWaves = 8, kSgwLanes = 64 * kSgwWaves;
+constexpr uint32_t kSgwStage = kSgwStageHost;  // stream bytes staged in LDS
+struct LevelSegWLDS {
+  uint32_t stage[(kSgwStage + kSgSlack) / 4];
+  uint32_t E[kSgwLanes], X[kSgwLanes], C[kSgwLanes], NR[kSgwLanes], ST[kSgwLanes], EC[kSgwLanes];
+  uint32_t wtot[kSgwWaves], wtot2[kSgwWaves], wst[kSgwWaves], wpos[kSgwWaves], wcode[kSgwWaves];
+  uint32_t dead, err_pos, err;
+};
+
+// The fast form of the header whose 8 bytes are x at stream position p, bit width bw (rs = value
+// bytes of an RLE run): a varint of at most 4 bytes announcing a well formed run complete inside the
+// stream. adv == 0: not a fast header.
+DEV SgHop sgg_decode(uint64_t x, uint32_t p, uint32_t n, uint32_t bw, uint32_t rs) {
+  const uint32_t u0 = (uint32_t)x;
+  const uint32_t t = ~u0 & 0x80808080u;
+  const uint32_t L = (uint32_t)(__builtin_ctz(t | 0x80000000u) >> 3) + 1;
+  const uint32_t y = (L >= 4 ? u0 : (u0 & ((1u << (8 * L)) - 1u))) & 0x7f7f7f7fu;
+  const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+  const uint32_t cnt = h >> 1, bp = h & 1u;
+  const uint64_t adv = bp ? L + (uint64_t)cnt * bw : (uint64_t)(L + rs);
+  const uint32_t rv = (uint32_t)(x >> (8 * L));
+  const uint32_t v = rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u));
+  const bool ok = t != 0 && cnt != 0 && (uint64_t)p + adv <= n && (bp || bw >= 32 || (v >> bw) == 0);
+  SgHop r;
+  r.adv = ok ? (uint32_t)adv : 0u;
+  r.nv = bp ? cnt * 8 : cnt;
+  r.bp = bp;
+  r.val = bp ? p + L : v;
+  r.L = L;
+  return r;
+}
+
+__global__ void __launch_bounds__(kSgwLanes) k_levels_segw(BatchDev b_in, const uint32_t *units) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelSegWLDS L;
+  const uint32_t u = units[blockIdx.x], pi = u >> 1, which = u & 1;
+  const bool rep = which == 0;
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6, ns = pd.num_slots;
+  const uint8_t *s = gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off);
+  const uint32_t n = rep ? pd.rep_len : pd.def_len;  // n + 24 <= kSgwStage (host)
+  const uint32_t bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw), rs = (bw + 7) >> 3;
+  const uint32_t sa = (uint32_t)((uintptr_t)s & 15u);
+  const uint32_t sa4 = (uint32_t)((uintptr_t)s & 3u);
+  const uint32_t *s4 = (const uint32_t *)(s - sa4);  // decode_hdr's view: global memory
+  uint2 *runs = b.lv_runs + b.lv_run_base[2 * pi + which];
+  uint32_t *trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[pi] + which;
+  const uint32_t tile_a = (uint32_t)(pd.slot_base & (kLfTile - 1)), ntiles = lf_tiles(pd.slot_base, ns);
+  // ---- stage
+  {
+    const uint4 *g = (const uint4 *)(s - sa);
+    const uint32_t lim = n + sa, nv = (lim + 15) / 16;
+    for (uint32_t k = tid; k < (kSgwStage + kSgSlack) / 16; k += kSgwLanes) {
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      if (k < nv) {
+        x = g[k];
+        const int32_t rel = (int32_t)(lim - 16 * k);
+        if (rel < 16) {
+          uint32_t q[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int32_t r = rel - 4 * i;
+            q[i] = r >= 4 ? q[i] : (r <= 0 ? 0u : (q[i] & ((1u << (8 * r)) - 1u)));
+          }
+          x = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+      }
+      *(uint4 *)&L.stage[4 * k] = x;
+    }
+    if (tid == 0) { L.dead = kSgwLanes; L.err = 0; L.err_pos = 0; }
+  }
+  if (!rep && tid == 0) b.page_nn[pi] = 0;  // k_level_fill adds the page's non-null count
+  wg_barrier();
+  const uint32_t need = ns;
+  uint32_t nruns = 0, covered = 0;
+  if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+    if (ns && tid == 0) { L.err = PQ_ERR_INVALID; L.err_pos = 0; }  // "reader is not initialized"
+  } else if (ns) {
+    // ---- A. speculative walks (as k_levels_seg), counting values and runs
+    const uint32_t S = max((n + kSgwLanes - 1) / kSgwLanes, 16u);
+    const uint32_t lo = tid * S, hi = lo + S;
+    const uint32_t lim = lo < n ? min(hi, n) : 0u;
+    const uint32_t twomax = rs >= 4 ? 0u : 4u - rs;  // a second hop fits the 8 bytes after a first of this length
+    uint32_t p = (tid == 0 || lo <= kSgMargin || lo >= n) ? 0u : lo - kSgMargin;
+    uint32_t entry = lo < n ? (p >= lo ? p : ~0u) : n, cnt = 0, nr = 0, st = SG_OK;
+    for (;;) {
+      const bool act = st == SG_OK && p < lim;
+      if (!__ballot(act)) break;  // (each wave ends its walks alone; the barrier follows the loop)
+      const uint64_t x = sg_bytes8(L.stage, p + sa);
+      const SgHop h = sgg_decode(x, p, n, bw, rs);
+      const bool spec = p < lo;
+      const bool take = h.adv != 0 && (!spec || h.adv <= kSgCap);
+      const uint32_t np = take ? p + h.adv : p + 1u;
+      const SgHop h2 = sgg_decode(x >> (8 * min(h.adv, 3u)), np, n, bw, rs);
+      const bool spec2 = np < lo;
+      const bool take2 = take && h.adv <= twomax && np < lim && h2.adv != 0 && (!spec2 || h2.adv <= kSgCap);
+      const uint32_t np2 = take2 ? np + h2.adv : np;
+      if (act && !spec) {
+        cnt += take ? h.nv : 0u;
+        nr += take ? 1u : 0u;
+        st = take ? SG_OK : SG_STOP;
+      }
+      if (act && take2 && !spec2) { cnt += h2.nv; nr++; }
+      if (act && spec && np >= lo) entry = np;
+      if (act && take2 && spec2 && np2 >= lo) entry = np2;
+      if (act && (take || spec)) p = np2;
+    }
+    if (lo < n && entry == ~0u) entry = p;
+    L.E[tid] = entry;
+    L.X[tid] = lo < n ? p : n;
+    L.C[tid] = cnt;
+    L.NR[tid] = nr;
+    L.ST[tid] = st;
+    L.EC[tid] = 0;
+    wg_barrier();
+    // ---- B. verification in lane order (wave 0 over the workgroup's lanes, 64 at a time); the first
+    // failing lane is re-walked exactly from its predecessor's exit
+    if (wv == 0) {
+      uint32_t before = 0, prevX = 0, dead = kSgwLanes;
+      for (uint32_t w = 0; w < kSgwWaves && dead == kSgwLanes; w++) {
+        const uint32_t t = w * 64 + lane;
+        uint64_t bad;
+        auto bad_mask = [&]() {
+          const uint32_t x = L.X[t], pv = __shfl_up(x, 1, 64);
+          const uint32_t prev = lane == 0 ? prevX : pv;
+          const bool ok = L.ST[t] == SG_OK && (t == 0 ? L.E[t] == 0 : L.E[t] == prev);
+          return __ballot(!ok);
+        };
+        bad = bad_mask();
+        while (bad) {
+          const uint32_t f = (uint32_t)__builtin_ctzll(bad), ft = w * 64 + f;
+          const uint32_t bef = before + (uint32_t)wave_sum64(lane < f ? L.C[t] : 0u);
+          if (bef >= need) { dead = ft; break; }
+          uint32_t P = f ? L.X[ft - 1] : prevX;
+          const uint32_t fhi = ft * S + S;
+          uint32_t c = 0, k = 0, fst = SG_OK, fcode = 0;
+          const uint32_t fentry = P;
+          while (P < fhi && P < n && bef + c < need) {
+            const SgHop h = sgg_decode(sg_bytes8(L.stage, P + sa), P, n, bw, rs);
+            if (h.adv) { c += h.nv; k++; P += h.adv; continue; }
+            const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, bw, rs);
+            if (eh.err) {
+              fst = SG_ERR;
+              fcode = eh.err == kErrLongVarint ? resolve_long_varint(s, P, n) : eh.err;
+              break;
+            }
+            const uint32_t okv = min(eh.nvals, eh.okvals);
+            if (okv < eh.nvals) {  // a bit-packed run cut by EOF: next() fails after its groups
+              c += okv;
+              k++;
+              fst = SG_TRUNC;
+              fcode = PQ_ERR_EOF;
+              break;
+            }
+            c += eh.nvals;
+            k++;
+            P += eh.adv;
+          }
+          if (lane == 0) {
+            L.E[ft] = fentry;
+            L.X[ft] = P;
+            L.C[ft] = c;
+            L.NR[ft] = k;
+            L.ST[ft] = fst;
+            L.EC[ft] = fcode;
+          }
+          wave_lds_sync();
+          if (fst != SG_OK || P >= n || bef + c >= need) { dead = ft + 1; break; }
+          bad = bad_mask() & ~((2ull << f) - 1ull);  // lanes <= f are verified now
+        }
+        if (dead != kSgwLanes) break;
+        before += (uint32_t)wave_sum64(L.C[t]);
+        prevX = rdlane(L.X[t], 63);
+        if (before >= need) dead = w * 64 + 64;  // nothing after this wave is read
+      }
+      if (lane == 0) L.dead = dead;
+    }
+    wg_barrier();
+    const uint32_t dead = L.dead;
+    cnt = tid < dead ? L.C[tid] : 0u;
+    nr = tid < dead ? L.NR[tid] : 0u;
+    st = tid < dead ? L.ST[tid] : SG_OK;
+    entry = L.E[tid];
+    const uint32_t exit = L.X[tid], ecode = L.EC[tid];
+    wg_barrier();  // (the arrays are reused by the scans below)
+    // ---- C. value bases and run indices: workgroup scans
+    const uint32_t wi1 = wave_incl_scan32(cnt), wi2 = wave_incl_scan32(nr);
+    if (lane == 63) { L.wtot[wv] = wi1; L.wtot2[wv] = wi2; }
+    wg_barrier();
+    uint32_t base = wi1 - cnt, rbase = wi2 - nr, total = 0;
+    for (uint32_t q = 0; q < kSgwWaves; q++) {
+      const uint32_t t1 = L.wtot[q], t2 = L.wtot2[q];
+      base += q < wv ? t1 : 0u;
+      rbase += q < wv ? t2 : 0u;
+      total += t1;
+    }
+    // the reference's first failure before num_values: the first erroring lane (lane order)
+    {
+      const bool e = (st == SG_ERR || st == SG_TRUNC) && base + cnt < need;
+      const uint64_t em = __ballot(e);
+      if (lane == 0) L.wst[wv] = em ? 1u : 0u;
+      if (em && lane == (uint32_t)__builtin_ctzll(em)) { L.wpos[wv] = base + cnt; L.wcode[wv] = ecode; }
+    }
+    wg_barrier();
+    if (tid == 0) {
+      uint32_t err = 0, epos = 0;
+      for (uint32_t q = 0; q < kSgwWaves; q++)
+        if (L.wst[q]) { err = L.wcode[q]; epos = L.wpos[q]; break; }
+      if (!err && total < need) { err = PQ_ERR_EOF; epos = total; }  // a header read at EOF
+      L.err = err;
+      L.err_pos = epos;
+    }
+    wg_barrier();
+    // ---- D. runs of every verified lane into the run table, with the fill tiles' first runs
+    uint32_t wrote = 0;
+    if (!L.err) {
+      const bool mine = cnt > 0 && base < need;
+      uint32_t P = entry, v = base, ri = rbase;
+      auto put = [&](uint32_t f, uint32_t c, uint32_t info) {
+        runs[ri] = make_uint2(f, info);
+        if (c && ntiles) {  // fill tiles whose first value lies in [f, f + c): tile k > 0 starts at k * T - a
+          uint64_t k = f == 0 ? 0 : ((uint64_t)f + tile_a + kLfTile - 1) / kLfTile;
+          const uint64_t khi = min(((uint64_t)f + c - 1 + tile_a) / kLfTile, (uint64_t)ntiles - 1);
+          for (; k <= khi; k++) trun[2 * k] = ri;
+        }
+        ri++;
+        wrote++;
+      };
+      while (mine && P < exit && v < need) {
+        SgHop h = sgg_decode(sg_bytes8(L.stage, P + sa), P, n, bw, rs);
+        if (!h.adv) {
+          const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, bw, rs);
+          h.adv = eh.adv;
+          h.nv = eh.nvals;
+          h.bp = eh.bp;
+          h.val = eh.value;
+        }
+        put(v, min(h.nv, need - v), h.bp ? 0x80000000u | h.val : h.val);
+        v += h.nv;
+        P += h.adv;
+      }
+      if (mine && st == SG_TRUNC && v < need) {  // a bit-packed run cut by EOF: its readable values
+        const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, bw, rs);
+        put(v, min(min(eh.okvals, eh.nvals), need - v), 0x80000000u | eh.value);
+        v += eh.okvals;
+      }
+    }
+    // the run count (runs before num_values) and the values they cover
+    const uint32_t ww = (uint32_t)wave_sum64(wrote);
+    if (lane == 0) L.wtot[wv] = ww;
+    wg_barrier();
+    for (uint32_t q = 0; q < kSgwWaves; q++) nruns += L.wtot[q];
+    covered = min(total, need);
+  }
+  if (tid == 0) {
+    const uint32_t err = L.err;
+    b.lv_meta[4 * pi + 2 * which] = nruns;
+    b.lv_meta[4 * pi + 2 * which + 1] = err ? 0u : covered;  // a failed page is not expanded
+    if (err) report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, L.err_pos, err);
+  }
+}
+
 // The same walk for the generic level streams (repetition levels, definition levels of max > 1):
 // one wavefront per (page, stream) writes the stream's run table (first value index; bit-packed
 // flag | payload position, or the RLE value) and the run of every k_level_fill tile's first value,
@@ -4102,8 +4376,13 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
   }
   if (l.n_level_pages) {
     const char *lw = getenv("PQ_LV_WAVE");
-    if (lw && atoi(lw) == 1) hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
-    else hipLaunchKernelGGL(k_levels, dim3(l.n_level_pages), dim3(kLvThreads), 0, s, b, l.level_pages);
+    if (lw && atoi(lw) == 1) {
+      hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
+    } else {  // streams that fit k_levels_segw's stage first (host order), then the list-ranking kernel
+      const uint32_t nseg = l.n_level_units_seg, nrest = l.n_level_pages - nseg;
+      if (nseg) hipLaunchKernelGGL(k_levels_segw, dim3(nseg), dim3(kSgwLanes), 0, s, b, l.level_pages);
+      if (nrest) hipLaunchKernelGGL(k_levels, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages + nseg);
+    }
   }
   return hipGetLastError();
 }
