@@ -249,6 +249,8 @@ struct HostChunk {
   // pqgpu_batch_share_ancestors: list levels [0, share_lists) and groups [0, share_groups) are
   // chunk share_from's (cleared by every decode)
   int32_t share_from = -1;
+  int8_t ba_class = -1;  // k_ba_emit class (byte-array chunks)
+  bool ba_presum = false;  // tile bases from k_ba_sums + k_ba_scan instead of the look-back
   uint32_t share_lists = 0, share_groups = 0;
   // byte-array dictionaries: (position, length) of every entry, from the host's walk of the
   // dictionary page (page_dict.go:35-72 + byteArrayPlainDecoder type_bytearray.go:24-55)
@@ -533,7 +535,9 @@ struct pqgpu_batch {
   bool any_ba_sync = false;
   // byte-array tile bases: k_ba_emit's decoupled look-back (default), or k_ba_sums + k_ba_scan
   // before k_ba_emit (PQ_BA_PRESUM=1; cfg3: 0.16 ms of k_ba_sums for 0.02 ms less k_ba_emit)
-  bool ba_presum = getenv("PQ_BA_PRESUM") && atoi(getenv("PQ_BA_PRESUM")) == 1;
+  // PQ_BA_PRESUM=2: only the chunks of the LDS-slot class (k_ba_emit_lds) take the pre-pass
+  int ba_presum_mode = getenv("PQ_BA_PRESUM") ? atoi(getenv("PQ_BA_PRESUM")) : 0;
+  bool ba_presum = false;  // some chunk of this upload takes the pre-pass
   uint8_t *d_payload = nullptr;         // payload arena of the bounded byte-array chunks
   size_t d_payload_cap = 0;
   // device
@@ -1383,6 +1387,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // are dispatched round-robin over the 8 XCDs, so the chunk's dictionary, slot table and index
   // streams stay in one XCD's L2, and a tile's predecessors have lower block indices.
   b->n_ba_class[0] = b->n_ba_class[1] = b->n_ba_class[2] = b->n_ba_class[3] = 0;
+  b->ba_presum = false;
   if (!b->ba_tile_page.empty()) {
     std::vector<std::vector<uint32_t>> q(32);
     std::vector<int8_t> cls(nc, -1);
@@ -1396,6 +1401,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       // (bytearray.hip k_ba_emit_lds)
       const bool lds = lds_ok && slot_only && hc.slot_shift <= 5 && hc.dict_count <= 1024;
       cls[c] = lds ? 3 : slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
+    }
+    for (uint32_t c : b->ba_chunks) {
+      HostChunk &hc = b->chunks[c];
+      hc.ba_class = cls[c];
+      hc.ba_presum = !hc.ba_sync && (b->ba_presum_mode == 1 || (b->ba_presum_mode == 2 && cls[c] == 3));
+      b->ba_presum |= hc.ba_presum;
     }
     // A class with fewer than 8 chunks would leave XCDs idle: chunk k of the class (in chunk order)
     // then gets 8 / n queues and its tiles go round-robin over them, still in block order (tile j
@@ -1668,7 +1679,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       cd.ba_ntiles = 0;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
         cd.ba_ntiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
-      if (!hc.ba_sync && b->ba_presum) cd.flags |= CF_BA_PRESUM;
+      if (hc.ba_presum) cd.flags |= CF_BA_PRESUM;
       if (hc.ba_sync) {
         cd.flags |= CF_BA_SYNC;
         cd.payload = hc.payload ? (uint64_t)hc.payload : 0;  // (re)sized after the scan of each decode
@@ -2251,7 +2262,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         if ((pd.vkind == VK_DICT && w > 0) || pd.vkind == VK_RLE_BOOL)
           dict_bytes += pd.val_len + (int64_t)nn[p] * (pd.vkind == VK_RLE_BOOL ? 1 : w);  // k_values_dict
         if (w == 0 && pd.vkind == VK_DICT) {
-          if (hc.ba_sync || b->ba_presum) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices
+          if (hc.ba_sync || hc.ba_presum) kb[4] += pd.val_len;  // k_ba_sums re-reads the indices
           kb[6] += pd.val_len;
           ba_dict_nn += nn[p];
         } else if ((pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values) {
@@ -2277,7 +2288,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       } else {
         // lengths of the non-dictionary pages: read by k_ba_sums; read with their sources and
         // bytes by k_ba_emit, which writes every offset and the payload
-        if (hc.ba_sync || b->ba_presum) kb[4] += 4 * ba_other_nn;
+        if (hc.ba_sync || hc.ba_presum) kb[4] += 4 * ba_other_nn;
         kb[6] += 4 * (hc.nn + 1) + hc.payload_bytes + 12 * ba_other_nn;
         kb[5] += 16 * (int64_t)b->chunk_desc[c].ba_ntiles;
         if (hc.slot_shift) kb[12] += (int64_t)hc.dict_len + 8 * (int64_t)hc.dict_count + ((int64_t)hc.dict_count << hc.slot_shift);
