@@ -351,7 +351,7 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // P0: pass A loads every value's whole first slot piece (its length and first 12 bytes: one request
 // per value of at most 12 bytes) and keeps it in registers for pass B instead of loading it again.
 #ifndef PQ_BA_P0
-#define PQ_BA_P0 1
+#define PQ_BA_P0 0  // measured slower on cfg3 (0.476 vs 0.459 ms): off
 #endif
 template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool P0 = false, class EL>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,

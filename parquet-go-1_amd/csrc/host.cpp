@@ -237,7 +237,7 @@ struct HostChunk {
   // device outputs (offsets into the arena)
   uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0;
   // nested (Arrow-style) output: list levels (0: none), per level offsets / validity, elements
-  uint32_t nest = 0, nest_tile0 = 0;
+  uint32_t nest = 0, nest_tile0 = 0, nest_ntiles = 0;
   uint64_t o_lvl_off[PQGPU_MAX_NEST] = {}, o_lvl_valid[PQGPU_MAX_NEST] = {}, o_elem_valid = 0;
   int64_t num_lists[PQGPU_MAX_NEST] = {}, num_elems = 0;
   // struct validity of the OPTIONAL groups on the path (pqgpu_chunk_result group_*): own bitmap
@@ -484,15 +484,15 @@ struct pqgpu_batch {
   std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_tiles, nest_chunks;
   std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
   uint64_t l_grp_tiles = 0;
-  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0;
+  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, o_nest_pk = 0, l_nest_tiles = 0, l_nest_chunks = 0;
   uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
   // generic level streams: run tables ([np][2] bases) and k_level_fill tiles
   std::vector<uint64_t> lv_run_base;
-  std::vector<uint32_t> lv_tile0, lv_tiles;
+  std::vector<uint32_t> lv_tile0, lv_tiles, lf_list;
   uint64_t lv_run_total = 0;
-  uint64_t o_lv_runs = 0, o_lv_run_base = 0, o_lv_meta = 0, o_lv_tile_run = 0, o_lv_tile0 = 0, l_lv_tiles = 0;
+  uint64_t o_lv_runs = 0, o_lv_run_base = 0, o_lv_meta = 0, o_lv_tile_run = 0, o_lv_tile0 = 0, l_lv_tiles = 0, l_lf_list = 0;
   std::vector<uint32_t> page_nn_init;
   std::vector<uint64_t> page_vbase_out;  // after sync: per-page value bases / non-null counts
   std::vector<uint32_t> page_nn_out;
@@ -503,6 +503,8 @@ struct pqgpu_batch {
   // is known up front; PQ_SPEC=0 keeps the serial order. cfg2: 0.559 vs 0.595 ms per step.
   bool force_serial = spec_disabled();
   bool split_values = getenv("PQ_SPLIT_VALUES") && atoi(getenv("PQ_SPLIT_VALUES")) != 0;
+  // PQ_ONE_STREAM=1 (profiling): every launch on the batch stream, so each kernel is timed alone
+  bool one_stream = getenv("PQ_ONE_STREAM") && atoi(getenv("PQ_ONE_STREAM")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
   // k_values_delta) or as their own zero-LDS launch on the copy stream: fused in the speculative
@@ -535,8 +537,11 @@ struct pqgpu_batch {
   bool any_ba_sync = false;
   // byte-array tile bases: k_ba_emit's decoupled look-back (default), or k_ba_sums + k_ba_scan
   // before k_ba_emit (PQ_BA_PRESUM=1; cfg3: 0.16 ms of k_ba_sums for 0.02 ms less k_ba_emit)
-  // PQ_BA_PRESUM=2: only the chunks of the LDS-slot class (k_ba_emit_lds) take the pre-pass
-  int ba_presum_mode = getenv("PQ_BA_PRESUM") ? atoi(getenv("PQ_BA_PRESUM")) : 0;
+  // PQ_BA_PRESUM=2: only the chunks of the LDS-slot class (k_ba_emit_lds) take the pre-pass.
+  // Default: the pre-pass whenever nested arrays are emitted beside the values path (their kernels
+  // hold CUs the look-back's predecessors wait for; cfg4: k_ba_emit 1.31 ms in the concurrent
+  // schedule, 0.28 ms alone; step 2.38 -> 2.12 ms with the pre-pass), else the look-back.
+  int ba_presum_mode = getenv("PQ_BA_PRESUM") ? atoi(getenv("PQ_BA_PRESUM")) : -1;
   bool ba_presum = false;  // some chunk of this upload takes the pre-pass
   uint8_t *d_payload = nullptr;         // payload arena of the bounded byte-array chunks
   size_t d_payload_cap = 0;
@@ -1150,6 +1155,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->lv_run_base.assign(2 * (size_t)np, 0);
   b->lv_tile0.assign(np, 0);
   b->lv_tiles.clear();
+  b->lf_list.clear();
   b->lv_run_total = 0;
   b->page_nn_init.assign(np, 0);
   b->ba_tile_page.clear();
@@ -1201,12 +1207,6 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       else if (j == R && dg == hc.col.max_def) hc.grp_alias[g] = R ? 8 : 9;
       if (hc.grp_alias[g] < 0) hc.o_grp_valid[g] = take(words);
     }
-  }
-  {  // nested counters per 4,096-slot tile: added by k_level_fill while it expands the levels
-    uint64_t nt = 0;
-    for (uint32_t c = 0; c < nc; c++)
-      if (b->chunks[c].nest) nt += (b->chunks[c].num_slots + 4095) / 4096;
-    b->o_nest_cnt = take(nt * kNestCnt * 4);
   }
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
@@ -1368,8 +1368,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
     }
   }
-  // nested tiles (nested.hip kNestTile = 4,096 slots), grouped by the chunks' list levels so that
-  // each k_nest_emit<R> launch covers one group; a chunk's tiles are contiguous
+  // fill tiles: the nested chunks' tiles (k_nest_count / k_nest_emit, nested.hip) grouped by the
+  // chunks' list levels so that each k_nest_emit<R> launch covers one group, a chunk's tiles
+  // contiguous and in slot order; the other chunks' tiles go to k_level_fill
+  for (uint32_t t = 0; t < (uint32_t)b->lv_tiles.size(); t++)
+    if (!b->chunks[b->pages[b->lv_tiles[t]].chunk].nest) b->lf_list.push_back(t);
   for (uint32_t r = 0; r <= PQGPU_MAX_NEST + 1; r++) b->nest_first[r] = 0;
   for (uint32_t r = 1; r <= PQGPU_MAX_NEST; r++) {
     b->nest_first[r] = (uint32_t)b->nest_tiles.size();
@@ -1377,7 +1380,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HostChunk &hc = b->chunks[c];
       if (hc.nest != r) continue;
       hc.nest_tile0 = (uint32_t)b->nest_tiles.size();
-      for (uint64_t k = 0; k < (hc.num_slots + 4095) / 4096; k++) b->nest_tiles.push_back(c);
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+        const uint64_t sb = b->pages[p].slot_base, ns = b->pages[p].num_slots;
+        const uint64_t nt = ns ? (sb + ns - 1) / kLfTileHost - sb / kLfTileHost + 1 : 0;
+        for (uint64_t k = 0; k < nt; k++) b->nest_tiles.push_back(b->lv_tile0[p] + (uint32_t)k);
+      }
+      hc.nest_ntiles = (uint32_t)b->nest_tiles.size() - hc.nest_tile0;
     }
   }
   b->nest_first[PQGPU_MAX_NEST + 1] = (uint32_t)b->nest_tiles.size();
@@ -1405,7 +1413,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     for (uint32_t c : b->ba_chunks) {
       HostChunk &hc = b->chunks[c];
       hc.ba_class = cls[c];
-      hc.ba_presum = !hc.ba_sync && (b->ba_presum_mode == 1 || (b->ba_presum_mode == 2 && cls[c] == 3));
+      const int mode = b->ba_presum_mode >= 0 ? b->ba_presum_mode : (!b->one_stream && !b->nest_chunks.empty()) ? 1 : 0;
+      hc.ba_presum = !hc.ba_sync && (mode == 1 || (mode == 2 && cls[c] == 3));
       b->ba_presum |= hc.ba_presum;
     }
     // A class with fewer than 8 chunks would leave XCDs idle: chunk k of the class (in chunk order)
@@ -1537,6 +1546,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_lv_tile_run = take((uint64_t)b->lv_tiles.size() * 8);
   b->o_lv_tile0 = take((uint64_t)np * 4);
   b->l_lv_tiles = take((uint64_t)b->lv_tiles.size() * 4);
+  b->l_lf_list = take((uint64_t)b->lf_list.size() * 4);
   b->o_run_base = take((uint64_t)np * 8);
   b->o_tile_base = take((uint64_t)np * 8);
   b->o_items = take(b->items.size() * sizeof(WorkItem));
@@ -1569,9 +1579,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->n_level_seg = 0;
     for (uint32_t p : b->level_pages_bw1) b->n_level_seg += fits(p);
   }
-  {  // generic level streams: k_levels_segw takes the units whose stream fits its LDS stage
-    const char *lsg = getenv("PQ_LV_SEG");
-    const bool seg = !(lsg && atoi(lsg) == 0);
+  {  // generic level streams: k_levels_segw takes the units whose stream fits its LDS stage when
+     // PQ_LV_SEGW=1 (measured slower than the list ranking on cfg4's list streams: off by default)
+    const char *lsg = getenv("PQ_LV_SEGW");
+    const bool seg = lsg && atoi(lsg) == 1;
     auto fits = [&](uint32_t u) {
       const PageDesc &pd = b->pages[u >> 1];
       return seg && (uint64_t)((u & 1) ? pd.def_len : pd.rep_len) + 24 <= kSgwStageHost;
@@ -1588,7 +1599,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_nest_tiles = take(b->nest_tiles.size() * 4);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
-  b->o_nest_base = take((uint64_t)b->nest_tiles.size() * kNestCnt * 8);
+  b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 4);  // every entry written by k_nest_count
+  b->o_nest_base = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 8);
+  b->o_nest_pk = take((uint64_t)b->nest_tiles.size() * kNestPkWords * 8);  // written by k_nest_count
   b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
   b->arena_size = a;
   if (a > b->d_arena_cap) {
@@ -1698,6 +1711,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.list_offsets = hc.o_lists ? dp(hc.o_lists) : 0;
     cd.nest = hc.nest;
     cd.nest_tile0 = hc.nest_tile0;
+    cd.nest_ntiles = hc.nest_ntiles;
+    cd.nest_pkb = cd.rep_bw + cd.def_bw > 4 ? 1u : 0u;
     for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) {
       cd.list_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_def[k] : 0);
       cd.list_null_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_null_def[k] : 0);
@@ -1768,6 +1783,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->o_lv_run_base, b->lv_run_base.data(), b->lv_run_base.size() * 8), err);
   HIPCHECK(up(b->o_lv_tile0, b->lv_tile0.data(), b->lv_tile0.size() * 4), err);
   HIPCHECK(up(b->l_lv_tiles, b->lv_tiles.data(), b->lv_tiles.size() * 4), err);
+  HIPCHECK(up(b->l_lf_list, b->lf_list.data(), b->lf_list.size() * 4), err);
   HIPCHECK(up(b->l_scan, b->scan_pages.data(), b->scan_pages.size() * 4), err);
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
@@ -1815,6 +1831,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.nest_cnt = (uint32_t *)(A + b->o_nest_cnt);
   d.nest_base = (uint64_t *)(A + b->o_nest_base);
   d.nest_tot = (uint64_t *)(A + b->o_nest_tot);
+  d.nest_pk = (uint64_t *)(A + b->o_nest_pk);
   d.runs = (HybRun *)(A + b->o_runs);
   d.lv_runs = (uint2 *)(A + b->o_lv_runs);
   d.lv_run_base = (const uint64_t *)(A + b->o_lv_run_base);
@@ -1861,6 +1878,8 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_level_pages_seg = b->n_level_seg;
   l.n_level_units_seg = b->n_level_units_seg;
   l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
+  l.lf_list = (const uint32_t *)(A + b->l_lf_list);
+  l.n_lf_list = (uint32_t)b->lf_list.size();
   l.n_lv_tiles = (uint32_t)b->lv_tiles.size();
   l.n_ba_delta = (uint32_t)b->ba_delta.size();
   l.scan_pages = (const uint32_t *)(A + b->l_scan);
@@ -1957,7 +1976,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   l2.n_items = l.n_items - b->n_delta_items - n_dict;
   // DELTA_BINARY_PACKED items (the first n_delta_items) go to k_values_delta on the DELTA stream,
   // beside the level kernels, the copies and the other values kinds; the default stream joins it
-  hipStream_t ds = b->ctx->delta;
+  hipStream_t ds = b->one_stream ? s : b->ctx->delta;
   if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
   // streams with nothing to run are neither forked nor joined (a cross-stream wait costs latency)
   const bool any_delta = l1.n_items || l.n_delta_pages;
@@ -1969,9 +1988,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (e == hipSuccess) e = hipEventRecord(b->ev_delta_join, ds);
     return e;
   };
-  // Nested (Arrow-style) arrays and struct bitmaps need only the decoded levels and the per-tile
-  // counts k_level_fill wrote: they run on the DELTA stream (after its DELTA pages) beside the values
-  // path, from the moment k_bases is queued; the batch stream joins them at the end.
+  // Nested (Arrow-style) arrays and struct bitmaps need only the level run tables and the per-half
+  // counts k_nest_count wrote (flat leaves' struct bitmaps: k_level_fill's u8 levels): they run on
+  // the DELTA stream (after its DELTA pages) beside the values path, from the moment k_bases is
+  // queued; the batch stream joins them at the end.
   if (!b->ev_levels) HIPCHECK(hipEventCreateWithFlags(&b->ev_levels, hipEventDisableTiming), err);
   if (!b->ev_nest_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_nest_join, hipEventDisableTiming), err);
   const bool any_nest = l.n_nest_chunks || l.n_nest_tiles || l.n_grp_tiles;
@@ -1987,7 +2007,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   };
   // PLAIN / BOOLEAN copies (k_values_copy) run on the copy stream beside everything else once
   // their value bases are known: at the start in speculative mode, after k_bases otherwise.
-  hipStream_t cs = b->ctx->copy;
+  hipStream_t cs = b->one_stream ? s : b->ctx->copy;
   if (!b->ev_copy) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming), err);
   if (!b->ev_copy_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy_join, hipEventDisableTiming), err);
   auto fork_copies = [&](hipStream_t from) -> hipError_t {
@@ -2002,7 +2022,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     // Column-group pipeline: group g's run scan and dictionary tiles (side stream) and its DELTA
     // pages and fused copies (DELTA stream) start when group g's SNAPPY launch is done, beside the
     // decompression of the later groups on the batch stream.
-    hipStream_t v = b->ctx->side;
+    hipStream_t v = b->one_stream ? s : b->ctx->side;
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
     for (uint32_t g = 0; g < G; g++) {
       LaunchLists lg = l;
@@ -2031,7 +2051,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     // the values path used against the decoded ones (sync_impl re-runs serially on a miss).
     // no level streams in the batch (REQUIRED columns only): the values path runs on the batch stream
     const bool lvl = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
-    hipStream_t v = lvl ? b->ctx->side : s;
+    hipStream_t v = lvl && !b->one_stream ? b->ctx->side : s;
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
     // PQ_COPY_MODE 4: the copies beside the level kernels, the values path after them;
@@ -2057,7 +2077,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (val_then_lv && v != s) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (!b->levels_first && !lv_then_val)
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
-    HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
+    HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
+    HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(fork_nest(), err);
     if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
@@ -2067,7 +2088,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (any_delta) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
-    HIPCHECK(timed(b, 15, s, l.n_lv_tiles, [&] { return launch_level_fill(d, l, s); }), err);
+    HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
+    HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
@@ -2131,7 +2153,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)
-  // (the per-tile nested counts were added by k_level_fill; k_nest_count re-read the levels for them)
+  // (k_nest_count counted the fill tiles' halves beside k_level_fill; k_nest_emit writes the levels)
   if (any_nest) HIPCHECK(hipStreamWaitEvent(s, b->ev_nest_join, 0), err);  // nested arrays (fork_nest)
   b->decoded = true;
   return PQ_OK;
@@ -2280,8 +2302,13 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         if (hc.o_def) lv_out += (int64_t)hc.num_slots;
         if (hc.o_rep) lv_out += (int64_t)hc.num_slots;
         if (hc.o_valid) lv_out += (int64_t)(hc.num_slots + 7) / 8;
-        if (hc.col.max_rep > 0 || hc.col.max_def > 1) kb[15] += lv_in + lv_out;
-        else lvl_bytes += lv_out;
+        if (hc.nest) {  // k_nest_count expands the streams and writes the levels (k_nest_emit: the nested arrays)
+          kb[13] += lv_in + lv_out;
+        } else if (hc.col.max_rep > 0 || hc.col.max_def > 1) {
+          kb[15] += lv_in + lv_out;
+        } else {
+          lvl_bytes += lv_out;
+        }
       }
       if (w) {
         val_bytes += hc.nn * w;  // (less the direct SNAPPY pages' values, below)
@@ -2295,10 +2322,8 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         (void)ba_dict_nn;
       }
       if (hc.o_lists && !hc.nest) kb[7] += (int64_t)hc.num_slots + 4 * (hc.records + 1);
-      if (hc.nest) {  // levels read by both nested kernels; offsets and bitmaps written by k_nest_emit
-        const int64_t lv = (int64_t)hc.num_slots * (hc.o_def ? 2 : 1) + (hc.o_def ? 0 : (int64_t)hc.num_slots / 8);
-        kb[13] += lv;
-        kb[14] += lv + (hc.num_elems + 7) / 8 + 4 * (hc.records + 1);  // + record offsets
+      if (hc.nest) {  // offsets and bitmaps written by k_nest_emit
+        kb[14] += (hc.num_elems + 7) / 8 + 4 * (hc.records + 1);  // + record offsets
         for (uint32_t k = 0; k < hc.nest; k++) kb[14] += 4 * (hc.num_lists[k] + 1) + (hc.num_lists[k] + 7) / 8;
         out_bytes += (hc.num_elems + 7) / 8;
         for (uint32_t k = 0; k < hc.nest; k++) out_bytes += 4 * (hc.num_lists[k] + 1) + (hc.num_lists[k] + 7) / 8;

@@ -20,9 +20,10 @@ struct BatchDev {
   uint32_t *page_rec;             // [npages] records (rep == 0) per page
   uint64_t *page_vbase;           // [npages] value base within chunk
   uint64_t *page_rbase;           // [npages] record base within chunk
-  uint32_t *nest_cnt;             // [ntiles][kNestCnt] lists starting per level, then elements, per tile
-  uint64_t *nest_base;            // [ntiles][kNestCnt] their exclusive prefix within the chunk
+  uint32_t *nest_cnt;             // [nested tiles][2][kNestCnt] lists starting per level, then elements, per half tile
+  uint64_t *nest_base;            // [nested tiles][2][kNestCnt] their exclusive prefix within the chunk
   uint64_t *nest_tot;             // [nchunks][kNestCnt] chunk totals
+  uint64_t *nest_pk;              // [nested tiles][kNestPkWords] the tiles' levels, packed by k_nest_count for k_nest_emit
   HybRun *runs;                   // run tables of hybrid value streams
   const uint64_t *run_base;       // [npages] first entry of each page's run table
   uint32_t *run_count;            // [npages]
@@ -57,13 +58,15 @@ struct BatchDev {
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
 constexpr uint32_t kNestCnt = 9;       // nested counters per page: lists of levels 1..8, then elements
+constexpr uint32_t kNestPkWords = 2048; // u64 words of packed levels per nested tile (nested.hip)
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
                                         // page's BA tiles are its dictionary tiles)
 
 struct LaunchLists {
   const uint32_t *level_pages; uint32_t n_level_pages;   // generic level streams: page << 1 | (0 rep, 1 def)
-  const uint32_t *lv_tiles; uint32_t n_lv_tiles;         // page of every k_level_fill tile
+  const uint32_t *lv_tiles; uint32_t n_lv_tiles;         // page of every fill tile
+  const uint32_t *lf_list; uint32_t n_lf_list;           // fill tiles of the non-nested chunks (k_level_fill)
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   uint32_t n_level_pages_seg;  // the first n of them go to k_levels_seg (def stream fits its LDS stage)
   uint32_t n_level_units_seg;  // the first n level_pages units go to k_levels_segw (stream fits its stage)
@@ -78,7 +81,7 @@ struct LaunchLists {
   const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
   uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
-  const uint32_t *nest_tiles; uint32_t n_nest_tiles;     // chunk of every 4,096-slot nested tile
+  const uint32_t *nest_tiles; uint32_t n_nest_tiles;     // fill tiles of the nested chunks (k_nest_count / k_nest_emit)
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
   const uint32_t *nest_chunks; uint32_t n_nest_chunks;
   const uint32_t *grp_tiles; uint32_t n_grp_tiles;       // chunk of every k_group_flat tile

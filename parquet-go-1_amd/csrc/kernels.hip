@@ -21,6 +21,7 @@
 #include "dev_util.h"
 #include "dict_tile.h"
 #include "kernels.h"
+#include "level_fill.h"
 
 namespace pq {
 
@@ -529,11 +530,6 @@ constexpr uint32_t kNoEntry = 0xffffffffu;
 constexpr uint32_t kLvRunShift = 48;  // generic widths: run counts in the P5 scan's high bits
 constexpr uint64_t kLvValMask = (1ull << kLvRunShift) - 1;
 constexpr uint32_t kLvTileBuf = 64;
-constexpr uint32_t kLfTile = kLfTileHost;  // values per k_level_fill tile (aligned on the chunk's slots)
-// Fill tiles of a page: the kLfTile-slot blocks of the chunk that hold any of its slots.
-DEV uint32_t lf_tiles(uint64_t slot_base, uint32_t ns) {
-  return ns ? (uint32_t)((slot_base + ns - 1) / kLfTile - slot_base / kLfTile + 1) : 0u;
-}
 enum : uint32_t { LV_RUN = 0, LV_STOP_NEED = 1, LV_STOP_ERR = 2, LV_STOP_TRUNC = 3 };
 
 struct LevelLDS {
@@ -2109,67 +2105,20 @@ __global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu
 // kLfRuns of them, searched in global memory), the run of a group's first value is found by
 // binary search and the group advances from there. Outputs: u8 levels, validity (definition
 // level == max_def) and the page's counts (records: repetition level == 0; non-null values),
-// added atomically once per tile.
+// added atomically once per tile. Nested chunks' tiles go to k_nest_count / k_nest_emit
+// (nested.hip), which expand both streams together and keep the levels in registers.
 constexpr uint32_t kLfGroups = kLfTile / (8 * kLvThreads);
-constexpr uint32_t kLfRuns = 2048;  // runs staged in LDS
 static_assert(kLfGroups * 8 * kLvThreads == kLfTile, "tile = groups x 8 values x threads");
 struct LevelFillLDS {
   uint2 run[kLfRuns];
   uint32_t vb[kLfTile / 32];
   uint32_t cnt[kLvThreads / 64];
-  uint32_t nest[2][kNestCnt][kLvThreads / 64];  // nested counters of the tile's two 4,096-slot halves
 };
-// The eight values of the group [g, g + 8) that lie in [vs, ve), from run table `R` (m runs):
-// one step per run the values cross (usually one, at a run boundary two), each step an RLE
-// broadcast or one read of the bit-packed payload, so the lanes of a wave stay converged.
-template <class RT>
-DEV void lf_group(const RT &R, uint32_t m, const uint8_t *src, uint32_t n, uint32_t bw, uint32_t cmp, int64_t g,
-                  uint32_t vs, uint32_t ve, uint64_t &word, uint32_t &eq) {
-  word = 0;
-  eq = 0;
-  if (vs >= ve) return;
-  uint32_t j = 0;
-  for (uint32_t step = 1u << (31 - __builtin_clz(m)); step; step >>= 1)
-    if (j + step < m && R(j + step).x <= vs) j += step;
-  const uint32_t bmask = (1u << bw) - 1u;
-  for (uint32_t v = vs; v < ve; j++) {
-    const uint2 r = R(j);
-    const uint32_t se = j + 1 < m ? min(ve, R(j + 1).x) : ve;  // this run's part of the group
-    const uint32_t cnt = se - v, sh = v - (uint32_t)g;
-    uint64_t pk;
-    uint32_t e;
-    if (!(r.y >> 31)) {  // RLE
-      pk = 0x0101010101010101ull * (uint64_t)(r.y & 0xffu);
-      e = r.y == cmp ? 0xffu : 0u;
-    } else if (bw <= 7) {  // bit-packed: one read for the segment
-      const uint64_t x = bits64c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v - r.x) * bw, cnt * bw);
-      pk = 0;
-      e = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < 8; q++) {
-        const uint32_t lv = (uint32_t)(x >> (q * bw)) & bmask;
-        pk |= (uint64_t)lv << (8 * q);
-        e |= (uint32_t)(lv == cmp) << q;
-      }
-    } else {  // wide levels (max level >= 128): value by value
-      pk = 0;
-      e = 0;
-      for (uint32_t q = 0; q < cnt; q++) {
-        const uint32_t lv = bits32c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v + q - r.x) * bw, bw);
-        pk |= (uint64_t)(lv & 0xffu) << (8 * q);
-        e |= (uint32_t)(lv == cmp) << q;
-      }
-    }
-    const uint64_t bm = cnt >= 8 ? ~0ull : ((1ull << (8 * cnt)) - 1ull);
-    word |= (pk & bm) << (8 * sh);
-    eq |= (e & ((1u << cnt) - 1u)) << sh;
-    v = se;
-  }
-}
-__global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const uint32_t *tiles) {
+// lv_tiles: page of every fill tile; list: the fill tiles of this launch
+__global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const uint32_t *lv_tiles, const uint32_t *list) {
   const BatchDev b = global_view(b_in);
   __shared__ LevelFillLDS L;
-  const uint32_t t = blockIdx.x, pi = tiles[t], tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t t = list[blockIdx.x], pi = lv_tiles[t], tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const PageDesc &pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint64_t sbase = pd.slot_base;
@@ -2178,7 +2127,6 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
   const int64_t t0 = (int64_t)k * kLfTile - a;  // page value index of the tile's first (aligned) slot
   const uint32_t lo = (uint32_t)max(t0, (int64_t)0), hi = (uint32_t)min(t0 + kLfTile, (int64_t)ns);
   const uint8_t *page = gp_u64<const uint8_t>(pd.data);
-  const uint32_t R = cd.nest;  // nested chunks: the tile's nested counters at the end
   for (uint32_t which = 0; which < 2; which++) {
     const bool rep = which == 0;
     if (rep ? cd.max_rep == 0 : cd.max_def == 0) continue;
@@ -2244,73 +2192,6 @@ __global__ void __launch_bounds__(kLvThreads) k_level_fill(BatchDev b_in, const 
       }
     }
     wg_barrier();  // L is reused by the next stream
-  }
-  if (R) {
-    // nested counters (nested.hip nest_flag: lists of levels 1..R starting, then leaf elements) of
-    // the tile's two 4,096-slot halves: groups 0-1 / 2-3 of every thread; one atomic per counter
-    // per half, the counters ride in 5-bit fields of one 64-bit sum (at most 16 slots per thread-half).
-    // Counter j < R: a level-(j+1) list starts (r <= j, d >= D_j); counter R: a leaf element
-    // (d >= D_R). Eight levels per 64-bit word compared at once (SWAR: levels below 128; wider
-    // levels take the byte loop).
-    constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
-    auto ge = [&](uint64_t x, uint32_t t) -> uint64_t { return ((x | H) - L1 * t) & H; };  // bytes x >= t
-    // The levels are read back from this thread's own stores of the two passes (each thread expanded
-    // the same groups of both streams), the definition bits from the LDS bitmap when max_def == 1.
-    const bool swar = cd.max_def < 128;
-    const uint32_t cov_r = b.lv_meta[4 * pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * pi + 3] : ns;
-    const uint32_t endc = min(hi, min(cov_r, cov_d));
-    const uint8_t *ro = gp_u64<const uint8_t>(cd.rep_levels) + sbase;
-    const uint8_t *dlv = cd.def_levels ? gp_u64<const uint8_t>(cd.def_levels) + sbase : nullptr;
-    uint64_t pa = 0, pb = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kLfGroups; q++) {
-      const int64_t g = t0 + (int64_t)(q * 8 * kLvThreads + 8 * tid);
-      const uint32_t vs = (uint32_t)max(g, (int64_t)lo), ve = (uint32_t)max(min(g + 8, (int64_t)endc), (int64_t)vs);
-      const uint32_t vm = vs < ve ? ((1u << (ve - vs)) - 1u) << (vs - (uint32_t)g) : 0u;
-      uint64_t acc = 0;
-      uint64_t rwq = 0, dwq = 0;
-      if (vm) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(ro + g);  // 8-B aligned: g is a group start
-        rwq = ((uint64_t)x.y << 32) | x.x;
-        if (dlv) {
-          const uint2 y = *reinterpret_cast<const uint2 *>(dlv + g);
-          dwq = ((uint64_t)y.y << 32) | y.x;
-        } else if (cd.max_def == 1) {  // the bitmap byte of the group: definition level = bit
-          const uint32_t e = reinterpret_cast<const uint8_t *>(L.vb)[q * kLvThreads + tid];
-          dwq = ((uint64_t)e * L1) & 0x8040201008040201ull;
-          dwq = ((dwq + 0x7f7f7f7f7f7f7f7full) & H) >> 7;
-        }
-      }
-      if (swar) {
-        const uint64_t mb = (((uint64_t)vm * L1) & 0x8040201008040201ull) + 0x7f7f7f7f7f7f7f7full & H;  // covered slots
-        for (uint32_t j = 0; j <= R; j++) {
-          const uint64_t th = j ? cd.list_def[j - 1] : 0u;
-          const uint64_t f = j < R ? ge(dwq, (uint32_t)th) & ~ge(rwq, j + 1) : ge(dwq, cd.list_def[R - 1]);
-          acc += (uint64_t)__popcll(f & mb) << (5 * j);
-        }
-      } else {
-#pragma unroll 1
-        for (uint32_t i = 0; i < 8; i++) {
-          if (!((vm >> i) & 1u)) continue;
-          const uint32_t r = (uint32_t)(rwq >> (8 * i)) & 0xffu, d = (uint32_t)(dwq >> (8 * i)) & 0xffu;
-          for (uint32_t j = 0; j <= R; j++)
-            acc += (uint64_t)(j < R ? (r <= j && d >= (j ? cd.list_def[j - 1] : 0u)) : d >= cd.list_def[R - 1]) << (5 * j);
-        }
-      }
-      if (q < kLfGroups / 2) pa += acc; else pb += acc;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++) {
-      const uint32_t a2 = (uint32_t)wave_sum64((pa >> (5 * j)) & 31u), b2 = (uint32_t)wave_sum64((pb >> (5 * j)) & 31u);
-      if (lane == 0) { L.nest[0][j][wv] = a2; L.nest[1][j][wv] = b2; }
-    }
-    wg_barrier();
-    if (tid < 2 * kNestCnt) {
-      const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
-      const uint32_t c = L.nest[h][j][0] + L.nest[h][j][1] + L.nest[h][j][2] + L.nest[h][j][3];
-      const uint64_t cs = ((sbase + (uint64_t)t0) >> 12) + h;  // the chunk's 4,096-slot nested tile
-      if (c) atomicAdd(&b.nest_cnt[(uint64_t)(cd.nest_tile0 + cs) * kNestCnt + j], c);
-    }
   }
 }
 
@@ -4430,8 +4311,8 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
   return hipGetLastError();
 }
 hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
-  if (l.n_lv_tiles)
-    hipLaunchKernelGGL(k_level_fill, dim3(l.n_lv_tiles), dim3(kLvThreads), 0, s, b, l.lv_tiles);
+  if (l.n_lf_list)
+    hipLaunchKernelGGL(k_level_fill, dim3(l.n_lf_list), dim3(kLvThreads), 0, s, b, l.lv_tiles, l.lf_list);
   return hipGetLastError();
 }
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
@@ -4456,8 +4337,9 @@ hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t
 }
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s, bool tiles) {
   if (!n) return hipSuccess;
-  const char *lde = getenv("PQ_DELTA_LOADER");  // 0: the 256-thread kernel (every wave loads)
-  const bool ld = !(lde && atoi(lde) == 0);
+  // PQ_DELTA_LOADER=1: the 320-thread kernel with a loader wave (measured slower on cfg2: off)
+  const char *lde = getenv("PQ_DELTA_LOADER");
+  const bool ld = lde && atoi(lde) == 1;
   if (ld && !tiles) hipLaunchKernelGGL(k_values_delta_ld, dim3(n), dim3(320), 0, s, b, items);
   else hipLaunchKernelGGL(k_values_delta, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();

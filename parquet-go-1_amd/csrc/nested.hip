@@ -13,22 +13,21 @@
 //   a level-k list gains a child   iff r <= k and d >= Dk  (= a level-(k+1) list starts; for the
 //                                      innermost level, a leaf element slot exists)
 //   a leaf element is non-null     iff d == maxD
-// Three launches over 4,096-slot tiles of the chunks: counts per tile (k_nest_count), per-chunk
-// exclusive scans over tiles (k_nest_scan), then the outputs (k_nest_emit), which also writes the
-// chunk's record offsets.
+// Three launches over the fill tiles of the chunks' pages (level_fill.h: kLfTile slots aligned on
+// the chunk's slot index, one per page that holds slots of it), each cut into two 4,096-slot
+// halves: counts per half (k_nest_count), per-chunk exclusive scans over the halves (k_nest_scan),
+// then the outputs (k_nest_emit): u8 levels, slot validity, list / record offsets and bitmaps.
+// Both tile kernels expand the two level streams from the run tables the level kernels wrote
+// (reading the compressed streams, ~0.4 B per slot) and keep the levels of their slots in
+// registers: no level array is read back.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 
 #include "dev_util.h"
+#include "level_fill.h"
 
 namespace pq {
-
-DEV uint32_t slot_def(const ChunkDesc &cd, const uint8_t *dl, const uint32_t *valid, uint64_t slot) {
-  if (dl) return dl[slot];
-  if (valid) return (valid[slot >> 5] >> (slot & 31)) & 1u;  // max_def == 1: the bit is the level
-  return 0;
-}
 
 // Counter j of slot (rep r, def d): j < R: a level-(j+1) list starts; j == R: a leaf element.
 DEV bool nest_flag(const ChunkDesc &cd, uint32_t j, uint32_t r, uint32_t d) {
@@ -37,84 +36,325 @@ DEV bool nest_flag(const ChunkDesc &cd, uint32_t j, uint32_t r, uint32_t d) {
   return d >= cd.list_def[R - 1];
 }
 
-constexpr uint32_t kNestTile = 4096;  // slots per tile (a chunk's slots are cut into tiles)
-constexpr uint32_t kNestWaveSlots = kNestTile / 4;
+constexpr uint32_t kNestHalf = 4096;               // slots per counting unit (half a fill tile)
+constexpr uint32_t kNestWaveSlots = kNestHalf / 4;  // a wave's slots of a half (16 per lane)
+static_assert(2 * kNestHalf == kLfTile, "a fill tile is two counting units");
 
-struct NestTile {
-  const ChunkDesc *cd;
-  uint32_t chunk, local;  // tile index within the chunk
-  uint64_t s0, s1;        // chunk slots [s0, s1)
+// The fill tile of nested tile `t` (global fill tile index; lv_tiles[t] = its page): the page's
+// slots [lo, hi) it covers, t0 = the page value index of its first (aligned) slot.
+struct NestFill {
+  uint32_t pi, k, lo, hi, ntiles;
+  int64_t t0;
+  uint64_t sbase;
 };
-
-DEV NestTile nest_tile(const BatchDev &b, const uint32_t *tile_chunk, uint32_t t) {
-  NestTile x;
-  x.chunk = tile_chunk[t];
-  x.cd = &b.chunks[x.chunk];
-  x.local = t - x.cd->nest_tile0;
-  x.s0 = (uint64_t)x.local * kNestTile;
-  x.s1 = min(x.s0 + kNestTile, x.cd->num_slots);
+DEV NestFill nest_fill(const BatchDev &b, const uint32_t *lv_tiles, uint32_t t) {
+  NestFill x;
+  x.pi = lv_tiles[t];
+  const PageDesc &pd = b.pages[x.pi];
+  x.sbase = pd.slot_base;
+  const uint32_t ns = pd.num_slots, a = (uint32_t)(x.sbase & (kLfTile - 1));
+  x.ntiles = lf_tiles(x.sbase, ns);
+  x.k = t - b.lv_tile0[x.pi];
+  x.t0 = (int64_t)x.k * kLfTile - a;
+  x.lo = (uint32_t)max(x.t0, (int64_t)0);
+  x.hi = (uint32_t)min(x.t0 + kLfTile, (int64_t)ns);
   return x;
 }
 
-// Per tile: how many entries of each counter (lists of levels 1..R, then leaf elements). A
-// thread takes 16 consecutive slots with one 16-byte load per level array (the level arrays
-// are 16-byte padded; a tile starts on a multiple of 4,096 slots).
-__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_t *tile_chunk) {
-  const BatchDev b = global_view(b_in);
-  const uint32_t t = blockIdx.x;
-  const NestTile x = nest_tile(b, tile_chunk, t);
-  const ChunkDesc &cd = *x.cd;
-  const uint8_t *rl = gp_u64<const uint8_t>(cd.rep_levels);
-  const uint8_t *dl = gp_u64<const uint8_t>(cd.def_levels);
-  const uint32_t *vb = gp_u64<const uint32_t>(cd.validity);
-  __shared__ uint32_t part[kNestCnt][4];
-  const uint32_t R = cd.nest, lane = lane_id(), wv = threadIdx.x >> 6;
-  uint32_t c[kNestCnt] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t s = x.s0 + 16 * (uint64_t)threadIdx.x;
-  if (s < x.s1) {
-    const uint32_t ns = (uint32_t)min((uint64_t)16, x.s1 - s);
-    const uint4 rv = *reinterpret_cast<const uint4 *>(rl + s);
-    uint4 dv = make_uint4(0, 0, 0, 0);
-    uint32_t vbits = 0;
-    if (dl) dv = *reinterpret_cast<const uint4 *>(dl + s);
-    else if (vb) vbits = vb[s >> 5] >> (s & 31);  // max_def == 1: the bit is the level
-    const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
+// One level stream of a fill tile: its runs from the one holding the tile's first value, staged
+// in LDS (`L`, kNfRuns entries) when they fit; `end`: the tile's values the stream covers end
+// there (a failed stream covers none). Workgroup-uniform; the caller synchronises after it.
+constexpr uint32_t kNfRuns = 1024;          // runs per stream staged by the nested tile kernels
+constexpr uint32_t kNfGroups = kLfTile / 8;  // groups of eight values per fill tile
+struct LfStream {
+  const uint2 *runs;
+  const uint8_t *src;
+  uint32_t m, n, bw, cmp, end;
+  bool staged, on;
+};
+DEV LfStream lf_stream(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, const NestFill &x, uint32_t which,
+                       uint2 *L, uint32_t tid) {
+  LfStream S;
+  const bool rep = which == 0;
+  S.on = false;
+  S.end = x.lo;
+  S.m = 0;
+  S.staged = false;
+  S.runs = nullptr;
+  S.src = nullptr;
+  S.n = S.bw = S.cmp = 0;
+  if (rep ? cd.max_rep == 0 : cd.max_def == 0) return S;
+  const uint32_t nr = b.lv_meta[4 * x.pi + 2 * which], cov = b.lv_meta[4 * x.pi + 2 * which + 1];
+  S.end = min(x.hi, cov);
+  if (x.lo >= S.end || nr == 0) {
+    S.end = x.lo;
+    return S;
+  }
+  const uint2 *runs = b.lv_runs + b.lv_run_base[2 * x.pi + which];
+  const uint32_t *trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[x.pi] + which;
+  const uint32_t r0 = trun[2 * x.k];
+  const bool more = x.k + 1 < x.ntiles && x.t0 + (int64_t)kLfTile < (int64_t)cov;
+  S.m = (more ? trun[2 * (x.k + 1)] : nr - 1) - r0 + 1;
+  S.runs = runs + r0;
+  S.staged = S.m <= kNfRuns;
+  if (S.staged)
+    for (uint32_t i = tid; i < S.m; i += 256) L[i] = S.runs[i];
+  S.src = gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off);
+  S.n = rep ? pd.rep_len : pd.def_len;
+  S.bw = (uint32_t)(rep ? cd.rep_bw : cd.def_bw);
+  S.cmp = rep ? 0u : (uint32_t)cd.max_def;
+  S.on = true;
+  return S;
+}
+// Thread tid's group q (q = 2 h + e) of a fill tile: 16 consecutive slots per thread and half;
+// its index among the tile's groups is h * 512 + 2 tid + e.
+DEV int64_t nest_group(const NestFill &x, uint32_t tid, uint32_t q) {
+  return x.t0 + (int64_t)((q >> 1) * kNestHalf + 16 * tid + 8 * (q & 1));
+}
+// Mask of the slots [g, g + n) that lie in [lo, end)
+DEV uint32_t nest_inmask(int64_t g, uint32_t n, uint32_t lo, uint32_t end) {
+  const int64_t vs = max(g, (int64_t)lo), ve = min(g + (int64_t)n, (int64_t)end);
+  return vs < ve ? (uint32_t)(((1ull << (ve - vs)) - 1ull) << (vs - g)) : 0u;
+}
+DEV uint32_t wave_incl_max(uint32_t v, uint32_t lane) {
 #pragma unroll
-    for (uint32_t q = 0; q < 16; q++) {
-      const uint32_t r = (rw[q >> 2] >> (8 * (q & 3))) & 0xffu;
-      const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
-      const bool in = q < ns;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d);
+    if (lane >= d) v = max(v, o);
+  }
+  return v;
+}
+
+// LDS of the expansion: both streams' staged runs and, per group of the tile, the last run that
+// starts at or before the group (marked by the runs, then a workgroup prefix maximum), so that a
+// group finds its run with one LDS read instead of a binary search.
+struct NestStage {
+  uint2 run[2][kNfRuns];
+  uint16_t grun[2][kNfGroups];
+  uint32_t wmax[2][2][4];
+  uint32_t cnt[2][4];
+};
+
+// Both streams of the thread's four groups expanded: lw[0] repetition, lw[1] definition levels
+// (bytes), eqd[q] the groups' definition == max_def masks; the u8 level arrays the chunk has are
+// written and the pages' counts (records, non-null values) added once per tile.
+DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, const NestFill &x, NestStage &T,
+                     uint32_t tid, uint64_t (&lw)[2][4], uint32_t (&eqd)[4], uint32_t &end_d) {
+  const uint32_t lane = lane_id(), wv = tid >> 6;
+  LfStream S[2];
+  S[0] = lf_stream(b, pd, cd, x, 0, T.run[0], tid);
+  S[1] = lf_stream(b, pd, cd, x, 1, T.run[1], tid);
+  end_d = S[1].end;
+  reinterpret_cast<uint2 *>(T.grun[0])[tid] = make_uint2(0, 0);
+  reinterpret_cast<uint2 *>(T.grun[1])[tid] = make_uint2(0, 0);
+  wg_barrier();
+  // run r > 0 starts in group ceil((x_r - t0) / 8) at the latest: the groups from there on begin in
+  // it or later; of the runs that mark one group the last one writes (no atomics)
 #pragma unroll
-      for (uint32_t j = 0; j < kNestCnt; j++)
-        if (j <= R) c[j] += in && nest_flag(cd, j, r, d);
+  for (uint32_t w = 0; w < 2; w++)
+    if (S[w].staged)
+      for (uint32_t r = 1 + tid; r < S[w].m; r += 256) {
+        const int64_t gs = ((int64_t)T.run[w][r].x - x.t0 + 7) >> 3;
+        const int64_t gn = r + 1 < S[w].m ? ((int64_t)T.run[w][r + 1].x - x.t0 + 7) >> 3 : (int64_t)kNfGroups;
+        if (gs > 0 && gs < (int64_t)kNfGroups && gn != gs) T.grun[w][gs] = (uint16_t)r;
+      }
+  wg_barrier();
+  // prefix maximum in group order: the thread's groups 2 tid, 2 tid + 1 (first half), 512 + 2 tid, + 1
+  uint32_t e[2][4], ex[2][2];
+#pragma unroll
+  for (uint32_t w = 0; w < 2; w++) {
+    const uint32_t p0 = reinterpret_cast<const uint32_t *>(T.grun[w])[tid];
+    const uint32_t p1 = reinterpret_cast<const uint32_t *>(T.grun[w] + kNfGroups / 2)[tid];
+    e[w][0] = p0 & 0xffffu; e[w][1] = max(p0 & 0xffffu, p0 >> 16); e[w][2] = p1 & 0xffffu; e[w][3] = max(p1 & 0xffffu, p1 >> 16);
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t incl = wave_incl_max(e[w][2 * h + 1], lane);
+      const uint32_t prev = __shfl_up(incl, 1);
+      ex[w][h] = lane ? prev : 0u;
+      if (lane == 63) T.wmax[w][h][wv] = incl;
+    }
+  }
+  wg_barrier();
+#pragma unroll
+  for (uint32_t w = 0; w < 2; w++) {
+    uint32_t before0 = 0, before1 = 0, tot0 = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      tot0 = max(tot0, T.wmax[w][0][q]);
+      if (q < wv) { before0 = max(before0, T.wmax[w][0][q]); before1 = max(before1, T.wmax[w][1][q]); }
+    }
+    const uint32_t c0 = max(before0, ex[w][0]), c1 = max(tot0, max(before1, ex[w][1]));
+    e[w][0] = max(e[w][0], c0); e[w][1] = max(e[w][1], c0);
+    e[w][2] = max(e[w][2], c1); e[w][3] = max(e[w][3], c1);
+  }
+  uint32_t nc[2] = {0, 0};
+#pragma unroll
+  for (uint32_t w = 0; w < 2; w++) {
+    const LfStream &Sw = S[w];
+    uint8_t *out = gp_u64<uint8_t>(w ? cd.def_levels : cd.rep_levels);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const int64_t g = nest_group(x, tid, q);
+      uint64_t word = 0;
+      uint32_t eq = 0;
+      const uint32_t vs = (uint32_t)max(g, (int64_t)x.lo), ve = (uint32_t)max(min(g + 8, (int64_t)Sw.end), (int64_t)vs);
+      if (Sw.on && !PQ_ABLATE(b, 18)) {
+        if (Sw.staged)
+          lf_group_from([&](uint32_t i) { return T.run[w][i]; }, Sw.m, e[w][q], Sw.src, Sw.n, Sw.bw, Sw.cmp, g, vs, ve, word, eq);
+        else
+          lf_group([&](uint32_t i) { return Sw.runs[i]; }, Sw.m, Sw.src, Sw.n, Sw.bw, Sw.cmp, g, vs, ve, word, eq);
+      }
+      lw[w][q] = word;
+      if (w) eqd[q] = eq;
+      nc[w] += __popc(eq);
+      if (out && vs < ve) {
+        uint8_t *o = out + x.sbase;
+        if (vs == g && ve == g + 8 && !(reinterpret_cast<uintptr_t>(o + g) & 7))
+          *reinterpret_cast<uint2 *>(o + g) = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
+        else
+          for (uint32_t v = vs; v < ve; v++) o[v] = (uint8_t)(word >> (8 * (v - (uint32_t)g)));
+      }
     }
   }
 #pragma unroll
-  for (uint32_t j = 0; j < kNestCnt; j++) {
-    const uint32_t v = (uint32_t)wave_sum64(c[j]);
-    if (lane == 0) part[j][wv] = v;
+  for (uint32_t w = 0; w < 2; w++) {  // page counts: one atomic per tile and stream
+    const uint32_t wc = (uint32_t)wave_sum64(nc[w]);
+    if (lane == 0) T.cnt[w][wv] = wc;
   }
-  wg_barrier();
-  if (threadIdx.x < kNestCnt)
-    b.nest_cnt[(uint64_t)t * kNestCnt + threadIdx.x] =
-        part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+  wg_barrier();  // cnt complete
+  if (tid < 2 && (tid ? S[1].on : S[0].on)) {
+    const uint32_t c = T.cnt[tid][0] + T.cnt[tid][1] + T.cnt[tid][2] + T.cnt[tid][3];
+    if (c) atomicAdd(tid ? &b.page_nn[x.pi] : &b.page_rec[x.pi], c);
+  }
 }
 
-// One 256-thread workgroup per chunk: thread i takes a contiguous run of the chunk's tiles, sums
-// its counters, one workgroup scan per counter gives the run's bases, and a second pass over the
-// run writes every tile's base (a chunk of 4 M records has ~5,000 tiles: a serial scan of them
-// cost ~0.5 ms).
+// Nibble packing of a slot's (rep, def) levels (rep_bw + def_bw <= 4): the low nibbles of the
+// eight bytes of x to 32 bits, and back.
+DEV uint32_t nib_pack(uint64_t x) {
+  x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+  x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+  return (uint32_t)(x | (x >> 16));
+}
+DEV uint64_t nib_unpack(uint32_t v) {
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+  x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+  return (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+}
+
+// Pass 1 over the nested chunks' fill tiles: both level streams expanded (the u8 level arrays,
+// the slot validity and the pages' record / non-null counts written from registers), the tile's
+// levels packed for pass 2 (nest_pk: per thread and half, sixteen (rep, def) pairs as nibbles in
+// one u64, or as two byte words each when the widths exceed a nibble), and per 4,096-slot half
+// how many entries of each counter (lists of levels 1..R starting, then leaf elements), stored at
+// the tile's position in the launch list (every half is written: no zeroing). Eight levels per
+// 64-bit word are compared at once (SWAR: levels below 128; wider levels take the byte loop); the
+// counters ride in 5-bit fields (at most 16 slots per thread and half).
+struct NestCountLDS {
+  NestStage st;
+  uint32_t vb[kLfTile / 32];  // slot validity of the tile (16 bits per thread and half)
+  uint32_t part[2][kNestCnt][4];
+};
+__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_t *lv_tiles, const uint32_t *tiles) {
+  const BatchDev b = global_view(b_in);
+  __shared__ NestCountLDS L;
+  const uint32_t pos = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const NestFill x = nest_fill(b, lv_tiles, tiles[pos]);
+  const PageDesc &pd = b.pages[x.pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t R = cd.nest;
+  uint64_t lw[2][4];
+  uint32_t eqd[4], end_d = 0;
+  nest_expand(b, pd, cd, x, L.st, tid, lw, eqd, end_d);
+  // slot validity (definition level == max_def) of the definition stream's covered values
+  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  if (vbits && x.lo < end_d) {  // workgroup-uniform
+    reinterpret_cast<uint16_t *>(L.vb)[tid] = (uint16_t)(eqd[0] | (eqd[1] << 8));
+    reinterpret_cast<uint16_t *>(L.vb)[256 + tid] = (uint16_t)(eqd[2] | (eqd[3] << 8));
+  }
+  // the levels for k_nest_emit
+  uint64_t *pk = b.nest_pk + (uint64_t)pos * kNestPkWords;
+  if (!cd.nest_pkb) {
+    const uint32_t sr = (uint32_t)cd.rep_bw;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t lo = nib_pack(lw[0][2 * h] | (lw[1][2 * h] << sr));
+      const uint32_t hi = nib_pack(lw[0][2 * h + 1] | (lw[1][2 * h + 1] << sr));
+      pk[h * 256 + tid] = ((uint64_t)hi << 32) | lo;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      uint4 *q = reinterpret_cast<uint4 *>(pk) + 2 * (h * 256 + tid);
+      q[0] = make_uint4((uint32_t)lw[0][2 * h], (uint32_t)(lw[0][2 * h] >> 32), (uint32_t)lw[0][2 * h + 1], (uint32_t)(lw[0][2 * h + 1] >> 32));
+      q[1] = make_uint4((uint32_t)lw[1][2 * h], (uint32_t)(lw[1][2 * h] >> 32), (uint32_t)lw[1][2 * h + 1], (uint32_t)(lw[1][2 * h + 1] >> 32));
+    }
+  }
+  constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
+  auto ge = [&](uint64_t v, uint32_t t) -> uint64_t { return ((v | H) - L1 * t) & H; };  // bytes v >= t
+  const bool swar = cd.max_def < 128;
+  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
+  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
+  uint64_t pa = 0, pb = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t vm = nest_inmask(nest_group(x, tid, q), 8, x.lo, endc);
+    const uint64_t rwq = lw[0][q], dwq = lw[1][q];
+    uint64_t acc = 0;
+    if (swar) {
+      const uint64_t mb = ((((uint64_t)vm * L1) & 0x8040201008040201ull) + 0x7f7f7f7f7f7f7f7full) & H;  // covered slots
+      for (uint32_t j = 0; j <= R; j++) {
+        const uint64_t th = j ? cd.list_def[j - 1] : 0u;
+        const uint64_t f = j < R ? ge(dwq, (uint32_t)th) & ~ge(rwq, j + 1) : ge(dwq, cd.list_def[R - 1]);
+        acc += (uint64_t)__popcll(f & mb) << (5 * j);
+      }
+    } else {
+#pragma unroll 1
+      for (uint32_t i = 0; i < 8; i++) {
+        if (!((vm >> i) & 1u)) continue;
+        const uint32_t r = (uint32_t)(rwq >> (8 * i)) & 0xffu, d = (uint32_t)(dwq >> (8 * i)) & 0xffu;
+        for (uint32_t j = 0; j <= R; j++) acc += (uint64_t)nest_flag(cd, j, r, d) << (5 * j);
+      }
+    }
+    if (q < 2) pa += acc; else pb += acc;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kNestCnt; j++) {
+    const uint32_t a2 = (uint32_t)wave_sum64((pa >> (5 * j)) & 31u), b2 = (uint32_t)wave_sum64((pb >> (5 * j)) & 31u);
+    if (lane == 0) { L.part[0][j][wv] = a2; L.part[1][j][wv] = b2; }
+  }
+  wg_barrier();
+  if (tid < 2 * kNestCnt) {
+    const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
+    b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j] = L.part[h][j][0] + L.part[h][j][1] + L.part[h][j][2] + L.part[h][j][3];
+  }
+  if (vbits && x.lo < end_d) {
+    const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
+    const int64_t w0 = x.t0 + 32 * (int64_t)w;
+    if (w0 + 32 > (int64_t)x.lo && w0 < (int64_t)end_d) {
+      const uint32_t v = L.vb[w];
+      uint32_t *dst = vbits + ((x.sbase + (uint64_t)w0) >> 5);
+      if (w0 >= (int64_t)x.lo && w0 + 32 <= (int64_t)end_d) *dst = v;  // the tile owns the whole word
+      else if (v) atomicOr(dst, v);                                     // shared with a neighbouring page
+    }
+  }
+}
+
+// One 256-thread workgroup per chunk: thread i takes a contiguous run of the chunk's counting
+// units (two per fill tile), sums its counters, one workgroup scan per counter gives the run's
+// bases, and a second pass over the run writes every unit's base. The chunk's totals close every
+// level's offsets and the record offsets.
 __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t *chunks) {
   const BatchDev b = global_view(b_in);
   __shared__ uint64_t wsum[4];
   const uint32_t c = chunks[blockIdx.x];
   const ChunkDesc &cd = b.chunks[c];
-  const uint32_t nt = (uint32_t)((cd.num_slots + kNestTile - 1) / kNestTile);
+  const uint32_t nt = 2 * cd.nest_ntiles;
   const uint32_t per = (nt + blockDim.x - 1) / blockDim.x;
   const uint32_t k0 = min(nt, threadIdx.x * per), k1 = min(nt, k0 + per);
-  const uint32_t *cnt = b.nest_cnt + (uint64_t)cd.nest_tile0 * kNestCnt;
-  uint64_t *base = b.nest_base + (uint64_t)cd.nest_tile0 * kNestCnt;
-  uint64_t acc[kNestCnt];
+  const uint32_t *cnt = b.nest_cnt + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
+  uint64_t *base = b.nest_base + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
+  uint64_t acc[kNestCnt], tot[kNestCnt];
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) acc[j] = 0;
   for (uint32_t k = k0; k < k1; k++)
@@ -122,9 +362,8 @@ __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t
     for (uint32_t j = 0; j < kNestCnt; j++) acc[j] += cnt[(uint64_t)k * kNestCnt + j];
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) {
-    uint64_t tot;
-    acc[j] = block_excl_scan64(acc[j], wsum, &tot);
-    if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot;
+    acc[j] = block_excl_scan64(acc[j], wsum, &tot[j]);
+    if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot[j];
   }
   for (uint32_t k = k0; k < k1; k++)
 #pragma unroll
@@ -132,6 +371,12 @@ __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t
       base[(uint64_t)k * kNestCnt + j] = acc[j];
       acc[j] += cnt[(uint64_t)k * kNestCnt + j];
     }
+  // closing entries: offsets[num_lists] = the next level's entries (elements), records -> slots
+  int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
+#pragma unroll
+  for (uint32_t j = 0; j + 1 < kNestCnt; j++)
+    if (threadIdx.x == j && j < cd.nest) gp_u64<int32_t>(cd.lvl_offsets[j])[tot[j]] = (int32_t)tot[j + 1];
+  if (threadIdx.x == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
 }
 
 // Bits of x at the positions set in m, packed towards bit 0 (Hacker's Delight 7-4, compress).
@@ -172,153 +417,154 @@ DEV void nest_put_bits(uint32_t *bm, uint64_t off, const uint32_t *row, uint32_t
   }
 }
 
-// Per tile: wave w owns 1,024 consecutive slots, lane i sixteen of them (one 16-byte load per
-// level array). Per counter j a lane holds the 16-bit mask of its flagged slots; wave prefix
-// sums of their counts (and one workgroup exchange of the wave totals) give every entry its
-// index. List offsets (the child counter's index at the list's first slot) and record offsets
-// (counter 0: a level-1 list starts at rep == 0, ColumnStore.get's record split) are staged in a
-// per-wave LDS row in entry order and leave as contiguous stores; the entries' validity bits are
-// compressed out of the lane's slot mask, placed at their index in a per-wave LDS bit row and
-// written with a funnel shift to their place in the bitmap.
+// Pass 2: per fill tile and 4,096-slot half, from the levels k_nest_count packed: wave w owns
+// 1,024 consecutive slots, lane i sixteen of them. Per counter j a lane holds the 16-bit mask of
+// its flagged slots; wave prefix sums of their counts (and one workgroup exchange of the wave
+// totals) give every entry its index. List offsets (the child counter's index at the list's first
+// slot) and record offsets (counter 0: a level-1 list starts at rep == 0, ColumnStore.get's record
+// split) are staged in a per-wave LDS row in entry order and leave as contiguous stores; the
+// entries' validity bits are compressed out of the lane's slot mask, placed at their index in a
+// per-wave LDS bit row and written with a funnel shift to their place in the bitmap.
 // R: the chunks' list levels (the launch covers the tiles of chunks with nest == R, so every
 // per-counter array is indexed by compile-time constants and stays in registers).
 template <uint32_t R>
-__global__ void __launch_bounds__(256) k_nest_emit(BatchDev b_in, const uint32_t *tile_chunk, uint32_t first) {
+struct NestEmitLDS {
+  uint32_t ent[4][kNestWaveSlots];  // per-wave entry rows
+  uint32_t wtot[2][R + 1][4];
+  uint32_t brow[4][kNestWaveSlots / 32 + 1];
+};
+template <uint32_t R>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 6 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint32_t *lv_tiles, const uint32_t *tiles,
+                                                   uint32_t first) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
-  const uint32_t t = first + blockIdx.x;
-  const NestTile x = nest_tile(b, tile_chunk, t);
-  const ChunkDesc &cd = *x.cd;
-  const uint8_t *rl = gp_u64<const uint8_t>(cd.rep_levels);
-  const uint8_t *dl = gp_u64<const uint8_t>(cd.def_levels);
-  const uint32_t *vb = gp_u64<const uint32_t>(cd.validity);
+  __shared__ NestEmitLDS<R> L;
+  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const NestFill x = nest_fill(b, lv_tiles, tiles[pos]);
+  const PageDesc &pd = b.pages[x.pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
   int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
   const uint32_t maxd = (uint32_t)cd.max_def;
-  __shared__ uint32_t wtot[C][4];
-  __shared__ uint32_t ent[4][kNestWaveSlots];
-  __shared__ uint32_t brow[4][kNestWaveSlots / 32 + 1];
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint64_t s = x.s0 + (uint64_t)wv * kNestWaveSlots + 16 * (uint64_t)lane;
-  const uint32_t ns = s < x.s1 ? (uint32_t)min((uint64_t)16, x.s1 - s) : 0u;
-  uint4 rv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
-  uint32_t vbits = 0;
-  if (ns) {
-    rv = *reinterpret_cast<const uint4 *>(rl + s);
-    if (dl) dv = *reinterpret_cast<const uint4 *>(dl + s);
-    else if (vb) vbits = vb[s >> 5] >> (s & 31);  // max_def == 1: the bit is the level
-  }
-  // the lane's flag and validity masks per counter
-  uint32_t f[C], vm[C];
+  const uint64_t *pk = b.nest_pk + (uint64_t)pos * kNestPkWords;
+  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
+  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
+  uint32_t *row = L.ent[wv];
+  uint32_t *bits = L.brow[wv];
+#pragma unroll 1
+  for (uint32_t h = 0; h < 2; h++) {
+    const int64_t g = nest_group(x, tid, 2 * h);
+    const uint32_t inm = nest_inmask(g, 16, x.lo, endc);
+    const uint64_t s = (uint64_t)((int64_t)x.sbase + g);  // the chunk slot of the lane's first slot
+    // the lane's levels (bytes) of its two groups: repetition r0, r1, definition d0, d1
+    uint64_t r0, r1, d0, d1;
+    if (!cd.nest_pkb) {
+      const uint32_t sr = (uint32_t)cd.rep_bw;
+      const uint64_t mr = 0x0101010101010101ull * ((1u << sr) - 1u), md = 0x0101010101010101ull * (0xfu >> sr);
+      const uint64_t v = pk[h * 256 + tid];
+      const uint64_t a0 = nib_unpack((uint32_t)v), a1 = nib_unpack((uint32_t)(v >> 32));
+      r0 = a0 & mr; d0 = (a0 >> sr) & md; r1 = a1 & mr; d1 = (a1 >> sr) & md;
+    } else {
+      const uint4 *q = reinterpret_cast<const uint4 *>(pk) + 2 * (h * 256 + tid);
+      const uint4 u = q[0], v = q[1];
+      r0 = ((uint64_t)u.y << 32) | u.x; r1 = ((uint64_t)u.w << 32) | u.z;
+      d0 = ((uint64_t)v.y << 32) | v.x; d1 = ((uint64_t)v.w << 32) | v.z;
+    }
+    // the lane's flag and validity masks per counter
+    uint32_t f[C], vm[C];
 #pragma unroll
-  for (uint32_t j = 0; j < C; j++) f[j] = vm[j] = 0;
-  {
-    const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
+    for (uint32_t j = 0; j < C; j++) f[j] = vm[j] = 0;
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-      const uint32_t r = (rw[q >> 2] >> (8 * (q & 3))) & 0xffu;
-      const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
-      const uint32_t in = q < ns ? 1u : 0u;
+      const uint32_t r = (uint32_t)((q < 8 ? r0 : r1) >> (8 * (q & 7))) & 0xffu;
+      const uint32_t d = (uint32_t)((q < 8 ? d0 : d1) >> (8 * (q & 7))) & 0xffu;
+      const uint32_t in = (inm >> q) & 1u;
 #pragma unroll
       for (uint32_t j = 0; j < C; j++) {
         f[j] |= (in & (uint32_t)nest_flag(cd, j, r, d)) << q;
         vm[j] |= (uint32_t)(j < R ? d >= cd.list_null_def[j] : d == maxd) << q;
       }
     }
-  }
-  // entry indices: wave prefix sums, then the waves before this one in the tile
-  uint32_t P[C], T[C];
+    // entry indices: wave prefix sums, then the waves before this one in the half
+    uint32_t P[C], T[C];
 #pragma unroll
-  for (uint32_t j = 0; j < C; j++) {
-    const uint32_t c = (uint32_t)__popc(f[j]);
-    const uint32_t incl = (uint32_t)wave_incl_scan64_dpp(c);
-    P[j] = incl - c;
-    T[j] = (uint32_t)__shfl(incl, 63);
-    if (lane == 0) wtot[j][wv] = T[j];
-  }
-  wg_barrier();
-  uint64_t run[C];
-#pragma unroll
-  for (uint32_t j = 0; j < C; j++) {
-    uint64_t v = b.nest_base[(uint64_t)t * kNestCnt + j];
-    for (uint32_t q = 0; q < wv; q++) v += wtot[j][q];
-    run[j] = v;
-  }
-  uint32_t *row = ent[wv];
-  // list offsets of each level, then the record offsets (level-1 list starts)
-#pragma unroll
-  for (uint32_t j = 0; j <= R; j++) {
-    const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
-    if (j == R && !rec) break;
-    if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
-    uint32_t m = f[lv], k = P[lv];
-    const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
-    while (m) {
-      const uint32_t i = __builtin_ctz(m);
-      m &= m - 1;
-      row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
+    for (uint32_t j = 0; j < C; j++) {
+      const uint32_t c = (uint32_t)__popc(f[j]);
+      const uint32_t incl = (uint32_t)wave_incl_scan64_dpp(c);
+      P[j] = incl - c;
+      T[j] = (uint32_t)__shfl(incl, 63);
+      if (lane == 0) L.wtot[h][j][wv] = T[j];
     }
-    wave_lds_sync();
-    int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
-    for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
-    wave_lds_sync();
-  }
-  // validity bits of every counter's entries
-  uint32_t *bits = brow[wv];
+    wg_barrier();  // wtot[h] complete (double-buffered: no barrier before the next half's stores)
+    uint64_t run[C];
 #pragma unroll
-  for (uint32_t j = 0; j < C; j++) {
-    if (PQ_ABLATE(b, 17)) break;  // diagnostic bit 17: no bitmaps
-    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
-    wave_lds_sync();
-    const uint32_t c = (uint32_t)__popc(f[j]);
-    if (c) {
-      const uint32_t comp = compress32(vm[j], f[j]), p = P[j], sh = p & 31;
-      atomicOr(&bits[p >> 5], comp << sh);
-      if (sh && sh + c > 32) atomicOr(&bits[(p >> 5) + 1], comp >> (32 - sh));
+    for (uint32_t j = 0; j < C; j++) {
+      uint64_t v = b.nest_base[(2 * (uint64_t)pos + h) * kNestCnt + j];
+      for (uint32_t q = 0; q < wv; q++) v += L.wtot[h][j][q];
+      run[j] = v;
     }
-    wave_lds_sync();
-    nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
-    wave_lds_sync();
-  }
-  // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
-  // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
-  // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
-  // bits go where that counter's validity goes
-  for (uint32_t g = 0; g < cd.ngroups; g++) {
-    uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[g]);
-    if (!gv) continue;  // shares list / element validity (workgroup-uniform)
-    const uint32_t j = cd.group_depth[g], dg = cd.group_def[g];
-    uint32_t fj = 0, pj = 0, tj = 0;
-    uint64_t rj = 0;
+    // list offsets of each level, then the record offsets (level-1 list starts)
 #pragma unroll
-    for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
-      if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
-    uint32_t vg = 0;
-    {
-      const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
-#pragma unroll
-      for (uint32_t q = 0; q < 16; q++) {
-        const uint32_t d = dl ? (dw[q >> 2] >> (8 * (q & 3))) & 0xffu : (vbits >> q) & 1u;
-        vg |= (uint32_t)(d >= dg) << q;
+    for (uint32_t j = 0; j <= R; j++) {
+      const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
+      if (j == R && !rec) break;
+      if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
+      uint32_t m = f[lv], k = P[lv];
+      const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
+      while (m) {
+        const uint32_t i = __builtin_ctz(m);
+        m &= m - 1;
+        row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
       }
+      wave_lds_sync();
+      int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
+      for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
+      wave_lds_sync();
     }
-    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
-    wave_lds_sync();
-    const uint32_t c = (uint32_t)__popc(fj);
-    if (c) {
-      const uint32_t comp = compress32(vg, fj), sh = pj & 31;
-      atomicOr(&bits[pj >> 5], comp << sh);
-      if (sh && sh + c > 32) atomicOr(&bits[(pj >> 5) + 1], comp >> (32 - sh));
+    // validity bits of every counter's entries
+#pragma unroll
+    for (uint32_t j = 0; j < C; j++) {
+      if (PQ_ABLATE(b, 17)) break;  // diagnostic bit 17: no bitmaps
+      if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+      wave_lds_sync();
+      const uint32_t c = (uint32_t)__popc(f[j]);
+      if (c) {
+        const uint32_t comp = compress32(vm[j], f[j]), p = P[j], sh = p & 31;
+        atomicOr(&bits[p >> 5], comp << sh);
+        if (sh && sh + c > 32) atomicOr(&bits[(p >> 5) + 1], comp >> (32 - sh));
+      }
+      wave_lds_sync();
+      nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
+      wave_lds_sync();
     }
-    wave_lds_sync();
-    nest_put_bits(gv, rj, bits, tj, lane);
-    wave_lds_sync();
-  }
-  // the chunk's last tile closes every level's offsets and the record offsets
-  const uint32_t nt = (uint32_t)((cd.num_slots + kNestTile - 1) / kNestTile);
-  if (x.local == nt - 1 && threadIdx.x < R) {
-    const uint64_t *tot = b.nest_tot + (uint64_t)x.chunk * kNestCnt;
-    gp_u64<int32_t>(cd.lvl_offsets[threadIdx.x])[tot[threadIdx.x]] = (int32_t)tot[threadIdx.x + 1];
-    if (threadIdx.x == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
+    // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
+    // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
+    // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
+    // bits go where that counter's validity goes
+    for (uint32_t gi = 0; gi < cd.ngroups; gi++) {
+      uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[gi]);
+      if (!gv) continue;  // shares list / element validity (workgroup-uniform)
+      const uint32_t j = cd.group_depth[gi], dg = cd.group_def[gi];
+      uint32_t fj = 0, pj = 0, tj = 0;
+      uint64_t rj = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
+        if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
+      uint32_t vg = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++)
+        vg |= (uint32_t)(((uint32_t)((q < 8 ? d0 : d1) >> (8 * (q & 7))) & 0xffu) >= dg) << q;
+      if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+      wave_lds_sync();
+      const uint32_t c = (uint32_t)__popc(fj);
+      if (c) {
+        const uint32_t comp = compress32(vg, fj), sh = pj & 31;
+        atomicOr(&bits[pj >> 5], comp << sh);
+        if (sh && sh + c > 32) atomicOr(&bits[(pj >> 5) + 1], comp >> (32 - sh));
+      }
+      wave_lds_sync();
+      nest_put_bits(gv, rj, bits, tj, lane);
+      wave_lds_sync();
+    }
   }
 }
 
@@ -378,7 +624,7 @@ hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_
 
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_count, dim3(l.n_nest_tiles), dim3(256), 0, s, b, l.nest_tiles);
+  hipLaunchKernelGGL(k_nest_count, dim3(l.n_nest_tiles), dim3(256), 0, s, b, l.lv_tiles, l.nest_tiles);
   return hipGetLastError();
 }
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
@@ -389,7 +635,7 @@ hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t
 template <uint32_t R>
 static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.nest_tiles, l.nest_first[R]);
+  if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.lv_tiles, l.nest_tiles, l.nest_first[R]);
 }
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;

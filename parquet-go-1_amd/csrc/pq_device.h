@@ -119,7 +119,9 @@ struct ChunkDesc {       // 192 B
                                  // [u32 length | bytes] (4, 5 or 6; 0: entries over 60 bytes, no table)
   uint64_t dict_slots;           // device address of the slot table (k_dict_slots, every decode)
   // nested (Arrow-style) output, max_rep > 0: nest = number of list levels (0: not produced)
-  uint32_t nest, nest_tile0;      // list levels; first k_nest tile of the chunk
+  uint32_t nest, nest_tile0;      // list levels; the chunk's first entry of the nested tile list
+  uint32_t nest_ntiles;           // the chunk's fill tiles (nested.hip: two counting units each)
+  uint32_t nest_pkb;              // packed levels: 0 a nibble per slot (rep_bw + def_bw <= 4), 1 two bytes
   uint8_t list_null_def[8], list_def[8];  // per REPEATED node: non-null from / has an element from
   uint64_t lvl_offsets[8];       // int32[num_lists + 1] per level
   uint64_t lvl_validity[8];      // uint32 bitmap per level

@@ -167,8 +167,7 @@ def test_oracle_generic_streams(files):
 def test_gpu_generic_streams(gpu_ctx, files, monkeypatch, kernel):
     import pqgpu
     import test_gpu_parity as P
-    if kernel == "ranking":
-        monkeypatch.setenv("PQ_LV_SEG", "0")
+    monkeypatch.setenv("PQ_LV_SEGW", "1" if kernel == "seg" else "0")
     for name, data in files.items():
         gpu = P._gpu_decode(gpu_ctx, data)
         for rg, col, r in pqtest.oracle_decode(data):
