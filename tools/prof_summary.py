@@ -14,6 +14,13 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+SLOT_KERNELS = {  # bench / library timer slot -> the kernels it brackets
+    "k_ba_emit": ["k_ba_emit", "k_ba_emit_slots", "k_ba_emit_slots64", "k_ba_emit_lds"],
+    "k_levels": ["k_levels", "k_levels_bw1", "k_levels_seg", "k_levels_segw", "k_levels_bw1w", "k_levels_w"],
+    "k_values_delta": ["k_values_delta", "k_values_delta_ld"],
+}
+
+
 def short(name):
     n = name.split("(")[0].split("<")[0]
     for p in ("pq::", "void "):
@@ -69,9 +76,36 @@ def main(cfg, rnd="r02"):
             r["stall_frac"] = {"wait_any": round(r.get("SQ_WAIT_ANY", 0) / w, 3),
                                "wait_inst_any": round(r.get("SQ_WAIT_INST_ANY", 0) / w, 3),
                                "active_inst_any": round(r.get("SQ_ACTIVE_INST_ANY", 0) / w, 3)}
+    # the stats pass's own bench line: its roofline kernel's live HIP-event mean against the trace
+    line, check = None, None
+    log = os.path.join(src, "stats.log")
+    if os.path.exists(log):
+        for ln in open(log):
+            if ln.startswith("{") and '"roofline"' in ln:
+                line = json.loads(ln)
+    if line:
+        rf = line["roofline"]
+        k = rf["kernel"]
+        # a timer slot may cover several kernels launched one after the other on its stream
+        ks = [x for x in SLOT_KERNELS.get(k, [k]) if x in res and "trace_avg_us" in res[x]]
+        steps = line["warmup"] + line["steps"] + max(line["steps"], 20)  # + bench.kernel_means' steps
+        if ks:
+            tot_us = sum(res[x]["trace_avg_us"] * res[x]["trace_dispatches"] for x in ks)
+            tr_ms = tot_us / 1e3 / steps
+            frac_tr = rf["bytes_per_launch"] * rf.get("launches_per_step", 1) / (tr_ms / 1e3) / 1e9 / rf["peak"]
+            check = {"kernel": k, "trace_kernels": ks, "line_kernel_ms": rf["kernel_ms"], "line_frac": rf["frac"],
+                     "trace_ms_per_step": round(tr_ms, 4), "trace_frac": round(frac_tr, 4),
+                     "line_over_trace": round(rf["kernel_ms"] / tr_ms, 4),
+                     "note": f"trace: the kernels' summed durations over every step of the command ({steps}: "
+                             "warm-up, timed and bench.kernel_means' steps)"}
+    stats = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        import shutil
+        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{rnd}_{cfg}_kernel_stats.csv"))
     out = {"source": "tools/prof.sh (rocprofv3: kernel trace; --pmc FETCH_SIZE, WRITE_SIZE and 8 SQ counters, "
                      "separate passes)", "config": cfg,
-           "command": f"python3 bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu-baseline --no-e2e",
+           "command": f"python3 bench.py --config {cfg} --steps 20 --warmup 3 --no-cpu-baseline --no-e2e",
+           "bench_line": line, "line_vs_trace": check,
            "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads, MI355X_MICROARCH.md HBM section)",
            "kernels": res}
     path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{cfg}.json")
