@@ -81,7 +81,7 @@ DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
 // workgroup-uniform).
 template <uint32_t NR>
 DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
-                        DictTileLDST<NR> &L, DictTile &t) {
+                        DictTileLDST<NR> &L, DictTile &t, uint32_t reserve = 0) {
   uint32_t r0 = 0, r1 = 0;
   if (!dict_tile_open(b, pd, page, v0, v1, nn, t, r0, r1)) return false;
   if (t.bw == 0) return true;
@@ -95,7 +95,7 @@ DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   const uintptr_t ga = ((uintptr_t)(t.s + lo)) & ~(uintptr_t)15;  // 16-B aligned global start
   const uint64_t sb = (uint64_t)(ga - (uintptr_t)t.s);             // its stream offset (may be "negative")
   const uint64_t span = hi > lo ? (hi + 8) - (lo & ~(uint64_t)15) + 16 : 0;
-  if (span <= kTileStageB) {
+  if (span + reserve <= kTileStageB) {  // reserve: bytes at the stage's end the caller keeps
     t.staged = true;
     t.sbit = sb * 8;
     const uint4 *src = (const uint4 *)gp_u64<const uint8_t>((uint64_t)ga);

@@ -481,7 +481,8 @@ struct pqgpu_batch {
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
   uint32_t n_delta_tiles = 0;
-  std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_tiles, nest_chunks;
+  std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_chunks;
+  std::vector<uint4> nest_tiles;  // nested fill tiles: {global fill tile, page, tile of the page, chunk}
   std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
   uint64_t l_grp_tiles = 0;
   uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, o_nest_pk = 0, l_nest_tiles = 0, l_nest_chunks = 0;
@@ -1383,7 +1384,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
         const uint64_t sb = b->pages[p].slot_base, ns = b->pages[p].num_slots;
         const uint64_t nt = ns ? (sb + ns - 1) / kLfTileHost - sb / kLfTileHost + 1 : 0;
-        for (uint64_t k = 0; k < nt; k++) b->nest_tiles.push_back(b->lv_tile0[p] + (uint32_t)k);
+        for (uint64_t k = 0; k < nt; k++) b->nest_tiles.push_back(make_uint4(b->lv_tile0[p] + (uint32_t)k, p, (uint32_t)k, c));
       }
       hc.nest_ntiles = (uint32_t)b->nest_tiles.size() - hc.nest_tile0;
     }
@@ -1596,7 +1597,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_base = take(b->base_chunks.size() * 4);
   b->l_ba = take(b->ba_chunks.size() * 4);
   b->l_rec = take(b->rec_pages.size() * 4);
-  b->l_nest_tiles = take(b->nest_tiles.size() * 4);
+  b->l_nest_tiles = take(b->nest_tiles.size() * 16);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
   b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 4);  // every entry written by k_nest_count
@@ -1788,7 +1789,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
-  HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 4), err);
+  HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 16), err);
   HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
   HIPCHECK(up(b->l_grp_tiles, b->grp_tiles.data(), b->grp_tiles.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
@@ -1899,7 +1900,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.slot_grid_x = b->slot_grid_x;
   l.rec_pages = (const uint32_t *)(A + b->l_rec);
   l.n_rec_pages = (uint32_t)b->rec_pages.size();
-  l.nest_tiles = (const uint32_t *)(A + b->l_nest_tiles);
+  l.nest_desc = (const uint4 *)(A + b->l_nest_tiles);
   l.n_nest_tiles = (uint32_t)b->nest_tiles.size();
   for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
   l.nest_chunks = (const uint32_t *)(A + b->l_nest_chunks);
@@ -1976,7 +1977,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   l2.n_items = l.n_items - b->n_delta_items - n_dict;
   // DELTA_BINARY_PACKED items (the first n_delta_items) go to k_values_delta on the DELTA stream,
   // beside the level kernels, the copies and the other values kinds; the default stream joins it
-  hipStream_t ds = b->one_stream ? s : b->ctx->delta;
+  // a batch without level streams and column groups keeps its DELTA pages on the batch stream: with
+  // nothing to overlap but the other values kinds they only compete with them (cfg5 6.19 -> 6.08 ms)
+  const bool lvl_any = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
+  hipStream_t ds = b->one_stream || (!lvl_any && b->n_groups == 0) ? s : b->ctx->delta;
   if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
   // streams with nothing to run are neither forked nor joined (a cross-stream wait costs latency)
   const bool any_delta = l1.n_items || l.n_delta_pages;

@@ -81,7 +81,8 @@ struct LaunchLists {
   const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
   uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
-  const uint32_t *nest_tiles; uint32_t n_nest_tiles;     // fill tiles of the nested chunks (k_nest_count / k_nest_emit)
+  const uint4 *nest_desc; uint32_t n_nest_tiles;         // fill tiles of the nested chunks (k_nest_count / k_nest_emit):
+                                                         // {global fill tile, page, tile of the page, chunk}
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
   const uint32_t *nest_chunks; uint32_t n_nest_chunks;
   const uint32_t *grp_tiles; uint32_t n_grp_tiles;       // chunk of every k_group_flat tile

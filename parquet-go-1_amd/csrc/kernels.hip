@@ -2402,16 +2402,26 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 #ifndef PQ_DICT_LDS
 #define PQ_DICT_LDS 1
 #endif
+constexpr uint32_t kDictEarly = 4096;  // dictionaries up to this many bytes are staged with the tile
 DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                  DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
   if (wi.v0 >= v1) return;
   DictTile t;
-  if (!dict_tile_load(b, pd, wi.page, wi.v0, v1, nn, lds, t)) return;
-  const uint64_t vb = b.page_vbase[wi.page];
   const bool is_bool = pd.vkind == VK_RLE_BOOL;
   const uint32_t w = (uint32_t)cd.value_width;
   const uint32_t dcount = cd.dict_count;
+  // a small dictionary (at most kDictEarly bytes) goes to the stage's end while the tile is staged,
+  // under the same barrier: no barrier pair after the index decode
+  const uint32_t dbytes = dcount * w;
+  const bool early = PQ_DICT_LDS && !is_bool && w == 4 && dbytes <= kDictEarly;  // workgroup-uniform
+  const uint32_t dword0 = (kTileStageB - kDictEarly) / 4;  // the dictionary's first stage word
+  if (early) {
+    const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
+    for (uint32_t k = threadIdx.x; k < dbytes / 4; k += blockDim.x) lds.stage[dword0 + k] = src[k];
+  }
+  if (!dict_tile_load(b, pd, wi.page, wi.v0, v1, nn, lds, t, early ? kDictEarly + 64 : 0)) return;
+  const uint64_t vb = b.page_vbase[wi.page];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values
   uint32_t first_err = 0xffffffffu;
@@ -2432,14 +2442,14 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
     // a dictionary that fits the stage is gathered from LDS: once every wave has its indices, the
     // stage's stream bytes are dead and the dictionary takes their place (PQ_DICT_LDS=0: global)
     const bool ldict = PQ_DICT_LDS && (uint64_t)dcount * w <= kTileStageB;  // workgroup-uniform
-    if (ldict) {
+    if (ldict && !early) {
       wg_barrier();  // every wave's reads of the staged stream are done
       const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
       for (uint32_t k = threadIdx.x; k < dcount * (w / 4); k += blockDim.x) lds.stage[k] = src[k];
       wg_barrier();
     }
     if (w == 4) {
-      const uint32_t *dv = ldict ? lds.stage : gp_u64<const uint32_t>(cd.dict_values);
+      const uint32_t *dv = early ? lds.stage + dword0 : ldict ? lds.stage : gp_u64<const uint32_t>(cd.dict_values);
       uint32_t *out = gp_u64<uint32_t>(cd.values) + vb + seg0 + lane;
       uint32_t val[16];
 #pragma unroll

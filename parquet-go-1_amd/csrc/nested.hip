@@ -40,21 +40,24 @@ constexpr uint32_t kNestHalf = 4096;               // slots per counting unit (h
 constexpr uint32_t kNestWaveSlots = kNestHalf / 4;  // a wave's slots of a half (16 per lane)
 static_assert(2 * kNestHalf == kLfTile, "a fill tile is two counting units");
 
-// The fill tile of nested tile `t` (global fill tile index; lv_tiles[t] = its page): the page's
-// slots [lo, hi) it covers, t0 = the page value index of its first (aligned) slot.
+// The fill tile of a nested tile descriptor (host-built, so the kernels start from one load:
+// {global fill tile t, page, tile k of the page, chunk}): the page's slots [lo, hi) it covers,
+// t0 = the page value index of its first (aligned) slot.
 struct NestFill {
-  uint32_t pi, k, lo, hi, ntiles;
+  uint32_t t, pi, k, chunk, lo, hi, ntiles;
   int64_t t0;
   uint64_t sbase;
 };
-DEV NestFill nest_fill(const BatchDev &b, const uint32_t *lv_tiles, uint32_t t) {
+DEV NestFill nest_fill(const BatchDev &b, uint4 d) {
   NestFill x;
-  x.pi = lv_tiles[t];
+  x.t = d.x;
+  x.pi = d.y;
+  x.k = d.z;
+  x.chunk = d.w;
   const PageDesc &pd = b.pages[x.pi];
   x.sbase = pd.slot_base;
   const uint32_t ns = pd.num_slots, a = (uint32_t)(x.sbase & (kLfTile - 1));
   x.ntiles = lf_tiles(x.sbase, ns);
-  x.k = t - b.lv_tile0[x.pi];
   x.t0 = (int64_t)x.k * kLfTile - a;
   x.lo = (uint32_t)max(x.t0, (int64_t)0);
   x.hi = (uint32_t)min(x.t0 + kLfTile, (int64_t)ns);
@@ -91,10 +94,10 @@ DEV LfStream lf_stream(const BatchDev &b, const PageDesc &pd, const ChunkDesc &c
     return S;
   }
   const uint2 *runs = b.lv_runs + b.lv_run_base[2 * x.pi + which];
-  const uint32_t *trun = b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[x.pi] + which;
-  const uint32_t r0 = trun[2 * x.k];
+  const uint32_t *trun = b.lv_tile_run + 2 * (uint64_t)x.t + which;
+  const uint32_t r0 = trun[0];
   const bool more = x.k + 1 < x.ntiles && x.t0 + (int64_t)kLfTile < (int64_t)cov;
-  S.m = (more ? trun[2 * (x.k + 1)] : nr - 1) - r0 + 1;
+  S.m = (more ? trun[2] : nr - 1) - r0 + 1;
   S.runs = runs + r0;
   S.staged = S.m <= kNfRuns;
   if (S.staged)
@@ -255,13 +258,13 @@ struct NestCountLDS {
   uint32_t vb[kLfTile / 32];  // slot validity of the tile (16 bits per thread and half)
   uint32_t part[2][kNestCnt][4];
 };
-__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint32_t *lv_tiles, const uint32_t *tiles) {
+__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *tiles) {
   const BatchDev b = global_view(b_in);
   __shared__ NestCountLDS L;
   const uint32_t pos = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const NestFill x = nest_fill(b, lv_tiles, tiles[pos]);
+  const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const PageDesc &pd = b.pages[x.pi];
-  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const ChunkDesc &cd = b.chunks[x.chunk];
   const uint32_t R = cd.nest;
   uint64_t lw[2][4];
   uint32_t eqd[4], end_d = 0;
@@ -354,23 +357,29 @@ __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t
   const uint32_t k0 = min(nt, threadIdx.x * per), k1 = min(nt, k0 + per);
   const uint32_t *cnt = b.nest_cnt + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
   uint64_t *base = b.nest_base + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
+  const uint32_t C = cd.nest + 1;  // counters in use (lists of levels 1..R, elements)
   uint64_t acc[kNestCnt], tot[kNestCnt];
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) acc[j] = 0;
   for (uint32_t k = k0; k < k1; k++)
 #pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++) acc[j] += cnt[(uint64_t)k * kNestCnt + j];
+    for (uint32_t j = 0; j < kNestCnt; j++)
+      if (j < C) acc[j] += cnt[(uint64_t)k * kNestCnt + j];
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) {
-    acc[j] = block_excl_scan64(acc[j], wsum, &tot[j]);
-    if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot[j];
+    tot[j] = 0;
+    if (j < C) {  // workgroup-uniform
+      acc[j] = block_excl_scan64(acc[j], wsum, &tot[j]);
+      if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot[j];
+    }
   }
   for (uint32_t k = k0; k < k1; k++)
 #pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++) {
-      base[(uint64_t)k * kNestCnt + j] = acc[j];
-      acc[j] += cnt[(uint64_t)k * kNestCnt + j];
-    }
+    for (uint32_t j = 0; j < kNestCnt; j++)
+      if (j < C) {
+        base[(uint64_t)k * kNestCnt + j] = acc[j];
+        acc[j] += cnt[(uint64_t)k * kNestCnt + j];
+      }
   // closing entries: offsets[num_lists] = the next level's entries (elements), records -> slots
   int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
 #pragma unroll
@@ -434,15 +443,14 @@ struct NestEmitLDS {
   uint32_t brow[4][kNestWaveSlots / 32 + 1];
 };
 template <uint32_t R>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 6 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint32_t *lv_tiles, const uint32_t *tiles,
-                                                   uint32_t first) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 6 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint4 *tiles, uint32_t first) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestEmitLDS<R> L;
   const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const NestFill x = nest_fill(b, lv_tiles, tiles[pos]);
+  const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const PageDesc &pd = b.pages[x.pi];
-  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const ChunkDesc &cd = b.chunks[x.chunk];
   int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
   const uint32_t maxd = (uint32_t)cd.max_def;
   const uint64_t *pk = b.nest_pk + (uint64_t)pos * kNestPkWords;
@@ -624,7 +632,7 @@ hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_
 
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_count, dim3(l.n_nest_tiles), dim3(256), 0, s, b, l.lv_tiles, l.nest_tiles);
+  hipLaunchKernelGGL(k_nest_count, dim3(l.n_nest_tiles), dim3(256), 0, s, b, l.nest_desc);
   return hipGetLastError();
 }
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
@@ -635,7 +643,7 @@ hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t
 template <uint32_t R>
 static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.lv_tiles, l.nest_tiles, l.nest_first[R]);
+  if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
 }
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;
