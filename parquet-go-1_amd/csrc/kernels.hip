@@ -3198,11 +3198,6 @@ DEV DeltaStream page_stream(const BatchDev &b, const WorkItem &wi, const PageDes
   return ds;
 }
 
-// LD (k_values_delta_ld, 320 threads): wave 4 is a loader that only loads the windows and writes them
-// to LDS; waves 0-3 decode and store. vmcnt counts stores and loads alike, so a wave that issues the
-// output stores and also waits for the next window's loads waits for its own stores too; with a
-// loader wave the decoding waves never wait on memory and the loader waits only for its loads.
-template <bool LD = false>
 DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, DeltaPageLDS &L) {
   if (nn == 0) return;
   const uint8_t *s = ds.s;
@@ -3210,9 +3205,8 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
   const bool is64 = ds.is64;
   const uint32_t mbc = ds.mbc, mbvc = ds.mbvc, bs = mbc * mbvc, g8 = mbvc / 8, gpb = bs / 8;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const bool loader = LD && wv == 4;  // (workgroup-uniform per wave)
-  constexpr uint32_t NL = LD ? 64 : 256;  // threads that load a window
-  const uint32_t lt = LD ? lane : tid;
+  constexpr uint32_t NL = 256;  // threads that load a window
+  const uint32_t lt = tid;
   uint32_t limit = nn;  // next() fails with io.EOF at positions >= the header's valuesCount
   bool final_eof = false;
   if ((uint32_t)max(ds.count, 0) < nn) { limit = (uint32_t)max(ds.count, 0); final_eof = true; }
@@ -3241,34 +3235,8 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
   PQ_STAMPS(st, b.dbg);
   st.begin();
   int32_t win0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
-  if (LD && loader) {
-    // the loader's own loop: the windows, and exactly the decoding waves' barriers (their count
-    // follows from the walk's block count, read from LDS), so its registers live apart from theirs
-    fetch(win0);
-    store();
-    wg_barrier();
-    while (blk < need) {
-      wg_barrier();  // the walk
-      const uint32_t nb = sgpr(L.nb);
-      hdr = sgpr(L.next);
-      const bool more = blk + nb < need && nb > 0;
-      const int32_t nwin0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
-      if (more) fetch(nwin0);  // lands during the parse and the batches
-      wg_barrier();  // the parse
-      const unsigned long long sk = sgpr64(L.stop);
-      for (uint32_t g0 = 0; g0 < nb * gpb; g0 += 256) wg_barrier();  // the batches
-      blk += nb;
-      if ((sk >> 4) < limit || !more) return;
-      win0 = nwin0;
-      store();
-      wg_barrier();
-    }
-    return;
-  }
-  if (!LD) {
-    fetch(win0);
-    store();
-  }
+  fetch(win0);
+  store();
   if (tid == 0) L.stop = ~0ull;
   wg_barrier();
   st.lap(0);
@@ -3334,7 +3302,7 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
     hdr = sgpr(L.next);
     const bool more = blk + nb < need && nb > 0;
     const int32_t nwin0 = (int32_t)hdr - (int32_t)(((uintptr_t)(s + hdr)) & 15u);
-    if (more && !LD) fetch(nwin0);  // lands during the parse and the batches
+    if (more) fetch(nwin0);  // lands during the parse and the batches
     // ---- 3. parse: thread k re-reads block k's header exactly, finds its first unreadable group
     if (tid < nb) {
       const uint32_t p = L.hpos[tid], j = blk + tid;
@@ -3497,7 +3465,7 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
     // ---- 2'. the prefetched window replaces the current one (every read of it is behind
     // the last batch's barrier, or the parse barrier when there was no batch)
     win0 = nwin0;
-    if (!LD) store();
+    store();
     wg_barrier();
     st.lap(0);
   }
@@ -3593,7 +3561,6 @@ union DeltaLDS {
 #ifndef PQ_DELTA_WPE
 #define PQ_DELTA_WPE 5
 #endif
-template <bool LD>
 DEV void values_delta(BatchDev b_in, const WorkItem *items, DeltaLDS &lds) {
   const BatchDev b = global_view(b_in);
   const WorkItem wi = items[blockIdx.x];
@@ -3602,20 +3569,15 @@ DEV void values_delta(BatchDev b_in, const WorkItem *items, DeltaLDS &lds) {
   const uint32_t nn = b.page_nn_v[wi.page];
   switch (wi.kind) {
     case WI_DELTA: do_delta_slow(b, page_stream(b, wi, pd, cd), nn); break;
-    case WI_DELTA_TILE: if (!LD) do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;  // (LD: none)
-    case WI_DELTA_PAGE: do_delta_page<LD>(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
+    case WI_DELTA_TILE: do_delta_tile(b, wi, pd, cd, nn, lds.dtile.scan, lds.dtile.stage); break;
+    case WI_DELTA_PAGE: do_delta_page(b, page_stream(b, wi, pd, cd), nn, lds.dpage); break;
     case WI_PLAIN: do_plain<PQ_FUSED_COPY_U>(b, wi, pd, cd, nn); break;  // fused copies (registers to spare: more in flight)
     case WI_BOOL: do_bool(b, wi, pd, cd, nn); break;
   }
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DELTA_WPE))) k_values_delta(BatchDev b_in, const WorkItem *items) {
   __shared__ DeltaLDS lds;
-  values_delta<false>(b_in, items, lds);
-}
-// The same with a loader wave (DELTA pages; no DELTA tiles in the launch): 320 threads
-__global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(PQ_DELTA_WPE))) k_values_delta_ld(BatchDev b_in, const WorkItem *items) {
-  __shared__ DeltaLDS lds;
-  values_delta<true>(b_in, items, lds);
+  values_delta(b_in, items, lds);
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_values(BatchDev b_in, const WorkItem *items) {
@@ -4347,11 +4309,8 @@ hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t
 }
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s, bool tiles) {
   if (!n) return hipSuccess;
-  // PQ_DELTA_LOADER=1: the 320-thread kernel with a loader wave (measured slower on cfg2: off)
-  const char *lde = getenv("PQ_DELTA_LOADER");
-  const bool ld = lde && atoi(lde) == 1;
-  if (ld && !tiles) hipLaunchKernelGGL(k_values_delta_ld, dim3(n), dim3(320), 0, s, b, items);
-  else hipLaunchKernelGGL(k_values_delta, dim3(n), dim3(256), 0, s, b, items);
+  (void)tiles;
+  hipLaunchKernelGGL(k_values_delta, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();
 }
 hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
