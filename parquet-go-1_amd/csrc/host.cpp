@@ -1965,8 +1965,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // per-decode state: two contiguous fills (validity bitmaps + counters; error keys + tile table).
   // page_nn of pages without level streams is constant and was uploaded with the descriptors.
   (void)np;
-  HIPCHECK(hipMemsetAsync(A + b->z_begin, 0, b->z_end - b->z_begin, s), err);
-  HIPCHECK(hipMemsetAsync(A + b->f_begin, 0xff, b->f_end - b->f_begin, s), err);
+  HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
   const PbaLists pl = pba_lists(b);

@@ -115,6 +115,8 @@ constexpr uint32_t kGrpTileHost = 8192;  // nested.hip kGrpTile: slots per k_gro
 hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // *flag |= 1 when the n words at a and b differ (pqgpu_batch_share_ancestors)
 hipError_t launch_words_differ(const uint32_t *a, const uint32_t *b, uint64_t n, uint32_t *flag, hipStream_t s);
+// the per-decode resets: zn bytes at z to 0, fn bytes at f to 0xff (16-B aligned, multiples of 16)
+hipError_t launch_reset(void *z, uint64_t zn, void *f, uint64_t fn, hipStream_t s);
 hipError_t launch_ba_delta(const BatchDev &b, const LaunchLists &l, hipStream_t s);      // DLBA / DBA values
 hipError_t launch_dba_gather(const BatchDev &b, const LaunchLists &l, hipStream_t s);    // DBA payloads
 hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njobs, hipStream_t s);  // SNAPPY pages

@@ -617,6 +617,25 @@ __global__ void __launch_bounds__(256) k_words_differ(const uint32_t *a_in, cons
     d |= a[i] != b[i];
   if (__ballot(d) && lane_id() == 0) atomicOr(gp(flag), 1u);
 }
+// The per-decode resets in one launch: [z, z + zn) to zero and [f, f + fn) to 0xff bytes (both
+// 16-B aligned, sizes multiples of 16), instead of two fill launches.
+__global__ void __launch_bounds__(256) k_reset(uint4 *z, uint64_t zn, uint4 *f, uint64_t fn) {
+  z = gp(z);
+  f = gp(f);
+  const uint64_t nz = zn / 16, nf = fn / 16, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz + nf; i += stride) {
+    if (i < nz) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    else f[i - nz] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+}
+hipError_t launch_reset(void *z, uint64_t zn, void *f, uint64_t fn, hipStream_t s) {
+  const uint64_t n = (zn + fn) / 16;
+  if (!n) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(k_reset, dim3(grid), dim3(256), 0, s, (uint4 *)z, zn, (uint4 *)f, fn);
+  return hipGetLastError();
+}
+
 hipError_t launch_words_differ(const uint32_t *a, const uint32_t *b, uint64_t n, uint32_t *flag, hipStream_t s) {
   if (!n) return hipSuccess;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 255) / 256);
