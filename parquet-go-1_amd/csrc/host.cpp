@@ -2010,7 +2010,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!any_delta) return hipSuccess;
     hipError_t e = hipStreamWaitEvent(ds, after, 0);
     if (e == hipSuccess) e = timed(b, 10, ds, l.n_delta_pages, [&] { return launch_delta_prep(d, l, ds); });
-    if (e == hipSuccess) e = timed(b, 1, ds, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, ds, l.n_delta_tiles > 0); });
+    if (e == hipSuccess) e = timed(b, 1, ds, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, ds); });
     if (e == hipSuccess) e = hipEventRecord(b->ev_delta_join, ds);
     return e;
   };
@@ -2064,7 +2064,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(timed(b, 9, v, lg.n_items, [&] { return launch_values(d, lg, v); }), err);
       if (nd) {
         HIPCHECK(hipStreamWaitEvent(ds, b->ev_snap[g], 0), err);
-        HIPCHECK(timed(b, 1, ds, nd, [&] { return launch_values_delta(d, it0, nd, ds, l.n_delta_tiles > 0); }), err);
+        HIPCHECK(timed(b, 1, ds, nd, [&] { return launch_values_delta(d, it0, nd, ds); }), err);
       }
     }
     HIPCHECK(hipEventRecord(b->ev_join, v), err);
@@ -2122,7 +2122,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);  // after k_bases: the value bases are known
     if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items one after the other (profiling)
       HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
-      HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s, l.n_delta_tiles > 0); }), err);
+      HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s); }), err);
       HIPCHECK(hipEventRecord(b->ev_delta_join, s), err);
     } else {
       HIPCHECK(fork_delta(b->ev_fork), err);

@@ -99,7 +99,7 @@ hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s);
-hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s, bool tiles);  // DELTA items only
+hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s);  // DELTA items only
 hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s);   // WI_DICT items only
 // byte-array outputs (bytearray.hip): per-tile payload sums, per-chunk scan of the tile sums,
 // offsets + payload of every tile

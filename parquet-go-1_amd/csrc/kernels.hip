@@ -4307,9 +4307,8 @@ hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t
   hipLaunchKernelGGL(k_values_dict, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();
 }
-hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s, bool tiles) {
+hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;
-  (void)tiles;
   hipLaunchKernelGGL(k_values_delta, dim3(n), dim3(256), 0, s, b, items);
   return hipGetLastError();
 }
