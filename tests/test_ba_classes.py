@@ -73,14 +73,26 @@ def test_oracle_ba_classes():
             assert pqtest.oracle_values(r) == ev, (rg, name)
 
 
+# Class routing (host.cpp): the 1,000-entry dictionaries of 16/32-B slots go to class 3 (first slot
+# pieces in LDS) by default, and to class 0 (k_ba_emit_slots: slot gathers) without it.
+BA_ROUTES = {"default": {}, "gather": {"PQ_BA_LDS_SLOTS": "0"}}
+
+
+def set_route(monkeypatch, route):
+    for k, v in BA_ROUTES[route].items():
+        monkeypatch.setenv(k, v)
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("route", list(BA_ROUTES))
 @pytest.mark.parametrize("seed", [0, 1])
-def test_gpu_ba_classes(gpu_ctx, seed):
+def test_gpu_ba_classes(gpu_ctx, seed, route, monkeypatch):
     import test_gpu_parity as P
+    set_route(monkeypatch, route)
     data, _ = build(seed)
     gpu = P._gpu_decode(gpu_ctx, data)
     for rg, col, r in pqtest.oracle_decode(data):
-        pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"seed={seed} rg{rg} {list(COLS)[col]}")
+        pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"seed={seed} {route} rg{rg} {list(COLS)[col]}")
 
 
 HELP_SCRIPT = r"""
@@ -109,3 +121,24 @@ def test_gpu_lookback_self_help():
                         os.path.join(root, "oracle")],
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "HELP-OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", list(BA_ROUTES))
+@pytest.mark.parametrize("name", ["cfg3_small", "cfg3_dict64k", "types_dict", "bad_dict_index", "cfg4_small"])
+def test_gpu_ba_routes_goldens(gpu_ctx, name, route, monkeypatch):
+    """The byte-array goldens (cfg3_dict64k: SURVEY.md §8(d)'s 65,536-entry, 16-bit dictionary)
+    through every k_ba_emit route: the oracle's bytes, or its error at the same page."""
+    import test_gpu_parity as P
+    set_route(monkeypatch, route)
+    data = pqtest.load(name)
+    gpu = P._gpu_decode(gpu_ctx, data)
+    for rg, col, r in pqtest.oracle_decode(data):
+        g = gpu[(rg, col)]
+        where = f"{name} {route} rg{rg} col{col}"
+        if isinstance(r, O.OracleError):
+            assert isinstance(g, P.pqgpu.DecodeError), f"{where}: oracle error {r} but GPU decoded"
+            assert (g.code, g.page) == (r.code, r.page), f"{where}: {g} vs {r}"
+        else:
+            assert not isinstance(g, P.pqgpu.DecodeError), f"{where}: GPU error {g}"
+            pqtest.assert_chunk_equal(g, r, where)

@@ -135,14 +135,18 @@ def test_chunk_page_split(gpu_ctx):
         b.close()
 
 
-def test_repeated_decode_with_failed_byte_array_chunk(gpu_ctx):
+@pytest.mark.parametrize("route", ["default", "gather"])
+def test_repeated_decode_with_failed_byte_array_chunk(gpu_ctx, route, monkeypatch):
     """A batch decoded twice (the benchmark's pattern) whose first BYTE_ARRAY chunk fails on the
     device (dictionary index out of range, type_dict.go:52-54) and whose second decodes: the good
-    chunk must be identical after both decodes, and the bad one must keep its error."""
+    chunk must be identical after both decodes, and the bad one must keep its error. Every
+    k_ba_emit route of a 16/32-B slot dictionary (test_ba_classes.BA_ROUTES)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
     import rawpq
+    import test_ba_classes
+    test_ba_classes.set_route(monkeypatch, route)
     rng = np.random.default_rng(5)
     vocab = sorted({bytes(rng.integers(97, 123, int(rng.integers(1, 30)), dtype=np.uint8)) for _ in range(200)})
     n = 5000
