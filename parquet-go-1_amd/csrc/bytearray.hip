@@ -72,7 +72,12 @@ DEV void lds_put(uint8_t *lb, uint32_t d, const uint8_t *src, uint32_t len) {
 
 // A slot's bytes (slot words 1 .. NW-1 of its first NP 16-B pieces, in registers; len + 4 <=
 // 16 NP) to LDS bytes [d, d + len): dword-aligned funnel shifts and ds_or into the zeroed buffer
-// (the first and last words are shared with the neighbouring values).
+// (the first and last words are shared with the neighbouring values). A slot's bytes past the
+// entry are zero (k_dict_slots), and so are the pieces not loaded, so the words need no masks:
+// the funnel shift brings zeros below the first byte and the padding supplies them past the last.
+#ifndef PQ_BA_NOMASK
+#define PQ_BA_NOMASK 1
+#endif
 template <int NP>
 DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
   constexpr int NW = 4 * NP;
@@ -91,9 +96,13 @@ DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
     if (4u * m >= end) break;
     const uint32_t prev = m ? W[m - 1] : 0u;
     const uint32_t word = sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m];
-    const uint32_t lo = max(sh, 4u * m) - 4u * m, hi = min(end, 4u * m + 4) - 4u * m;  // valid bytes [lo, hi)
-    const uint32_t mask = (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
-    atomicOr(&lw[d0 + m], word & mask);
+    if (PQ_BA_NOMASK && NP == 2) {  // (64-B slots keep the masks: without them the 16-word loop is not unrolled)
+      atomicOr(&lw[d0 + m], word);
+    } else {
+      const uint32_t lo = max(sh, 4u * m) - 4u * m, hi = min(end, 4u * m + 4) - 4u * m;  // valid bytes [lo, hi)
+      const uint32_t mask = (hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+      atomicOr(&lw[d0 + m], word & mask);
+    }
   }
 }
 
