@@ -75,6 +75,36 @@ DEV bool dict_tile_open(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   return true;
 }
 
+// Stage stream bytes [lo, hi) of tile t's stream in L.stage (one coalesced sweep of 16-B loads; bytes
+// at or past the stream end read as zero) when they fit with `reserve` bytes left at the stage's end.
+template <uint32_t NR>
+DEV void dict_tile_stage(DictTileLDST<NR> &L, DictTile &t, uint64_t lo, uint64_t hi, uint32_t reserve) {
+  const uintptr_t ga = ((uintptr_t)(t.s + lo)) & ~(uintptr_t)15;  // 16-B aligned global start
+  const uint64_t sb = (uint64_t)(ga - (uintptr_t)t.s);             // its stream offset (may be "negative")
+  const uint64_t span = hi > lo ? (hi + 8) - (lo & ~(uint64_t)15) + 16 : 0;
+  if (span + reserve > kTileStageB) return;  // reserve: bytes at the stage's end the caller keeps
+  t.staged = true;
+  t.sbit = sb * 8;
+  const uint4 *src = (const uint4 *)gp_u64<const uint8_t>((uint64_t)ga);
+  const uint32_t nv = (uint32_t)((span + 15) / 16);
+  for (uint32_t k = threadIdx.x; k < nv; k += blockDim.x) {
+    uint4 x = src[k];
+    // zero the bytes at or past the stream end (stream offset sb + 16k + j >= n)
+    const int64_t rel = (int64_t)t.n - (int64_t)(sb + 16ull * k);  // stream bytes left at this block
+    if (rel < 16) {
+      uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int64_t r = rel - 4 * q;
+        w[q] = r >= 4 ? w[q] : (r <= 0 ? 0u : (w[q] & ((1u << (8 * r)) - 1u)));
+      }
+      x = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    *(uint4 *)&L.stage[4 * k] = x;
+  }
+  if (threadIdx.x < 8) L.stage[4 * nv + threadIdx.x] = 0;  // funnel reads past the last block
+}
+
 // Load tile [v0, v1) of page `page`: dict_tile_open, then the runs (up to NR) and the
 // stream bytes of the tile's bit-packed values are staged in LDS. Every thread of the workgroup
 // calls it; it ends with a barrier unless it returns false or the bit width is 0 (both
@@ -90,35 +120,39 @@ DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
     for (uint32_t k = threadIdx.x; k < t.nr; k += blockDim.x) L.runs[k] = rg[k];
     t.runs = L.runs;
   }
-  // stream bytes of the tile's bit-packed values (the descriptor's [lo, hi))
-  const uint64_t lo = t.lo, hi = t.hi;
-  const uintptr_t ga = ((uintptr_t)(t.s + lo)) & ~(uintptr_t)15;  // 16-B aligned global start
-  const uint64_t sb = (uint64_t)(ga - (uintptr_t)t.s);             // its stream offset (may be "negative")
-  const uint64_t span = hi > lo ? (hi + 8) - (lo & ~(uint64_t)15) + 16 : 0;
-  if (span + reserve <= kTileStageB) {  // reserve: bytes at the stage's end the caller keeps
-    t.staged = true;
-    t.sbit = sb * 8;
-    const uint4 *src = (const uint4 *)gp_u64<const uint8_t>((uint64_t)ga);
-    const uint32_t nv = (uint32_t)((span + 15) / 16);
-    for (uint32_t k = threadIdx.x; k < nv; k += blockDim.x) {
-      uint4 x = src[k];
-      // zero the bytes at or past the stream end (stream offset sb + 16k + j >= n)
-      const int64_t rel = (int64_t)t.n - (int64_t)(sb + 16ull * k);  // stream bytes left at this block
-      if (rel < 16) {
-        uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int64_t r = rel - 4 * q;
-          w[q] = r >= 4 ? w[q] : (r <= 0 ? 0u : (w[q] & ((1u << (8 * r)) - 1u)));
-        }
-        x = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      *(uint4 *)&L.stage[4 * k] = x;
-    }
-    if (threadIdx.x < 8) L.stage[4 * nv + threadIdx.x] = 0;  // funnel reads past the last block
-  }
+  dict_tile_stage(L, t, t.lo, t.hi, reserve);  // the descriptor's [lo, hi)
   wg_barrier();
   return true;
+}
+
+// Two consecutive tiles of one page, [v0, v0 + kDictTile) and [v0 + kDictTile, v1), loaded
+// together: both descriptors are read at once, and the union of their runs (contiguous in the run
+// table, at most one shared) and of their stream bytes is staged under ONE barrier, so a workgroup
+// pays the tile-load latency chain once for both. ok_a / ok_b: dict_tile_load's result for each
+// (tile b is never valid without tile a: the scan validates runs in stream order). Ends with a
+// barrier iff ok_a and the bit width is not 0 (workgroup-uniform).
+template <uint32_t NR>
+DEV void dict_tile_load2(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
+                         DictTileLDST<NR> &L, DictTile &ta, DictTile &tb, bool &ok_a, bool &ok_b,
+                         uint32_t reserve = 0) {
+  const uint32_t m = min(v0 + kDictTile, v1);
+  uint32_t ra0 = 0, ra1 = 0, rb0 = 0, rb1 = 0;
+  ok_a = dict_tile_open(b, pd, page, v0, m, nn, ta, ra0, ra1);
+  ok_b = m < v1 && dict_tile_open(b, pd, page, m, v1, nn, tb, rb0, rb1);
+  ok_b = ok_b && ok_a;
+  if (!ok_a || ta.bw == 0) return;
+  const uint32_t nr = (ok_b ? rb1 : ra1) - ra0 + 1;  // union of the runs
+  if (nr <= NR) {
+    const HybRun *rg = ta.runs;
+    for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) L.runs[k] = rg[k];
+    ta.runs = L.runs;
+    if (ok_b) tb.runs = L.runs + (rb0 - ra0);
+  }
+  const uint64_t lo = ok_b ? min(ta.lo, tb.lo) : ta.lo, hi = ok_b ? max(ta.hi, tb.hi) : ta.hi;
+  dict_tile_stage(L, ta, lo, hi, reserve);
+  tb.staged = ta.staged;
+  tb.sbit = ta.sbit;
+  wg_barrier();
 }
 
 // The run of value v: binary search over the tile's runs (first value of a lane).

@@ -514,7 +514,8 @@ struct pqgpu_batch {
   // PQ_COPY_FUSED=0/1 forces either (set per plan).
   bool copy_fused = false;
   uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
-  uint32_t n_dict_items = 0;      // the WI_DICT items, after the n_delta_items: k_values_dict
+  uint32_t n_dict_items = 0;      // the WI_DICT(2) items, after the n_delta_items: k_values_dict(2)
+  uint32_t n_dict2_items = 0;     // the first of them: paired (WI_DICT2)
   // PQ_COPY_MODE (speculative schedule): where k_values_copy waits — 0 from the start beside
   // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
@@ -1514,27 +1515,61 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   b->copy_fused = cf ? atoi(cf) != 0 : (b->spec || b->n_groups > 0);
   const bool fused = b->copy_fused;
+  // Dictionary tiles of 4-byte values whose dictionary is staged with the tile (kernels.hip
+  // do_dict2) go two to a workgroup when the batch has many (dict_tile_load2: one tile-load latency
+  // chain per pair). PQ_DICT_PAIR=<n>: pair from n tiles on (0: never). Not with column groups
+  // (their dictionary launches are per group).
+  {
+    const char *pe = getenv("PQ_DICT_PAIR");
+    const size_t min_tiles = pe ? (size_t)atoll(pe) : 8192;
+    size_t nd = 0;
+    for (const auto &it : b->items) nd += it.kind == WI_DICT;
+    if (min_tiles && nd >= min_tiles && b->n_groups == 0) {
+      std::vector<WorkItem> out;
+      out.reserve(b->items.size());
+      for (size_t i = 0; i < b->items.size(); i++) {
+        WorkItem it = b->items[i];
+        const HostChunk &hc = b->chunks[b->pages[it.page].chunk];
+        const bool small = it.kind == WI_DICT && b->pages[it.page].vkind == VK_DICT && hc.value_width == 4 &&
+                           (uint64_t)hc.dict_count * 4 <= kDictEarlyHost;
+        if (small && i + 1 < b->items.size()) {
+          const WorkItem &nx = b->items[i + 1];
+          if (nx.kind == WI_DICT && nx.page == it.page && nx.v0 == it.v1) {  // the page's next tile
+            it.v1 = nx.v1;
+            it.kind = WI_DICT2;
+            i++;
+          }
+        }
+        out.push_back(it);
+      }
+      b->items.swap(out);
+    }
+  }
   // ranks: DELTA tiles, DELTA pages, fused PLAIN / BOOLEAN copies (these three are k_values_delta's
   // launch: latency-bound pages first, the bandwidth-bound copies fill the CUs around them), the
   // dictionary tiles (k_values_dict), the other LDS-staged kinds (k_values), unfused copies
   // (k_values_copy)
   auto rank = [fused](uint8_t k) {
     const bool copy = k == WI_PLAIN || k == WI_BOOL;
-    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 5) : k == WI_DICT ? 3 : 4;
+    return k == WI_DELTA_TILE ? 0 : (k == WI_DELTA || k == WI_DELTA_PAGE) ? 1 : copy ? (fused ? 2 : 5) : (k == WI_DICT || k == WI_DICT2) ? 3 : 4;
   };
   const uint32_t G = b->n_groups;
   auto grp = [&](uint32_t page) { return G ? b->pages[page].chunk * G / nc : 0u; };
   std::stable_sort(b->items.begin(), b->items.end(), [&](const WorkItem &x, const WorkItem &y) {
     const uint32_t gx = grp(x.page), gy = grp(y.page);
-    return gx != gy ? gx < gy : rank(x.kind) < rank(y.kind);
+    if (gx != gy) return gx < gy;
+    if (rank(x.kind) != rank(y.kind)) return rank(x.kind) < rank(y.kind);
+    return x.kind == WI_DICT2 && y.kind != WI_DICT2;  // k_values_dict2's items first
   });
   b->n_delta_items = 0;
   b->n_dict_items = 0;
+  b->n_dict2_items = 0;
   b->n_delta_tiles = 0;
   b->n_copy_items = 0;
   for (auto &it : b->items) {
     b->n_delta_items += rank(it.kind) <= 2;  // k_values_delta's launch
-    b->n_dict_items += rank(it.kind) == 3;   // k_values_dict's launch
+    b->n_dict_items += rank(it.kind) == 3;   // k_values_dict's launch (k_values_dict2's first)
+    b->n_dict2_items += it.kind == WI_DICT2;
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
     b->n_copy_items += rank(it.kind) == 5;
   }
@@ -2002,7 +2037,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // a batch without level streams and column groups keeps its DELTA pages on the batch stream: with
   // nothing to overlap but the other values kinds they only compete with them (cfg5 6.19 -> 6.08 ms)
   const bool lvl_any = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
-  hipStream_t ds = b->one_stream || (!lvl_any && b->n_groups == 0) ? s : b->ctx->delta;
+  const char *dside = getenv("PQ_DELTA_SIDE");  // 1: the DELTA stream in every batch (comparison runs)
+  const bool side = dside && atoi(dside) != 0;
+  hipStream_t ds = b->one_stream || (!lvl_any && b->n_groups == 0 && !side) ? s : b->ctx->delta;
   if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
   // streams with nothing to run are neither forked nor joined (a cross-stream wait costs latency)
   const bool any_delta = l1.n_items || l.n_delta_pages;
@@ -2060,7 +2097,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       lg.n_items = ni - nd - nk;
       HIPCHECK(hipStreamWaitEvent(v, b->ev_snap[g], 0), err);
       HIPCHECK(timed(b, 2, v, lg.n_scan_pages, [&] { return launch_scan_runs(d, lg, v); }), err);
-      HIPCHECK(timed(b, 8, v, nk, [&] { return launch_values_dict(d, it0 + nd, nk, v); }), err);
+      HIPCHECK(timed(b, 8, v, nk, [&] { return launch_values_dict(d, it0 + nd, 0, nk, v); }), err);
       HIPCHECK(timed(b, 9, v, lg.n_items, [&] { return launch_values(d, lg, v); }), err);
       if (nd) {
         HIPCHECK(hipStreamWaitEvent(ds, b->ev_snap[g], 0), err);
@@ -2094,7 +2131,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
     if (b->copy_mode == 6)  // the copies first on the side stream, then the LDS kinds
       HIPCHECK(timed(b, 20, v, l.n_copy_items, [&] { return launch_values_copy(d, l, v); }), err);
-    HIPCHECK(timed(b, 8, v, n_dict, [&] { return launch_values_dict(d, dict_items, n_dict, v); }), err);
+    HIPCHECK(timed(b, 8, v, n_dict, [&] { return launch_values_dict(d, dict_items, b->n_dict2_items, n_dict, v); }), err);
     HIPCHECK(timed(b, 9, v, l2.n_items, [&] { return launch_values(d, l2, v); }), err);
     if (b->copy_mode == 1) HIPCHECK(fork_copies(v), err);
     HIPCHECK(timed(b, 17, v, pl.n_pages, [&] { return launch_plain_ba(d, pl, v); }), err);
@@ -2129,7 +2166,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     HIPCHECK(fork_nest(), err);  // on the DELTA stream after its pages
     HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
-    HIPCHECK(timed(b, 8, s, n_dict, [&] { return launch_values_dict(d, dict_items, n_dict, s); }), err);
+    HIPCHECK(timed(b, 8, s, n_dict, [&] { return launch_values_dict(d, dict_items, b->n_dict2_items, n_dict, s); }), err);
     HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values

@@ -2395,14 +2395,44 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 
 // Dictionary indices of a fixed-width column (type_dict.go:40-60: dst[i] = dict[idx], an index
 // outside the dictionary fails the page with "dict: invalid index") and boolean RLE
-// (type_boolean.go:109-120: value = index == 1), one kDictTile-value tile per workgroup.
-// The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
+// (type_boolean.go:109-120: value = index == 1), one kDictTile-value tile per workgroup, or two
+// (paired items, do_dict). The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
 // [w * 1024, (w + 1) * 1024) of the tile in 16 rounds of 64 consecutive values, so every
 // store instruction writes 64 consecutive outputs (256 B for 4-byte values).
 #ifndef PQ_DICT_LDS
 #define PQ_DICT_LDS 1
 #endif
 constexpr uint32_t kDictEarly = 4096;  // dictionaries up to this many bytes are staged with the tile
+constexpr uint32_t kDictEarlyWord = (kTileStageB - kDictEarly) / 4;  // the early dictionary's first stage word
+
+// This wave's 1024 values of tile t as 16 rounds of indices (LDS reads): idx ~0u where there is no
+// value, or where the index is outside the dictionary (first_err: the first such value).
+DEV void dict_tile_indices(const DictTile &t, const DictTileLDST<kDictRuns> &lds, uint32_t seg0, uint32_t dcount,
+                           uint32_t (&idx)[16], uint32_t &first_err) {
+  const uint32_t lane = lane_id();
+  uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
+#pragma unroll
+  for (uint32_t r = 0; r < 16; r++) {
+    const uint32_t v = seg0 + r * 64 + lane;
+    idx[r] = ~0u;
+    if (v >= t.v0 && v < t.v1) {
+      const uint32_t x = dict_tile_value(t, lds, ri, v);
+      if (x < dcount) idx[r] = x;
+      else first_err = min(first_err, v);
+    }
+  }
+}
+// 4-byte values: all 16 gathers in flight at once, then the stores (out: the wave's first value
+// of round 0 for this lane)
+DEV void dict_store4(const BatchDev &b, uint32_t *out, const uint32_t *dv, const uint32_t (&idx)[16]) {
+  uint32_t val[16];
+#pragma unroll
+  for (uint32_t r = 0; r < 16; r++) val[r] = idx[r] != ~0u ? (PQ_ABLATE(b, 24) ? idx[r] : dv[idx[r]]) : 0u;
+#pragma unroll
+  for (uint32_t r = 0; r < 16; r++)
+    if (idx[r] != ~0u) out[r * 64] = val[r];
+}
+
 DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                  DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
@@ -2415,30 +2445,19 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   // under the same barrier: no barrier pair after the index decode
   const uint32_t dbytes = dcount * w;
   const bool early = PQ_DICT_LDS && !is_bool && w == 4 && dbytes <= kDictEarly;  // workgroup-uniform
-  const uint32_t dword0 = (kTileStageB - kDictEarly) / 4;  // the dictionary's first stage word
   if (early) {
     const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
-    for (uint32_t k = threadIdx.x; k < dbytes / 4; k += blockDim.x) lds.stage[dword0 + k] = src[k];
+    for (uint32_t k = threadIdx.x; k < dbytes / 4; k += blockDim.x) lds.stage[kDictEarlyWord + k] = src[k];
   }
   if (!dict_tile_load(b, pd, wi.page, wi.v0, v1, nn, lds, t, early ? kDictEarly + 64 : 0)) return;
   const uint64_t vb = b.page_vbase[wi.page];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values
   uint32_t first_err = 0xffffffffu;
-  uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
   if (!is_bool && (w == 4 || w == 8)) {
     // the 16 rounds' indices first (LDS), then all gathers in flight at once, then the stores
     uint32_t idx[16];
-#pragma unroll
-    for (uint32_t r = 0; r < 16; r++) {
-      const uint32_t v = seg0 + r * 64 + lane;
-      idx[r] = ~0u;
-      if (v >= t.v0 && v < t.v1) {
-        const uint32_t x = dict_tile_value(t, lds, ri, v);
-        if (x < dcount) idx[r] = x;
-        else first_err = min(first_err, v);
-      }
-    }
+    dict_tile_indices(t, lds, seg0, dcount, idx, first_err);
     // a dictionary that fits the stage is gathered from LDS: once every wave has its indices, the
     // stage's stream bytes are dead and the dictionary takes their place (PQ_DICT_LDS=0: global)
     const bool ldict = PQ_DICT_LDS && (uint64_t)dcount * w <= kTileStageB;  // workgroup-uniform
@@ -2449,14 +2468,8 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
       wg_barrier();
     }
     if (w == 4) {
-      const uint32_t *dv = early ? lds.stage + dword0 : ldict ? lds.stage : gp_u64<const uint32_t>(cd.dict_values);
-      uint32_t *out = gp_u64<uint32_t>(cd.values) + vb + seg0 + lane;
-      uint32_t val[16];
-#pragma unroll
-      for (uint32_t r = 0; r < 16; r++) val[r] = idx[r] != ~0u ? (PQ_ABLATE(b, 24) ? idx[r] : dv[idx[r]]) : 0u;
-#pragma unroll
-      for (uint32_t r = 0; r < 16; r++)
-        if (idx[r] != ~0u) out[r * 64] = val[r];
+      const uint32_t *dv = early ? lds.stage + kDictEarlyWord : ldict ? lds.stage : gp_u64<const uint32_t>(cd.dict_values);
+      dict_store4(b, gp_u64<uint32_t>(cd.values) + vb + seg0 + lane, dv, idx);
     } else {
       const uint64_t *dv = ldict ? (const uint64_t *)lds.stage : gp_u64<const uint64_t>(cd.dict_values);
       uint64_t *out = gp_u64<uint64_t>(cd.values) + vb + seg0 + lane;
@@ -2473,6 +2486,7 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
     if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
     return;
   }
+  uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
   for (uint32_t r = 0; r < 16; r++) {
     const uint32_t v = seg0 + r * 64 + lane;
     if (v < t.v0 || v >= t.v1) continue;
@@ -2490,6 +2504,38 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
       uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v) * w;
       for (uint32_t k = 0; k < w; k++) dst[k] = src[k];
     }
+  }
+  if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
+}
+
+// A paired item (WI_DICT2): two consecutive tiles of one page loaded together (dict_tile_load2), so
+// the workgroup pays the tile-load latency chain (item, descriptors, runs and stream) once for
+// both. host.cpp pairs only dictionary pages of 4-byte values whose dictionary fits kDictEarly;
+// the dictionary is staged with the tiles and stays there for both.
+DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
+                  DictTileLDST<kDictRuns> &lds) {
+  const uint32_t v1 = min(wi.v1, nn);
+  const uint32_t dcount = cd.dict_count;
+  if (wi.v0 >= v1 || cd.value_width != 4 || pd.vkind != VK_DICT || dcount * 4 > kDictEarly) return;  // (see above)
+  {
+    const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
+    for (uint32_t k = threadIdx.x; k < dcount; k += blockDim.x) lds.stage[kDictEarlyWord + k] = src[k];
+  }
+  DictTile ta, tb;
+  bool ok_a, ok_b;
+  dict_tile_load2(b, pd, wi.page, wi.v0, v1, nn, lds, ta, tb, ok_a, ok_b, kDictEarly + 64);
+  if (!ok_a) return;
+  if (ta.bw == 0) wg_barrier();  // (no stream staged: the dictionary's stores still need one)
+  const uint64_t vb = b.page_vbase[wi.page];
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t first_err = 0xffffffffu;
+#pragma nounroll
+  for (uint32_t k = 0; k < (ok_b ? 2u : 1u); k++) {
+    const DictTile t = k ? tb : ta;
+    const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values of the tile
+    uint32_t idx[16];
+    dict_tile_indices(t, lds, seg0, dcount, idx, first_err);
+    dict_store4(b, gp_u64<uint32_t>(cd.values) + vb + seg0 + lane, lds.stage + kDictEarlyWord, idx);
   }
   if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
 }
@@ -3624,6 +3670,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DIC
   const PageDesc &pd = b.pages[wi.page];
   do_dict(b, wi, pd, b.chunks[pd.chunk], b.page_nn_v[wi.page], lds);
 }
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DICT_WPE))) k_values_dict2(BatchDev b_in, const WorkItem *items) {
+  const BatchDev b = global_view(b_in);
+  __shared__ DictTileLDST<kDictRuns> lds;
+  const WorkItem wi = items[blockIdx.x];
+  const PageDesc &pd = b.pages[wi.page];
+  do_dict2(b, wi, pd, b.chunks[pd.chunk], b.page_nn_v[wi.page], lds);
+}
 
 // ---------------------------------------------------------------------------
 // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY values (type_bytearray.go:117-140, :216-240).
@@ -4302,9 +4355,9 @@ hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s)
   hipLaunchKernelGGL(k_values, dim3(l.n_items), dim3(256), 0, s, b, l.items);
   return hipGetLastError();
 }
-hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_values_dict, dim3(n), dim3(256), 0, s, b, items);
+hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n_pair, uint32_t n, hipStream_t s) {
+  if (n_pair) hipLaunchKernelGGL(k_values_dict2, dim3(n_pair), dim3(256), 0, s, b, items);  // paired items first
+  if (n > n_pair) hipLaunchKernelGGL(k_values_dict, dim3(n - n_pair), dim3(256), 0, s, b, items + n_pair);
   return hipGetLastError();
 }
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s) {

@@ -51,6 +51,15 @@ def test_fixture_parity(gpu_ctx, name):
             pqtest.assert_chunk_equal(g, r, where)
 
 
+@pytest.mark.parametrize("name", ["cfg1", "cfg1_full", "types_dict", "bad_dict_index", "cfg5_small", "edge_tiny_pages",
+                                  "edge_nulls_v1", "edge_nulls_v2", "cfg4_small"])
+def test_fixture_parity_paired_dict_tiles(gpu_ctx, name, monkeypatch):
+    """Every dictionary tile pairing it can (PQ_DICT_PAIR=1: k_values_dict2, two tiles of a page
+    per workgroup, host.cpp) must give the oracle's values, and its errors at the same page."""
+    monkeypatch.setenv("PQ_DICT_PAIR", "1")
+    test_fixture_parity(gpu_ctx, name)
+
+
 @pytest.mark.parametrize("name,expected", sorted(pqtest.EXPECTED_ERRORS.items()))
 def test_expected_errors(gpu_ctx, name, expected):
     gpu = _gpu_decode(gpu_ctx, pqtest.load(name))
