@@ -179,4 +179,37 @@ DEV uint32_t dict_tile_value(const DictTile &t, const L_ &L, uint32_t &ri, uint3
   return bits32c(t.s, t.n, bo, t.bw);
 }
 
+// A lane's run cursor with the run in registers: the run's first value, payload offset and info,
+// and the next run's first value, so the values of one run (most of a lane's values: a bit-packed
+// run is up to 504 values long) cost no run-table reads. Values visited must not decrease.
+struct DictCursor {
+  uint32_t ri, start, off, info, next;
+};
+DEV void dict_cursor_load(const DictTile &t, DictCursor &c) {
+  const HybRun r = t.runs[c.ri];
+  c.start = r.value_start;
+  c.off = r.payload_off;
+  c.info = r.info;
+  c.next = c.ri + 1 < t.nr ? t.runs[c.ri + 1].value_start : 0xffffffffu;
+}
+DEV DictCursor dict_cursor(const DictTile &t, uint32_t v) {  // the run of value v
+  DictCursor c{0, 0, 0, 0, 0xffffffffu};
+  if (t.bw == 0) return c;
+  c.ri = dict_tile_seek(t, v);
+  dict_cursor_load(t, c);
+  return c;
+}
+template <class L_>
+DEV uint32_t dict_cursor_value(const DictTile &t, const L_ &L, DictCursor &c, uint32_t v) {
+  if (t.bw == 0) return 0;
+  if (v >= c.next) {
+    do c.ri++; while (c.ri + 1 < t.nr && t.runs[c.ri + 1].value_start <= v);
+    dict_cursor_load(t, c);
+  }
+  if (!(c.info & 0x80000000u)) return c.info;
+  const uint64_t bo = (uint64_t)c.off * 8 + (uint64_t)(v - c.start) * t.bw;
+  if (t.staged) return (uint32_t)lds_bits64(L.stage, (uint32_t)(bo - t.sbit), t.bw);
+  return bits32c(t.s, t.n, bo, t.bw);
+}
+
 }  // namespace pq

@@ -2405,18 +2405,22 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 constexpr uint32_t kDictEarly = 4096;  // dictionaries up to this many bytes are staged with the tile
 constexpr uint32_t kDictEarlyWord = (kTileStageB - kDictEarly) / 4;  // the early dictionary's first stage word
 
+#ifndef PQ_DICT_CURSOR
+#define PQ_DICT_CURSOR 1  // the run in registers (dict_tile.h DictCursor); 0: a run-table read per value
+#endif
 // This wave's 1024 values of tile t as 16 rounds of indices (LDS reads): idx ~0u where there is no
 // value, or where the index is outside the dictionary (first_err: the first such value).
 DEV void dict_tile_indices(const DictTile &t, const DictTileLDST<kDictRuns> &lds, uint32_t seg0, uint32_t dcount,
                            uint32_t (&idx)[16], uint32_t &first_err) {
   const uint32_t lane = lane_id();
-  uint32_t ri = dict_tile_seek(t, max(seg0 + lane, t.v0));
+  DictCursor c = dict_cursor(t, max(seg0 + lane, t.v0));
+  uint32_t ri = PQ_DICT_CURSOR ? 0 : dict_tile_seek(t, max(seg0 + lane, t.v0));
 #pragma unroll
   for (uint32_t r = 0; r < 16; r++) {
     const uint32_t v = seg0 + r * 64 + lane;
     idx[r] = ~0u;
     if (v >= t.v0 && v < t.v1) {
-      const uint32_t x = dict_tile_value(t, lds, ri, v);
+      const uint32_t x = PQ_DICT_CURSOR ? dict_cursor_value(t, lds, c, v) : dict_tile_value(t, lds, ri, v);
       if (x < dcount) idx[r] = x;
       else first_err = min(first_err, v);
     }
@@ -2517,6 +2521,8 @@ DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   const uint32_t v1 = min(wi.v1, nn);
   const uint32_t dcount = cd.dict_count;
   if (wi.v0 >= v1 || cd.value_width != 4 || pd.vkind != VK_DICT || dcount * 4 > kDictEarly) return;  // (see above)
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
   {
     const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
     for (uint32_t k = threadIdx.x; k < dcount; k += blockDim.x) lds.stage[kDictEarlyWord + k] = src[k];
@@ -2526,6 +2532,7 @@ DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
   dict_tile_load2(b, pd, wi.page, wi.v0, v1, nn, lds, ta, tb, ok_a, ok_b, kDictEarly + 64);
   if (!ok_a) return;
   if (ta.bw == 0) wg_barrier();  // (no stream staged: the dictionary's stores still need one)
+  st.lap(0);  // diagnostic stamps: item, descriptors, runs, stream and dictionary staged
   const uint64_t vb = b.page_vbase[wi.page];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t first_err = 0xffffffffu;
@@ -2535,9 +2542,17 @@ DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values of the tile
     uint32_t idx[16];
     dict_tile_indices(t, lds, seg0, dcount, idx, first_err);
+    st.lap(1);  // indices
     dict_store4(b, gp_u64<uint32_t>(cd.values) + vb + seg0 + lane, lds.stage + kDictEarlyWord, idx);
+    st.lap(2);  // gathers and stores issued
   }
   if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
+#ifdef PQ_DIAG_STAMPS
+  if (b.dbg) __builtin_amdgcn_s_waitcnt(0);  // (diagnostic: the stores' drain)
+#endif
+  st.lap(3);
+  st.count(4);
+  st.flush(32);
 }
 
 // DELTA_BINARY_PACKED (deltabp_decoder.go:113-174 / :272-333), one workgroup per page,

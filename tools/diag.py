@@ -45,6 +45,11 @@ dn = ["reload", "walk_wait", "unpack", "scan", "write", "hops#x4", "parse", "wal
 for k, n in enumerate(dn):
     v = int(d[8 + k])
     print(f"delta  {n:12s} total {v:>14d}  per page(wave) {v / (pages // 2) / 4:>12.1f}")
+dd = ["load", "indices", "stores_issue", "drain", "waves#"]
+nw = max(1, int(d[36]))
+for k, n in enumerate(dd):
+    v = int(d[32 + k])
+    print(f"dict2  {n:12s} total {v:>14d}  per wave {v / nw:>12.1f}")
 sn = ["fast_hops", "decode", "chain", "sink", "window", "hops#", "steps#", "-"]
 for k, n in enumerate(sn[:7]):
     v = int(d[56 + k])
