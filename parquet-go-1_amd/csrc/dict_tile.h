@@ -182,6 +182,9 @@ DEV uint32_t dict_tile_value(const DictTile &t, const L_ &L, uint32_t &ri, uint3
 // A lane's run cursor with the run in registers: the run's first value, payload offset and info,
 // and the next run's first value, so the values of one run (most of a lane's values: a bit-packed
 // run is up to 504 values long) cost no run-table reads. Values visited must not decrease.
+#ifndef PQ_DICT_BYTE
+#define PQ_DICT_BYTE 1
+#endif
 struct DictCursor {
   uint32_t ri, start, off, info, next;
 };
@@ -207,6 +210,8 @@ DEV uint32_t dict_cursor_value(const DictTile &t, const L_ &L, DictCursor &c, ui
     dict_cursor_load(t, c);
   }
   if (!(c.info & 0x80000000u)) return c.info;
+  if (PQ_DICT_BYTE && t.bw == 8 && t.staged)  // (uniform) byte-wide indices: one LDS byte read
+    return ((const uint8_t *)L.stage)[c.off + (v - c.start) - (uint32_t)(t.sbit >> 3)];
   const uint64_t bo = (uint64_t)c.off * 8 + (uint64_t)(v - c.start) * t.bw;
   if (t.staged) return (uint32_t)lds_bits64(L.stage, (uint32_t)(bo - t.sbit), t.bw);
   return bits32c(t.s, t.n, bo, t.bw);
