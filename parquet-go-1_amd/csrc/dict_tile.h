@@ -125,33 +125,49 @@ DEV bool dict_tile_load(const BatchDev &b, const PageDesc &pd, uint32_t page, ui
   return true;
 }
 
-// Two consecutive tiles of one page, [v0, v0 + kDictTile) and [v0 + kDictTile, v1), loaded
-// together: both descriptors are read at once, and the union of their runs (contiguous in the run
-// table, at most one shared) and of their stream bytes is staged under ONE barrier, so a workgroup
-// pays the tile-load latency chain once for both. ok_a / ok_b: dict_tile_load's result for each
-// (tile b is never valid without tile a: the scan validates runs in stream order). Ends with a
-// barrier iff ok_a and the bit width is not 0 (workgroup-uniform).
-template <uint32_t NR>
-DEV void dict_tile_load2(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
-                         DictTileLDST<NR> &L, DictTile &ta, DictTile &tb, bool &ok_a, bool &ok_b,
-                         uint32_t reserve = 0) {
-  const uint32_t m = min(v0 + kDictTile, v1);
-  uint32_t ra0 = 0, ra1 = 0, rb0 = 0, rb1 = 0;
-  ok_a = dict_tile_open(b, pd, page, v0, m, nn, ta, ra0, ra1);
-  ok_b = m < v1 && dict_tile_open(b, pd, page, m, v1, nn, tb, rb0, rb1);
-  ok_b = ok_b && ok_a;
-  if (!ok_a || ta.bw == 0) return;
-  const uint32_t nr = (ok_b ? rb1 : ra1) - ra0 + 1;  // union of the runs
-  if (nr <= NR) {
-    const HybRun *rg = ta.runs;
-    for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) L.runs[k] = rg[k];
-    ta.runs = L.runs;
-    if (ok_b) tb.runs = L.runs + (rb0 - ra0);
+// Up to N consecutive tiles of one page ([v0, v1) cut at kDictTile boundaries) loaded together:
+// every descriptor is read at once, and the union of their runs (contiguous in the run table,
+// neighbours share at most one) and of their stream bytes is staged under ONE barrier, so a
+// workgroup pays the tile-load latency chain once for all of them. nt = the tiles loaded (a prefix:
+// a tile is never valid after an invalid one, since the scan validates runs in stream order).
+// Ends with a barrier iff nt > 0 and the bit width is not 0 (workgroup-uniform).
+template <uint32_t N, uint32_t NR>
+DEV void dict_tile_loadn(const BatchDev &b, const PageDesc &pd, uint32_t page, uint32_t v0, uint32_t v1, uint32_t nn,
+                         DictTileLDST<NR> &L, DictTile (&t)[N], uint32_t &nt, uint32_t reserve = 0) {
+  uint32_t r0[N], r1[N];
+  bool ok[N];
+#pragma unroll
+  for (uint32_t k = 0; k < N; k++) {
+    const uint32_t a = v0 + k * kDictTile;
+    ok[k] = a < v1 && dict_tile_open(b, pd, page, a, min(a + kDictTile, v1), nn, t[k], r0[k], r1[k]);
   }
-  const uint64_t lo = ok_b ? min(ta.lo, tb.lo) : ta.lo, hi = ok_b ? max(ta.hi, tb.hi) : ta.hi;
-  dict_tile_stage(L, ta, lo, hi, reserve);
-  tb.staged = ta.staged;
-  tb.sbit = ta.sbit;
+  nt = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < N; k++)
+    if (ok[k] && nt == k) nt = k + 1;
+  if (nt == 0 || t[0].bw == 0) return;
+  uint32_t rl = r1[0];
+  uint64_t lo = t[0].lo, hi = t[0].hi;
+#pragma unroll
+  for (uint32_t k = 1; k < N; k++)
+    if (k < nt) {
+      rl = r1[k];
+      lo = min(lo, (uint64_t)t[k].lo);
+      hi = max(hi, (uint64_t)t[k].hi);
+    }
+  const uint32_t nr = rl - r0[0] + 1;  // the union of the runs
+  if (nr <= NR) {
+    const HybRun *rg = t[0].runs;
+    for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) L.runs[k] = rg[k];
+#pragma unroll
+    for (uint32_t k = 0; k < N; k++) t[k].runs = L.runs + (r0[k] - r0[0]);
+  }
+  dict_tile_stage(L, t[0], lo, hi, reserve);
+#pragma unroll
+  for (uint32_t k = 1; k < N; k++) {
+    t[k].staged = t[0].staged;
+    t[k].sbit = t[0].sbit;
+  }
   wg_barrier();
 }
 

@@ -515,7 +515,7 @@ struct pqgpu_batch {
   bool copy_fused = false;
   uint32_t n_copy_items = 0;      // the last n_copy_items work items go to k_values_copy
   uint32_t n_dict_items = 0;      // the WI_DICT(2) items, after the n_delta_items: k_values_dict(2)
-  uint32_t n_dict2_items = 0;     // the first of them: paired (WI_DICT2)
+  uint32_t n_dict2_items = 0;     // the first of them: grouped (WI_DICT2)
   // PQ_COPY_MODE (speculative schedule): where k_values_copy waits — 0 from the start beside
   // everything, 1 after k_values on the side stream, 2 after the level kernels, 3 after both
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
@@ -1516,12 +1516,15 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->copy_fused = cf ? atoi(cf) != 0 : (b->spec || b->n_groups > 0);
   const bool fused = b->copy_fused;
   // Dictionary tiles of 4-byte values whose dictionary is staged with the tile (kernels.hip
-  // do_dict2) go two to a workgroup when the batch has many (dict_tile_load2: one tile-load latency
-  // chain per pair). PQ_DICT_PAIR=<n>: pair from n tiles on (0: never). Not with column groups
-  // (their dictionary launches are per group).
+  // do_dict2) go up to kDictGroupHost to a workgroup when the batch has many (dict_tile_loadn: one tile-load
+  // latency chain per group), as many as fit the stage beside the dictionary: 12 KiB of index
+  // stream, 24 / bw tiles. PQ_DICT_PAIR=<n>: group from n tiles on (0: never). Not with column
+  // groups (their dictionary launches are per group).
   {
     const char *pe = getenv("PQ_DICT_PAIR");
     const size_t min_tiles = pe ? (size_t)atoll(pe) : 8192;
+    const char *gm = getenv("PQ_DICT_GROUP");  // (comparison runs: at most this many tiles per item)
+    const uint32_t gmax = gm && atoi(gm) > 0 ? std::min<uint32_t>((uint32_t)atoi(gm), kDictGroupHost) : kDictGroupHost;
     size_t nd = 0;
     for (const auto &it : b->items) nd += it.kind == WI_DICT;
     if (min_tiles && nd >= min_tiles && b->n_groups == 0) {
@@ -1529,16 +1532,17 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       out.reserve(b->items.size());
       for (size_t i = 0; i < b->items.size(); i++) {
         WorkItem it = b->items[i];
-        const HostChunk &hc = b->chunks[b->pages[it.page].chunk];
-        const bool small = it.kind == WI_DICT && b->pages[it.page].vkind == VK_DICT && hc.value_width == 4 &&
+        const PageDesc &pd = b->pages[it.page];
+        const HostChunk &hc = b->chunks[pd.chunk];
+        const bool small = it.kind == WI_DICT && pd.vkind == VK_DICT && hc.value_width == 4 &&
                            (uint64_t)hc.dict_count * 4 <= kDictEarlyHost;
-        if (small && i + 1 < b->items.size()) {
+        const uint32_t g = small ? std::min<uint32_t>(gmax, pd.dict_bw ? 24u / pd.dict_bw : gmax) : 1;
+        for (uint32_t k = 1; k < g && i + 1 < b->items.size(); k++) {
           const WorkItem &nx = b->items[i + 1];
-          if (nx.kind == WI_DICT && nx.page == it.page && nx.v0 == it.v1) {  // the page's next tile
-            it.v1 = nx.v1;
-            it.kind = WI_DICT2;
-            i++;
-          }
+          if (nx.kind != WI_DICT || nx.page != it.page || nx.v0 != it.v1) break;  // the page's next tile
+          it.v1 = nx.v1;
+          it.kind = WI_DICT2;
+          i++;
         }
         out.push_back(it);
       }

@@ -61,6 +61,7 @@ constexpr uint32_t kNestCnt = 9;       // nested counters per page: lists of lev
 constexpr uint32_t kNestPkWords = 2048; // u64 words of packed levels per nested tile (nested.hip)
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kDictEarlyHost = 4096;  // kernels.hip kDictEarly: dictionaries staged with their tile
+constexpr uint32_t kDictGroupHost = 2;     // kernels.hip kDictGroup: tiles per WI_DICT2 item (at most)
 constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
                                         // page's BA tiles are its dictionary tiles)
 
@@ -101,7 +102,7 @@ hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s);  // DELTA items only
-// WI_DICT2 (paired) items [0, n_pair), then WI_DICT items [n_pair, n)
+// WI_DICT2 (grouped) items [0, n_pair), then WI_DICT items [n_pair, n)
 hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n_pair, uint32_t n, hipStream_t s);
 // byte-array outputs (bytearray.hip): per-tile payload sums, per-chunk scan of the tile sums,
 // offsets + payload of every tile

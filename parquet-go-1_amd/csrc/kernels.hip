@@ -2395,8 +2395,8 @@ DEV void do_bool(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
 
 // Dictionary indices of a fixed-width column (type_dict.go:40-60: dst[i] = dict[idx], an index
 // outside the dictionary fails the page with "dict: invalid index") and boolean RLE
-// (type_boolean.go:109-120: value = index == 1), one kDictTile-value tile per workgroup, or two
-// (paired items, do_dict). The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
+// (type_boolean.go:109-120: value = index == 1), one kDictTile-value tile per workgroup, or
+// kDictGroup of them (grouped items, do_dict2). The tile's runs and stream bytes are staged in LDS (dict_tile.h); wave w takes values
 // [w * 1024, (w + 1) * 1024) of the tile in 16 rounds of 64 consecutive values, so every
 // store instruction writes 64 consecutive outputs (256 B for 4-byte values).
 #ifndef PQ_DICT_LDS
@@ -2512,10 +2512,13 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
   if (first_err != 0xffffffffu) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, first_err, PQ_ERR_DICT_INDEX);
 }
 
-// A paired item (WI_DICT2): two consecutive tiles of one page loaded together (dict_tile_load2), so
-// the workgroup pays the tile-load latency chain (item, descriptors, runs and stream) once for
-// both. host.cpp pairs only dictionary pages of 4-byte values whose dictionary fits kDictEarly;
-// the dictionary is staged with the tiles and stays there for both.
+// A grouped item (WI_DICT2): up to kDictGroup consecutive tiles of one page loaded together
+// (dict_tile_loadn), so the workgroup pays the tile-load latency chain (item, descriptors, runs and
+// stream) once for all of them. host.cpp groups only dictionary pages of 4-byte values whose
+// dictionary fits kDictEarly, and sizes the group so its stream bytes fit the stage beside the
+// dictionary, which is staged with the tiles and stays there for all of them.
+constexpr uint32_t kDictGroup = 2;  // (3 measured the same on cfg5: 0.661 against 0.662 ms)
+static_assert(kDictGroup == kDictGroupHost, "host.cpp groups at most kDictGroupHost tiles");
 DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn,
                   DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
@@ -2527,21 +2530,21 @@ DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
     const uint32_t *src = gp_u64<const uint32_t>(cd.dict_values);
     for (uint32_t k = threadIdx.x; k < dcount; k += blockDim.x) lds.stage[kDictEarlyWord + k] = src[k];
   }
-  DictTile ta, tb;
-  bool ok_a, ok_b;
-  dict_tile_load2(b, pd, wi.page, wi.v0, v1, nn, lds, ta, tb, ok_a, ok_b, kDictEarly + 64);
-  if (!ok_a) return;
-  if (ta.bw == 0) wg_barrier();  // (no stream staged: the dictionary's stores still need one)
+  DictTile t[kDictGroup];
+  uint32_t nt;
+  dict_tile_loadn(b, pd, wi.page, wi.v0, v1, nn, lds, t, nt, kDictEarly + 64);
+  if (nt == 0) return;
+  if (t[0].bw == 0) wg_barrier();  // (no stream staged: the dictionary's stores still need one)
   st.lap(0);  // diagnostic stamps: item, descriptors, runs, stream and dictionary staged
   const uint64_t vb = b.page_vbase[wi.page];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t first_err = 0xffffffffu;
-#pragma nounroll
-  for (uint32_t k = 0; k < (ok_b ? 2u : 1u); k++) {
-    const DictTile t = k ? tb : ta;
-    const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values of the tile
+#pragma unroll
+  for (uint32_t k = 0; k < kDictGroup; k++) {
+    if (k >= nt) break;
+    const uint32_t seg0 = t[k].v0 - t[k].v0 % kDictTile + wv * 1024;  // this wave's 1024 values of the tile
     uint32_t idx[16];
-    dict_tile_indices(t, lds, seg0, dcount, idx, first_err);
+    dict_tile_indices(t[k], lds, seg0, dcount, idx, first_err);
     st.lap(1);  // indices
     dict_store4(b, gp_u64<uint32_t>(cd.values) + vb + seg0 + lane, lds.stage + kDictEarlyWord, idx);
     st.lap(2);  // gathers and stores issued
@@ -4371,7 +4374,7 @@ hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s)
   return hipGetLastError();
 }
 hipError_t launch_values_dict(const BatchDev &b, const WorkItem *items, uint32_t n_pair, uint32_t n, hipStream_t s) {
-  if (n_pair) hipLaunchKernelGGL(k_values_dict2, dim3(n_pair), dim3(256), 0, s, b, items);  // paired items first
+  if (n_pair) hipLaunchKernelGGL(k_values_dict2, dim3(n_pair), dim3(256), 0, s, b, items);  // grouped items first
   if (n > n_pair) hipLaunchKernelGGL(k_values_dict, dim3(n - n_pair), dim3(256), 0, s, b, items + n_pair);
   return hipGetLastError();
 }

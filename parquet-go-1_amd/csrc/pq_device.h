@@ -141,7 +141,7 @@ enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED =
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,
                  WI_DELTA_TILE = 6, WI_DELTA_PAGE = 7, WI_DLENS = 8,
-                 WI_DICT2 = 9 };  // two consecutive dictionary tiles of one page (k_values_dict2)
+                 WI_DICT2 = 9 };  // 2-3 consecutive dictionary tiles of one page (k_values_dict2)
 
 // DELTA_BINARY_PACKED block table entry (one per block of a page), written by the header
 // walk (k_delta_walk), completed by the per-page scan of block sums (k_delta_prefix).
