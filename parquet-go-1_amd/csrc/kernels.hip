@@ -3977,6 +3977,15 @@ struct SnappyCmd {                         // LDS: wave 0 -> helper waves
 };
 
 // Share of one long-literal body for wave `w` (all waves call it between two barriers).
+// PQ_SNAPPY_ONELOAD: one load per 16-B piece (the funnel's second block is the next lane's first,
+// taken by a lane shuffle as in copy_bytes_u; wave w's round covers 64 U consecutive pieces); 0: two
+// loads per piece.
+#ifndef PQ_SNAPPY_ONELOAD
+#define PQ_SNAPPY_ONELOAD 0
+#endif
+#ifndef PQ_SNAPPY_U
+#define PQ_SNAPPY_U 4
+#endif
 DEV void snappy_body(const SnappyCmd &c, uint8_t *ring, uint8_t *dst, uint32_t w) {
   const uint8_t *S = gp_u64<const uint8_t>(c.src);
   const uint32_t P = c.P, pieces = c.pieces, ring_from = c.ring_from;
@@ -3985,6 +3994,34 @@ DEV void snappy_body(const SnappyCmd &c, uint8_t *ring, uint8_t *dst, uint32_t w
   uint4 *d = (uint4 *)(dst + P);
   constexpr uint32_t NT = 64 * kSnappyWaves, U = 4;
   uint32_t i = w * 64 + lane_id();
+  if (PQ_SNAPPY_ONELOAD) {
+    const uint32_t lane = lane_id();
+    const int nxt = (int)(((lane + 1) & 63u) * 4);
+    auto shd = [nxt](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)v); };
+    constexpr uint32_t U1 = PQ_SNAPPY_U;  // pieces per lane in flight
+    uint32_t r0 = 0;
+    for (; r0 + NT * U1 <= pieces; r0 += NT * U1) {
+      const uint32_t j = r0 + w * 64 * U1 + lane;
+      uint4 a[U1];
+#pragma unroll
+      for (uint32_t u = 0; u < U1; u++) a[u] = sb[j + 64 * u];
+      uint4 e = make_uint4(0u, 0u, 0u, 0u);
+      if (sa && lane == 63) e = sb[j + 64 * (U1 - 1) + 1];
+#pragma unroll
+      for (uint32_t u = 0; u < U1; u++) {
+        uint4 v = a[u];
+        if (sa) {
+          const uint4 o = (lane == 0 && u + 1 < U1) ? a[u + 1] : a[u];  // what lane l - 1 takes from this lane
+          uint4 nb = make_uint4(shd(o.x), shd(o.y), shd(o.z), shd(o.w));
+          if (lane == 63 && u + 1 == U1) nb = e;
+          v = funnel16(a[u], nb, sa);
+        }
+        d[j + 64 * u] = v;
+        if (j + 64 * u >= ring_from) *(uint4 *)(ring + ((P + (j + 64 * u) * 16) & kRingMask)) = v;
+      }
+    }
+    i = r0 + w * 64 + lane;
+  }
   for (; i + (U - 1) * NT < pieces; i += U * NT) {
     uint4 a[U], e[U];
 #pragma unroll
