@@ -3979,9 +3979,10 @@ struct SnappyCmd {                         // LDS: wave 0 -> helper waves
 // Share of one long-literal body for wave `w` (all waves call it between two barriers).
 // PQ_SNAPPY_ONELOAD: one load per 16-B piece (the funnel's second block is the next lane's first,
 // taken by a lane shuffle as in copy_bytes_u; wave w's round covers 64 U consecutive pieces); 0: two
-// loads per piece.
+// loads per piece. cfg5 k_snappy 3.867 -> 3.834 ms; 8 pieces per lane 3.853 ms
+// (profiles/r04_s19_probe_snappy_oneload.txt).
 #ifndef PQ_SNAPPY_ONELOAD
-#define PQ_SNAPPY_ONELOAD 0
+#define PQ_SNAPPY_ONELOAD 1
 #endif
 #ifndef PQ_SNAPPY_U
 #define PQ_SNAPPY_U 4
