@@ -199,11 +199,11 @@ __global__ void __launch_bounds__(256) k_ba_sums(BatchDev b_in) {
       if (dict_tile_load(b, pd, p, v0, v1, nn, lds, tl)) {
         const uint2 *ent = gp_u64<const uint2>(cd.dict_offsets);
         const uint32_t lane = lane_id(), seg0 = v0 + (threadIdx.x >> 6) * 1024;
-        uint32_t ri = dict_tile_seek(tl, max(seg0 + lane, tl.v0));
+        DictCursor rc = dict_cursor(tl, max(seg0 + lane, tl.v0));
         for (uint32_t r = 0; r < 16; r++) {
           const uint32_t v = seg0 + r * 64 + lane;
           if (v < tl.v0 || v >= tl.v1) continue;
-          const uint32_t idx = dict_tile_value(tl, lds, ri, v);
+          const uint32_t idx = dict_cursor_value(tl, lds, rc, v);
           if (idx < cd.dict_count) sum += ent[idx].y;  // out of range: k_ba_emit reports it
         }
       }
@@ -381,14 +381,14 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   // ---- pass A: indices (LDS), then the lengths (slot word 0) for all rounds at once
   uint32_t idx[R];
   uint32_t first_err = 0xffffffffu;
-  uint32_t ri = (is_dict && have) ? dict_tile_seek(tl, max(seg0 + lane, lo)) : 0;
+  DictCursor rc = (is_dict && have) ? dict_cursor(tl, max(seg0 + lane, lo)) : DictCursor{0, 0, 0, 0, 0xffffffffu};
 #pragma unroll
   for (uint32_t r = 0; r < R; r++) {
     const uint32_t v = seg0 + r * 64 + lane;
     idx[r] = ~0u;
     if (have && v >= lo && v < hi) {
       if (is_dict) {
-        const uint32_t x = dict_tile_value(tl, L.tile, ri, v);
+        const uint32_t x = dict_cursor_value(tl, L.tile, rc, v);
         if (x < cd.dict_count) idx[r] = x;
         else first_err = min(first_err, v);
       } else {
