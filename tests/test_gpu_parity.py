@@ -121,6 +121,16 @@ def test_speculative_and_serial_schedules_agree(gpu_ctx, monkeypatch):
                 pqtest.assert_chunk_equal(gpu[(rg, col)], r, f"{name} serial={serial} rg{rg} col{col}")
 
 
+@pytest.mark.parametrize("name", ["cfg2_v2_small", "cfg3_small", "cfg4_small", "cfg4_v2", "cfg5_small", "types_v2",
+                                  "bad_dict_index"])
+def test_one_stream_schedule_agrees(gpu_ctx, name, monkeypatch):
+    """PQ_ONE_STREAM=1 runs every kernel of a decode on the batch stream (no DELTA / copy / side
+    streams, the byte-array look-back instead of the pre-pass beside nested arrays): the profiling
+    schedule must give the oracle's bytes, and its errors at the same page."""
+    monkeypatch.setenv("PQ_ONE_STREAM", "1")
+    test_fixture_parity(gpu_ctx, name)
+
+
 def test_chunk_page_split(gpu_ctx):
     """pqgpu_batch_chunk_pages: page k of a chunk owns its header's num_values level slots and
     the non-null values its definition levels count, in order (data_store.go:236-260)."""
