@@ -1534,8 +1534,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         WorkItem it = b->items[i];
         const PageDesc &pd = b->pages[it.page];
         const HostChunk &hc = b->chunks[pd.chunk];
-        const bool small = it.kind == WI_DICT && pd.vkind == VK_DICT && hc.value_width == 4 &&
-                           (uint64_t)hc.dict_count * 4 <= kDictEarlyHost;
+        const bool small = it.kind == WI_DICT && dict2_eligible(pd.vkind, hc.value_width, hc.dict_count);
         const uint32_t g = small ? std::min<uint32_t>(gmax, pd.dict_bw ? 24u / pd.dict_bw : gmax) : 1;
         for (uint32_t k = 1; k < g && i + 1 < b->items.size(); k++) {
           const WorkItem &nx = b->items[i + 1];
@@ -3131,16 +3130,19 @@ int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t 
     same = h == 0;
   }
   if (same) {
-    // link to the root of ia's sharing chain, never to a chunk that already follows ib: the links
-    // stay acyclic, so chunk_result's walk along share_from ends
-    int32_t root = ia;
-    for (int32_t hops = 0; b->chunks[(size_t)root].share_from >= 0 && hops <= (int32_t)b->chunks.size(); hops++)
-      root = b->chunks[(size_t)root].share_from;
-    if (root == ib) {  // ia already takes its arrays from ib: nothing to link
-      if (equal) *equal = 1;
-      return PQ_OK;
+    // link ib to ia itself: ia's own result resolves its levels [0, La) (those it shares further down
+    // its chain come from there, chunk_result recurses), while the chain's root may hold fewer of
+    // them. The chain is walked only to keep the links acyclic: when ia already follows ib, the
+    // arrays are equal and nothing is linked, so chunk_result's walk along share_from ends.
+    int32_t at = ia;
+    for (int32_t hops = 0; at >= 0 && hops <= (int32_t)b->chunks.size(); hops++) {
+      if (at == ib) {
+        if (equal) *equal = 1;
+        return PQ_OK;
+      }
+      at = b->chunks[(size_t)at].share_from;
     }
-    hb.share_from = root;
+    hb.share_from = ia;
     hb.share_lists = (uint32_t)La;
     hb.share_groups = (uint32_t)Ga;
     if (equal) *equal = 1;

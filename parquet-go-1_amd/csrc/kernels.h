@@ -62,6 +62,11 @@ constexpr uint32_t kNestPkWords = 2048; // u64 words of packed levels per nested
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kDictEarlyHost = 4096;  // kernels.hip kDictEarly: dictionaries staged with their tile
 constexpr uint32_t kDictGroupHost = 2;     // kernels.hip kDictGroup: tiles per WI_DICT2 item (at most)
+// The pages whose dictionary tiles may be grouped into WI_DICT2 items: host.cpp groups only these and
+// kernels.hip do_dict2 decodes only these (a grouped item outside it is reported, never dropped).
+__host__ __device__ constexpr inline bool dict2_eligible(uint32_t vkind, uint32_t value_width, uint64_t dict_count) {
+  return vkind == VK_DICT && value_width == 4 && dict_count * 4 <= kDictEarlyHost;
+}
 constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
                                         // page's BA tiles are its dictionary tiles)
 

@@ -2454,6 +2454,9 @@ DEV void do_dict(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, cons
     for (uint32_t k = threadIdx.x; k < dbytes / 4; k += blockDim.x) lds.stage[kDictEarlyWord + k] = src[k];
   }
   if (!dict_tile_load(b, pd, wi.page, wi.v0, v1, nn, lds, t, early ? kDictEarly + 64 : 0)) return;
+  // dict_tile_load ends without a barrier at bit width 0 (workgroup-uniform): the early dictionary's
+  // stores above must still be visible to every wave before the gathers
+  if (early && t.bw == 0) wg_barrier();
   const uint64_t vb = b.page_vbase[wi.page];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t seg0 = t.v0 - t.v0 % kDictTile + wv * 1024;  // this wave's 1024 values
@@ -2523,7 +2526,12 @@ DEV void do_dict2(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, con
                   DictTileLDST<kDictRuns> &lds) {
   const uint32_t v1 = min(wi.v1, nn);
   const uint32_t dcount = cd.dict_count;
-  if (wi.v0 >= v1 || cd.value_width != 4 || pd.vkind != VK_DICT || dcount * 4 > kDictEarly) return;  // (see above)
+  if (wi.v0 >= v1) return;
+  static_assert(kDictEarly == kDictEarlyHost, "dict2_eligible sizes the dictionary by kDictEarlyHost");
+  if (!dict2_eligible(pd.vkind, (uint32_t)cd.value_width, dcount)) {  // (workgroup-uniform) never grouped by host.cpp
+    if (threadIdx.x == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, wi.v0, PQ_ERR_UNSUPPORTED);
+    return;
+  }
   PQ_STAMPS(st, b.dbg);
   st.begin();
   {

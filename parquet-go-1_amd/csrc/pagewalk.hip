@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     if (lane == 0) at = atomicAdd(table_n, n);
     at = sgpr(__shfl(at, 0));
     if ((uint64_t)at + n > table_cap) return false;
-    // test_skip (PQ_IX_TEST_SKIP_STORE, tests only): chunk test_skip reserves its slots but stores
+    // test_skip (PQ_IX_TEST_SKIP_STORE, diagnostic build): chunk test_skip reserves its slots but stores
     // nothing, as if its stores were lost; the host must not trust what the slots hold
     if (lane < n && c != test_skip) table[at + lane] = mine;
     return true;
@@ -470,8 +470,13 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
                             int validate_crc, uint32_t gen, hipStream_t s) {
   if (!nchunks) return hipSuccess;
   const uint32_t sys_fence = getenv("PQ_IX_FENCE") && atoi(getenv("PQ_IX_FENCE")) == 1;
-  const char *skip_env = getenv("PQ_IX_TEST_SKIP_STORE");  // tests: one chunk's table stores are dropped
+#ifdef PQ_DIAG_STAMPS
+  // diagnostic build only (tests/test_page_index.py): one chunk's table stores are dropped
+  const char *skip_env = getenv("PQ_IX_TEST_SKIP_STORE");
   const uint32_t test_skip = skip_env ? (uint32_t)atoi(skip_env) : 0xffffffffu;
+#else
+  const uint32_t test_skip = 0xffffffffu;
+#endif
   hipLaunchKernelGGL(k_page_walk_init, dim3((nchunks + 255) / 256), dim3(256), 0, s, table_n, res, nchunks);
   for (uint32_t c0 = 0; c0 < nchunks; c0 += kIxArgChunks) {
     const uint32_t n = std::min<uint32_t>(kIxArgChunks, nchunks - c0);

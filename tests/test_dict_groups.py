@@ -86,6 +86,62 @@ def test_oracle_dict_groups(optional):
         np.testing.assert_array_equal(np.asarray(pqtest.oracle_values(r)), np.asarray(expect[name], np.int32), err_msg=name)
 
 
+def build_bw0(seed, optional=False, entries=1):
+    """INT32 RLE_DICTIONARY pages of index bit width 0 (parquet-mr sizes the width from the largest
+    index: a one-entry dictionary gets width 0). hybrid_decoder.go:83-85 returns 0 for every value
+    without reading the stream, so the stream bytes after the width byte are arbitrary; here a few
+    RLE and bit-packed run headers. Pages are long enough that every wave of a 4,096-value tile (and
+    of a tile pair) has values. entries=0: every index is out of range (type_dict.go:52-54)."""
+    rng = np.random.default_rng(1700 + seed)
+    vocab = [int(x) for x in rng.integers(-2**31, 2**31 - 1, entries)]
+    pages = [rawpq.dict_page_ref("INT32", vocab)]
+    vals = []
+    for nv in PAGE_VALUES:
+        nulls = rng.random(nv) < (0.1 if optional else 0.0)
+        dl = (~nulls).astype(int)
+        body = bytes([0]) + rawpq.uvar(int(dl.sum()) << 1) + rawpq.uvar((3 << 1) | 1)
+        pages.append(rawpq.data_page_v1_ref(nv, "RLE_DICTIONARY", body, dl.tolist() if optional else None,
+                                            1 if optional else 0))
+        vals += [vocab[0] if entries else None] * int(dl.sum())
+    schema = [[(4, rawpq.BIN, "schema"), (5, rawpq.I32, 1)]]
+    schema += [rawpq.schema_leaf("bw0", "INT32", "OPTIONAL" if optional else "REQUIRED")]
+    return rawpq.write_file_schema(schema, [("bw0", "INT32")], [(sum(PAGE_VALUES), [(pages, sum(PAGE_VALUES), True)])]), vals
+
+
+@pytest.mark.parametrize("optional", [False, True])
+def test_oracle_dict_bw0(optional):
+    data, expect = build_bw0(0, optional=optional)
+    r = O.File(data).read_chunk(0, 0)
+    np.testing.assert_array_equal(np.asarray(pqtest.oracle_values(r)), np.asarray(expect, np.int32))
+    bad, _ = build_bw0(0, optional=optional, entries=0)
+    with pytest.raises(O.OracleError) as e:
+        O.File(bad).read_chunk(0, 0)
+    assert (e.value.code, e.value.page) == (5, 0)  # PQ_ERR_DICT_INDEX on the first data page
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pair", ["1", "0"])
+@pytest.mark.parametrize("optional", [False, True])
+@pytest.mark.parametrize("entries", [1, 0])
+def test_gpu_dict_bw0(gpu_ctx, pair, optional, entries, monkeypatch):
+    """Bit width 0 on the early-dictionary path of do_dict (the one-entry dictionary is staged with
+    the tile, and dict_tile_load ends without a barrier at width 0) and of do_dict2; decoded twice so
+    that a read of stale LDS from an earlier workgroup would show."""
+    import test_gpu_parity as P
+    monkeypatch.setenv("PQ_DICT_PAIR", pair)
+    data, _ = build_bw0(2, optional=optional, entries=entries)
+    ((_, _, r),) = list(pqtest.oracle_decode(data))
+    for rep in range(2):
+        g = P._gpu_decode(gpu_ctx, data)[(0, 0)]
+        where = f"pair={pair} optional={optional} entries={entries} rep={rep}"
+        if isinstance(r, O.OracleError):
+            assert isinstance(g, P.pqgpu.DecodeError), f"{where}: oracle error {r} but GPU decoded"
+            assert (g.code, g.page) == (r.code, r.page), f"{where}: {g} vs {r}"
+        else:
+            assert not isinstance(g, P.pqgpu.DecodeError), f"{where}: GPU error {g}"
+            pqtest.assert_chunk_equal(g, r, where)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pair", ["1", "0"])
 @pytest.mark.parametrize("optional", [False, True])

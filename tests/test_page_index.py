@@ -362,23 +362,19 @@ def test_build_stats_clean(gpu_ctx, name):
         assert st == {"polls": 0, "unreported": 0, "fallback_chunks": 0, "overflowed": 0, "stale_entries": 0}, (name, st)
 
 
-@pytest.mark.parametrize("name", ["edge_tiny_pages", "cfg2_v2_small"])
-def test_stale_entries_dropped(gpu_ctx, monkeypatch, name):
-    """Table entries carry the build's generation stamp. A chunk whose walk reports success with the
-    right page count but whose table stores never landed (PQ_IX_TEST_SKIP_STORE: its slots are
-    reserved and left as they were — here holding the previous build's entries for the same chunk,
-    same slots, same count) must not be trusted: its entries are dropped as stale, the count no
-    longer adds up, the chunk falls back to the host walk, and the decode still equals the oracle."""
+def _stale_entries_body(gpu_ctx, name):
+    """(run in a diagnostic-library process: PQ_IX_TEST_SKIP_STORE exists only in that build)"""
     data = pqtest.load(name)
     f = pqgpu.File(data)
     chunks = _all_chunks(f)
     k = len(chunks) - 1  # the chunk whose stores are dropped
     mine = [chunks[k]]
+    os.environ.pop("PQ_IX_TEST_SKIP_STORE", None)
     ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, mine, whole_file=True)  # fills the scratch table
     pages, status = ix.chunk(0)
     assert status == pqgpu.IX_OK and pages > 0
     ix.close()
-    monkeypatch.setenv("PQ_IX_TEST_SKIP_STORE", "0")
+    os.environ["PQ_IX_TEST_SKIP_STORE"] = "0"
     ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, mine, whole_file=True)
     st = ix.stats()
     assert ix.chunk(0) == (0, pqgpu.IX_FALLBACK), (name, st)
@@ -386,10 +382,53 @@ def test_stale_entries_dropped(gpu_ctx, monkeypatch, name):
     ix.close()
     # the whole file with one chunk's stores dropped: that chunk is walked by the host, the others
     # by the device, and every result equals the oracle's
-    monkeypatch.setenv("PQ_IX_TEST_SKIP_STORE", str(k))
+    os.environ["PQ_IX_TEST_SKIP_STORE"] = str(k)
     ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, chunks, whole_file=True)
     st = ix.stats()
     assert st["fallback_chunks"] == 1 and st["stale_entries"] >= 0, st
     assert ix.chunk(k)[1] == pqgpu.IX_FALLBACK and all(ix.chunk(j)[1] == pqgpu.IX_OK for j in range(k))
     ix.close()
-    _check_against_oracle(name, data, _decode_indexed(gpu_ctx, data))
+    got = _decode_indexed(gpu_ctx, data)
+    os.environ.pop("PQ_IX_TEST_SKIP_STORE", None)
+    _check_against_oracle(name, data, got)
+
+
+STALE_SCRIPT = """
+import sys
+sys.path[:0] = sys.argv[2:5]
+import pqgpu, test_page_index as T
+T._stale_entries_body(pqgpu.Context(0), sys.argv[1])
+print("STALE-OK")
+"""
+
+
+@pytest.mark.parametrize("name", ["edge_tiny_pages", "cfg2_v2_small"])
+def test_stale_entries_dropped(name):
+    """Table entries carry the build's generation stamp. A chunk whose walk reports success with the
+    right page count but whose table stores never landed (PQ_IX_TEST_SKIP_STORE, a hook of the
+    diagnostic library only: its slots are reserved and left as they were — here holding the
+    previous build's entries for the same chunk, same slots, same count) must not be trusted: its
+    entries are dropped as stale, the count no longer adds up, the chunk falls back to the host
+    walk, and the decode still equals the oracle."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "parquet-go-1_amd", "lib", "libpqgpu_diag.so")
+    assert os.path.exists(diag), "make -C parquet-go-1_amd diag"
+    env = dict(os.environ, PQGPU_LIB=diag)
+    env.pop("PQ_IX_TEST_SKIP_STORE", None)
+    tests = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", STALE_SCRIPT, name, tests, os.path.join(root, "parquet-go-1_amd"),
+                        os.path.join(root, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "STALE-OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_skip_store_hook_absent_from_product(gpu_ctx, monkeypatch):
+    """The production library ignores PQ_IX_TEST_SKIP_STORE: every chunk is walked on the device."""
+    data = pqtest.load("edge_tiny_pages")
+    f = pqgpu.File(data)
+    chunks = _all_chunks(f)
+    monkeypatch.setenv("PQ_IX_TEST_SKIP_STORE", "0")
+    ix = pqgpu.PageIndex.for_chunks(gpu_ctx, f, chunks, whole_file=True)
+    st = ix.stats()
+    assert st["fallback_chunks"] == 0 and st["stale_entries"] == 0, st
+    ix.close()

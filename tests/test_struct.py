@@ -232,6 +232,64 @@ def test_gpu_share_ancestors_detects_mismatch(gpu_ctx):
     b.close()
 
 
+def _three_leaf_file():
+    """a: list<struct<x: int32, b: list<struct<y: int32, z: int32>>>> with nulls at every level:
+    leaf x has one list level, leaves b.y and b.z two, and all three share a's list."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(77)
+    rows = []
+    for _ in range(3000):
+        if rng.random() < 0.05:
+            rows.append(None)
+            continue
+        elems = []
+        for _ in range(int(rng.integers(0, 4))):
+            if rng.random() < 0.1:
+                elems.append(None)
+                continue
+            bl = None if rng.random() < 0.1 else [
+                None if rng.random() < 0.1 else {"y": None if rng.random() < 0.2 else int(rng.integers(0, 1000)),
+                                                  "z": int(rng.integers(0, 1000))}
+                for _ in range(int(rng.integers(0, 4)))]
+            elems.append({"x": None if rng.random() < 0.2 else int(rng.integers(0, 1000)), "b": bl})
+        rows.append(elems)
+    inner = pa.struct([("y", pa.int32()), ("z", pa.int32())])
+    typ = pa.list_(pa.struct([("x", pa.int32()), ("b", pa.list_(inner))]))
+    buf = io.BytesIO()
+    pq.write_table(pa.table({"a": pa.array(rows, typ)}), buf, row_group_size=1000, data_page_size=2048,
+                   use_dictionary=False)
+    return buf.getvalue()
+
+
+@pytest.mark.gpu
+def test_gpu_share_ancestors_mixed_depths(gpu_ctx):
+    """Leaf b.y first shares one list level with the shallower leaf x, then two list levels with its
+    sibling b.z: b.z must take levels it shares with b.y from b.y (whose own result resolves level 0
+    through x), not from the chain's root x, which has no level 1. Every result keeps its contents."""
+    data = _three_leaf_file()
+    f, b, ids = _decode_all(gpu_ctx, data)
+    paths = f.column_paths()
+    ix, iy, iz = (paths.index(p) for p in ("a.list.element.x", "a.list.element.b.list.element.y",
+                                           "a.list.element.b.list.element.z"))
+    for rg in range(f.num_row_groups):
+        cx, cy, cz = ids[(rg, ix)], ids[(rg, iy)], ids[(rg, iz)]
+        before = {c: b.result(c) for c in (cx, cy, cz)}
+        assert b.share_ancestors(cx, cy)
+        assert b.share_ancestors(cy, cz)
+        assert b.share_ancestors(cz, cx)  # cz already follows cx through cy: no link back
+        for c in (cx, cy, cz):
+            r0, r1 = before[c], b.result(c)
+            assert len(r0.nested) == len(r1.nested)
+            for (o1, v1), (o2, v2) in zip(r0.nested, r1.nested):
+                np.testing.assert_array_equal(o1, o2)
+                np.testing.assert_array_equal(v1, v2)
+            assert [p for p, _ in r0.groups] == [p for p, _ in r1.groups]
+            for (_p1, g1), (_p2, g2) in zip(r0.groups, r1.groups):
+                np.testing.assert_array_equal(g1, g2)
+    b.close()
+
+
 @pytest.mark.gpu
 def test_gpu_share_ancestors_no_cycles(gpu_ctx):
     """Sharing links stay acyclic: a leaf cannot share with itself (an argument error), sharing a
