@@ -100,9 +100,16 @@ func toErr(rc C.int, e *C.pqgpu_error) error {
 // per GPU, like the reference's FileReader (file_reader.go:18).
 type Context struct{ c *C.pqgpu_ctx }
 
+// ErrABI reports a libpqgpu whose C ABI differs from the pqgpu.h this package
+// was compiled against (a stale header/library pair would otherwise bind silently).
+var ErrABI = errors.New("libpqgpu ABI version mismatch")
+
 // NewContext opens GPU `device`; it fails when no MI355X is visible (there is
-// no CPU fallback).
+// no CPU fallback) and when the loaded library's ABI is not PQGPU_ABI_VERSION.
 func NewContext(device int) (*Context, error) {
+	if got := int(C.pqgpu_abi_version()); got != int(C.PQGPU_ABI_VERSION) {
+		return nil, fmt.Errorf("%w: library %d, header %d", ErrABI, got, int(C.PQGPU_ABI_VERSION))
+	}
 	var e C.pqgpu_error
 	var c *C.pqgpu_ctx
 	if err := toErr(C.pqgpu_ctx_create(C.int(device), &c, &e), &e); err != nil {
@@ -276,6 +283,12 @@ type ChunkMeta struct {
 
 // AddChunk plans one column chunk whose pages are in buf (the library copies
 // the page bytes it needs before returning, so buf may be Go memory).
+//
+// It gives the reference's flat pageReader contract only (interfaces.go:11-18:
+// per page, values plus definition / repetition levels): the nested-array
+// thresholds of ColumnInfo (list / group definition levels) are left zero, so
+// no Arrow list offsets or struct bitmaps are emitted. Use AddFileChunk, which
+// takes them from the file's schema walk, for nested outputs.
 func (b *Batch) AddChunk(buf []byte, col ColumnInfo, meta ChunkMeta, validateCRC bool) (int32, error) {
 	var ci C.pqgpu_column_info
 	ci.physical_type = C.int32_t(col.PhysicalType)

@@ -271,6 +271,21 @@ DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, 
 // those (so every store instruction writes 1 KiB contiguous). A lane's second source block is the
 // next piece: lane l + 1's block (lane 63: lane 0's next block) by one lane shuffle, and only lane
 // 63's last piece loads its own.
+#ifndef PQ_COPY_NT
+#define PQ_COPY_NT 0  // copy_bytes_u: 1 non-temporal stores, 2 non-temporal loads and stores (experiments)
+#endif
+typedef uint32_t nt_v4u32 __attribute__((ext_vector_type(4)));
+DEV uint4 cp_ld16(const uint4 *p) {
+  if (PQ_COPY_NT >= 2) {
+    const nt_v4u32 v = __builtin_nontemporal_load((const nt_v4u32 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+DEV void cp_st16(uint4 *p, uint4 v) {
+  if (PQ_COPY_NT >= 1) __builtin_nontemporal_store(nt_v4u32{v.x, v.y, v.z, v.w}, (nt_v4u32 *)p);
+  else *p = v;
+}
 template <uint32_t U>
 DEV void copy_bytes_u(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
   if (n == 0) return;
@@ -293,7 +308,7 @@ DEV void copy_bytes_u(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid
     const uint64_t i = r0 + (uint64_t)wv * 64 * U + lane;
     uint4 a[U];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) a[u] = sb[i + 64 * u];
+    for (uint32_t u = 0; u < U; u++) a[u] = cp_ld16(&sb[i + 64 * u]);
     if (sa) {
       uint4 e = make_uint4(0u, 0u, 0u, 0u);
       if (lane == 63) e = sb[i + 64 * (U - 1) + 1];
@@ -302,11 +317,11 @@ DEV void copy_bytes_u(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid
         const uint4 o = (lane == 0 && u + 1 < U) ? a[u + 1] : a[u];  // what lane l - 1 takes from this lane
         uint4 b = make_uint4(shd(o.x), shd(o.y), shd(o.z), shd(o.w));
         if (lane == 63 && u + 1 == U) b = e;
-        d[i + 64 * u] = funnel16(a[u], b, sa);
+        cp_st16(&d[i + 64 * u], funnel16(a[u], b, sa));
       }
     } else {
 #pragma unroll
-      for (uint32_t u = 0; u < U; u++) d[i + 64 * u] = a[u];
+      for (uint32_t u = 0; u < U; u++) cp_st16(&d[i + 64 * u], a[u]);
     }
   }
   for (uint64_t i = r0 + tid; i < pieces; i += nt) d[i] = sa ? funnel16(sb[i], sb[i + 1], sa) : sb[i];

@@ -1640,13 +1640,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->n_level_seg = 0;
     for (uint32_t p : b->level_pages_bw1) b->n_level_seg += fits(p);
   }
-  {  // generic level streams: k_levels_segw takes the units whose stream fits its LDS stage when
-     // PQ_LV_SEGW=1 (measured slower than the list ranking on cfg4's list streams: off by default)
+  {  // generic level streams: k_levels_segw (segment speculation) takes the definition streams that
+     // fit its LDS stage (PQ_LV_SEGW=2, the default: Arrow's definition streams alternate 2-byte RLE
+     // runs with short literal runs, cfg4 k_levels 0.377 -> 0.269 ms); the repetition streams are
+     // maximal literal runs (64 B at bit width 1), which k_levels' stride prelude walks 64 at a time
+     // and on which segment speculation fails (PQ_LV_SEGW=1, every stream: 1.01 ms). 0: none.
     const char *lsg = getenv("PQ_LV_SEGW");
-    const bool seg = lsg && atoi(lsg) == 1;
+    const int segm = lsg ? atoi(lsg) : 2;
     auto fits = [&](uint32_t u) {
       const PageDesc &pd = b->pages[u >> 1];
-      return seg && (uint64_t)((u & 1) ? pd.def_len : pd.rep_len) + 24 <= kSgwStageHost;
+      return (segm == 1 || (segm == 2 && (u & 1))) && (uint64_t)((u & 1) ? pd.def_len : pd.rep_len) + 24 <= kSgwStageHost;
     };
     std::stable_partition(b->level_pages.begin(), b->level_pages.end(), fits);
     b->n_level_units_seg = 0;
@@ -2704,11 +2707,9 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
   ix->metas.assign(metas, metas + n_chunks);
   ix->chunks.resize(n_chunks);
   uint64_t cap = 4096;
-  // test knobs: PQ_IX_CAP forces the first table capacity (drives the grow path; PQ_IX_NOGROW=1
-  // the overflow path),
-  // PQ_IX_POOL=1 takes the scratch from the stream-ordered pool (the DESIGN.md §9 experiment)
+  // test knobs (tests/test_page_index.py): PQ_IX_CAP forces the first table capacity (drives the
+  // grow path; PQ_IX_NOGROW=1 the overflow path)
   const char *cap_env = getenv("PQ_IX_CAP");
-  const bool use_pool = getenv("PQ_IX_POOL") && atoi(getenv("PQ_IX_POOL")) == 1;
   const bool no_grow = getenv("PQ_IX_NOGROW") && atoi(getenv("PQ_IX_NOGROW")) == 1;  // with PQ_IX_CAP
   for (int32_t c = 0; c < n_chunks; c++) {
     const pqgpu_chunk_meta &m = metas[c];
@@ -2731,13 +2732,7 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
     cap = std::min<uint64_t>(cap, 1u << 26);
     size_t dcap = 0;
     const size_t bytes = 256 + res_bytes + cap * sizeof(PageIxEntry);
-    void *d = nullptr;
-    if (use_pool) {
-      dcap = bytes;
-      if (hipMallocAsync(&d, bytes, s) != hipSuccess) d = nullptr;
-    } else {
-      d = ctx->scratch_get(bytes, &dcap);
-    }
+    void *d = ctx->scratch_get(bytes, &dcap);  // hipMalloc'd, never stream-ordered
     if (!d) HIPCHECK(hipErrorOutOfMemory, err);
     uint8_t *D = (uint8_t *)d;
     uint32_t *d_n = (uint32_t *)D;
@@ -2764,7 +2759,6 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
     ix->polls += polls;
-    if (polls && getenv("PQ_IX_DEBUG")) fprintf(stderr, "[ix] results complete after %d polls\n", polls);
     if (he == hipSuccess) he = hipMemcpyAsync(&n, d_n, 4, hipMemcpyDeviceToHost, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
     const bool grow = he == hipSuccess && n > cap && cap < (1u << 26) && attempt < (no_grow ? 0 : 3);
@@ -2790,20 +2784,10 @@ int pqgpu_page_index_build(pqgpu_ctx *ctx, const void *dev_bytes, int64_t file_o
       }
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);  // the scratch is free for the next build
-    if (use_pool) (void)hipFreeAsync(d, s);
-    else ctx->scratch_put(d, dcap);
+    ctx->scratch_put(d, dcap);
     HIPCHECK(he, err);
     if (!grow) break;
     cap = (uint64_t)n * 2 + 4096;
-  }
-  if (getenv("PQ_IX_DEBUG")) {
-    fprintf(stderr, "[ix] n=%u cap=%llu\n", n, (unsigned long long)cap);
-    for (int32_t c = 0; c < n_chunks; c++)
-      fprintf(stderr, "[ix] chunk %d start %lld total %lld status %u npages %u fail %u\n", c,
-              (long long)ix->chunks[c].start, (long long)ix->chunks[c].total, ix->chunks[c].status,
-              ix->chunks[c].npages, ix->chunks[c].fail_page);
-    for (const auto &x : ix->entries)
-      fprintf(stderr, "[ix]   e chunk %u seq %u off %lld type %d cs %d\n", x.chunk, x.seq, (long long)x.hdr_off, x.type, x.csize);
   }
   // entries stamped by another build (scratch reused: a slot this build reserved but whose store
   // never landed) or of a chunk id outside the build cannot come from this build's walk: dropped.

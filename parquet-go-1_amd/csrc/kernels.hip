@@ -549,6 +549,7 @@ struct LevelLDS {
     uint2 rbuf[kLvChunk / 2];       // generic widths: the chunk's run-table entries
   };
   uint32_t tb_k[kLvTileBuf], tb_r[kLvTileBuf], ntb;  // generic widths: fill-tile starts of the chunk
+  uint32_t sp_e, sp_d, sp_r;                          // generic widths: the stride prelude's chain state
 };
 
 // Fast candidate at stream position c: a header varint of at most 4 bytes whose run is
@@ -652,6 +653,74 @@ DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uin
   lv_emit_run<BW1>(sk, L.stage, sb, send, f, cnt, bp, value);
 }
 
+// The stride prelude of lv_walk (generic widths; one wave, wave-uniform state): from chain position
+// `entry` (value `done`, run-table entry `runs_done`), follow runs of at least kLvStrideMin stream
+// bytes 64 at a time (lane k: the header k runs on, if the runs between have this run's header;
+// the leading lanes with exactly that header are chain nodes by induction, and lane m's position is
+// the true next header whatever it holds). Each taken run goes straight to the run table, with
+// the fill tiles whose first value it holds. A header the fast form does not take (long varint,
+// zero count, run past the stream, RLE value >= 2^bw), a short run or the stream end stops it;
+// runs past the one that reaches `need` are never read (decodePackedArray helpers.go:133-149).
+#ifndef PQ_LV_STRIDE
+#define PQ_LV_STRIDE 1
+#endif
+constexpr uint32_t kLvStrideMin = 32;
+DEV void lv_stride(LevelSink &sk, uint32_t need, uint32_t &entry, uint32_t &done, uint32_t &runs_done) {
+  const uint8_t *sg = sk.s;
+  const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3, lane = lane_id();
+  uint32_t pos = entry, dn = done, rd = runs_done;
+  while (dn < need && pos < n) {
+    const uint64_t x0 = ld64(sg + pos);  // bytes past the stream end are never used (checks below)
+    const uint32_t u0 = sgpr((uint32_t)x0), u1 = sgpr((uint32_t)(x0 >> 32));
+    const uint32_t tm = ~u0 & 0x80808080u;
+    if (!tm) break;
+    const uint32_t Lv = (uint32_t)(__builtin_ctz(tm) >> 3) + 1;
+    const uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
+    const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+    const uint32_t cnt = h >> 1, isbp = h & 1u;
+    const uint64_t adv = isbp ? Lv + (uint64_t)cnt * bw : (uint64_t)(Lv + rs);
+    const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
+    const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
+    const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
+    if (!(ok && adv >= kLvStrideMin)) break;
+    const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - dn;
+    const uint64_t Pk = (uint64_t)pos + (uint64_t)lane * adv;
+    bool same = lane == 0;
+    uint32_t vk = val;
+    if (lane > 0 && Pk + adv <= n) {
+      const uint64_t xk = ld64(sg + Pk);
+      const uint32_t a0 = (uint32_t)xk;
+      const uint32_t tk = ~a0 & 0x80808080u;
+      const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
+      const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
+      const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
+      const uint32_t rk = (uint32_t)(xk >> (8 * Lk));
+      vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
+      same = tk != 0 && Lk == Lv && hk == h && (isbp || bw >= 32 || (vk >> bw) == 0);
+    }
+    const uint64_t nb = ~__ballot(same);
+    const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);  // runs that cover rem
+    const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, mneed);
+    if (lane < m) {
+      const uint32_t f = dn + lane * nv, c = min(nv, need - f), idx = rd + lane;
+      sk.runs[idx] = make_uint2(f, isbp ? 0x80000000u | vk : vk);
+      if (sk.ntiles) {  // fill tiles whose first value lies in [f, f + c): tile k > 0 starts at k * T - a
+        const uint64_t a = sk.tile_a;
+        uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
+        const uint64_t khi = min(((uint64_t)f + c - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+        for (; k <= khi; k++) sk.trun[2 * k] = idx;
+      }
+    }
+    rd += m;
+    if (m == mneed) { dn = need; break; }
+    dn += m * nv;
+    pos += (uint32_t)(m * adv);
+  }
+  entry = pos;
+  done = dn;
+  runs_done = rd;
+}
+
 // Decode `need` level values of one stream into the sink; every thread of the workgroup
 // calls this (control flow outside per-lane work is workgroup-uniform). Chunks are fixed
 // stream ranges [k * kLvChunk, (k + 1) * kLvChunk); the chain enters chunk k where it left
@@ -709,6 +778,28 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
   for (;;) {
     if (done >= need) break;
     if (entry >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
+    if constexpr (!BW1) {
+      if (PQ_LV_STRIDE) {
+        // Stride prelude (wave 0, straight from global memory; the run-header chain of hyb_scan's
+        // prelude): while the chain's runs are long (>= kLvStrideMin stream bytes) and alike, lane k
+        // decodes the header that would start k runs on if the runs between had this run's header.
+        // Writers emit maximal literal runs back to back (Arrow's level streams: 63 groups, 64 B
+        // at bit width 1, 127 B at 2), so the leading lanes with that exact header are chain nodes
+        // by induction: up to 64 runs per step go to the run table (and the fill-tile starts they
+        // hold), with no LDS staging and no list ranking. Anything else stops the prelude and the
+        // chunk walk below takes the chain from there with the exact semantics.
+        if (tid < 64) lv_stride(sk, need, entry, done, runs_done);
+        if (tid == 0) { L.sp_e = entry; L.sp_d = done; L.sp_r = runs_done; }
+        wg_barrier();
+        entry = L.sp_e;
+        done = L.sp_d;
+        runs_done = L.sp_r;
+        sk.nruns = runs_done;
+        sk.covered = min(done, need);
+        if (done >= need) break;
+        if (entry >= n) { sk.error(done, PQ_ERR_EOF); break; }
+      }
+    }
     const uint32_t cs = entry - entry % kLvChunk, e0 = entry - cs;
     const uint32_t clen = min(kLvChunk, n - cs), send = cs + kLvStageB;
     if (fetched != cs) { fetch(cs); fetched = cs; }
@@ -3485,7 +3576,7 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
           if (al16) {
             uint4 *dst = (uint4 *)dst0;
 #pragma unroll
-            for (uint32_t q = 0; q < 2; q++) dst[q * 64 + lane] = xw[xsw(q * 64 + lane)];
+            for (uint32_t q = 0; q < 2; q++) cp_st16(&dst[q * 64 + lane], xw[xsw(q * 64 + lane)]);
           } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
             const uint32_t bytes = 2048, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
             const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;

@@ -269,7 +269,7 @@ struct IxChunkArgs {
 __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t len, int64_t file_off,
                                                   const IxChunkArgs args, uint32_t chunk0, uint4 *res_in,
                                                   PageIxEntry *table_in, uint32_t *table_n, uint32_t table_cap,
-                                                  uint32_t gen, uint32_t sys_fence, uint32_t test_skip) {
+                                                  uint32_t gen, uint32_t test_skip) {
   __shared__ TFrame stk[kIxDepth];
   const uint8_t *buf = gp(buf_in);
   PageIxEntry *table = gp(table_in);
@@ -338,10 +338,7 @@ __global__ void __launch_bounds__(64) k_page_walk(const uint8_t *buf_in, int64_t
     }
   }
   if (status == IX_OK && seq > flushed && !flush(seq - flushed)) status = IX_FALLBACK;
-  // PQ_IX_FENCE=1 (the DESIGN.md §9 experiment): a system-scope release after the walk's stores
-  if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) gp(res_in)[c] = make_uint4(status, status == IX_OK ? seq : 0u, seq, gen);
-  if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // ---------------------------------------------------------------------------
@@ -384,7 +381,7 @@ constexpr uint32_t kCrcThreads = 256;
 
 __global__ void __launch_bounds__(kCrcThreads) k_page_crc(const uint8_t *buf_in, int64_t len, int64_t file_off,
                                                           PageIxEntry *table_in, const uint32_t *table_n_in,
-                                                          uint32_t table_cap, uint32_t sys_fence) {
+                                                          uint32_t table_cap) {
   __shared__ uint32_t T[4][256];
   __shared__ uint32_t wred[kCrcThreads / 64];
   const uint8_t *buf = gp(buf_in);
@@ -433,7 +430,6 @@ __global__ void __launch_bounds__(kCrcThreads) k_page_crc(const uint8_t *buf_in,
       uint32_t tot = 0;
       for (uint32_t w = 0; w < kCrcThreads / 64; w++) tot ^= wred[w];
       table[e].flags = fl | IXF_CRC_CHECKED | (tot == (uint32_t)h.crc ? IXF_CRC_OK : 0u);
-      if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     wg_barrier();
   }
@@ -469,7 +465,6 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
                             uint32_t nchunks, uint4 *res, PageIxEntry *table, uint32_t *table_n, uint32_t table_cap,
                             int validate_crc, uint32_t gen, hipStream_t s) {
   if (!nchunks) return hipSuccess;
-  const uint32_t sys_fence = getenv("PQ_IX_FENCE") && atoi(getenv("PQ_IX_FENCE")) == 1;
 #ifdef PQ_DIAG_STAMPS
   // diagnostic build only (tests/test_page_index.py): one chunk's table stores are dropped
   const char *skip_env = getenv("PQ_IX_TEST_SKIP_STORE");
@@ -483,11 +478,11 @@ hipError_t launch_page_walk(const uint8_t *buf, int64_t len, int64_t file_off, c
     IxChunkArgs a;
     memset(&a, 0, sizeof(a));
     memcpy(a.c, chunks + c0, n * sizeof(PageIxChunk));
-    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap, gen, sys_fence, test_skip);
+    hipLaunchKernelGGL(k_page_walk, dim3(n), dim3(64), 0, s, buf, len, file_off, a, c0, res, table, table_n, table_cap, gen, test_skip);
   }
   if (validate_crc)
     hipLaunchKernelGGL(k_page_crc, dim3(2048), dim3(kCrcThreads), 0, s, buf, len, file_off, table,
-                       (const uint32_t *)table_n, table_cap, sys_fence);
+                       (const uint32_t *)table_n, table_cap);
   return hipGetLastError();
 }
 
