@@ -413,7 +413,8 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // B, which gathers nothing (tools/ubench/ba_ubench.hip: the emit 0.433 -> 0.351 ms, with
 // non-temporal payload stores 0.288 ms).
 #ifndef PQ_BA_PA
-#define PQ_BA_PA 1
+#define PQ_BA_PA 0  // product kernel: 128 VGPRs with 68 B of spills at 4 waves per SIMD; cfg3 k_ba_emit
+                    // 0.428 ms against 0.352 ms without (profiles/r05_s4_probe_ba_emit.txt): off
 #endif
 template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool PA = false, class EL>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,

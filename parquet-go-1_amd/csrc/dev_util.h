@@ -272,7 +272,10 @@ DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, 
 // next piece: lane l + 1's block (lane 63: lane 0's next block) by one lane shuffle, and only lane
 // 63's last piece loads its own.
 #ifndef PQ_COPY_NT
-#define PQ_COPY_NT 0  // copy_bytes_u: 1 non-temporal stores, 2 non-temporal loads and stores (experiments)
+// copy_bytes_u (PLAIN copies) and k_values_delta's transposed output: 2 non-temporal loads and
+// stores, 1 stores only, 0 neither. Streams read or written once need no L2 residency; cfg2 step
+// 0.478 -> 0.453 ms with 2, 0.464 ms with 1, on one box (profiles/r05_s5_probe_copy_nt.txt)
+#define PQ_COPY_NT 2
 #endif
 typedef uint32_t nt_v4u32 __attribute__((ext_vector_type(4)));
 DEV uint4 cp_ld16(const uint4 *p) {

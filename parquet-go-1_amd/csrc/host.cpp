@@ -476,7 +476,7 @@ struct pqgpu_batch {
   uint64_t o_snappy = 0;
   std::vector<WorkItem> items;
   std::vector<uint32_t> level_pages_bw1;  // flat OPTIONAL pages: k_levels_seg's first, then the others
-  uint32_t n_level_seg = 0, n_level_units_seg = 0;
+  uint32_t n_level_seg = 0, n_level_units_seg = 0, n_level_units_hyb = 0;
   std::vector<uint32_t> delta_pages;      // tiled DELTA pages
   std::vector<uint64_t> dblk_base;        // [np] first DeltaBlk of each page
   uint64_t dblk_total = 0;
@@ -1654,6 +1654,13 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     std::stable_partition(b->level_pages.begin(), b->level_pages.end(), fits);
     b->n_level_units_seg = 0;
     for (uint32_t u : b->level_pages) b->n_level_units_seg += fits(u);
+    // then the repetition streams for k_levels_hyb (PQ_LV_HYB=0: the list ranking of k_levels)
+    const char *lh = getenv("PQ_LV_HYB");
+    const bool hyb = !(lh && atoi(lh) == 0);
+    auto is_hyb = [&](uint32_t u) { return hyb && !(u & 1); };
+    std::stable_partition(b->level_pages.begin() + b->n_level_units_seg, b->level_pages.end(), is_hyb);
+    b->n_level_units_hyb = 0;
+    for (size_t k = b->n_level_units_seg; k < b->level_pages.size(); k++) b->n_level_units_hyb += is_hyb(b->level_pages[k]);
   }
   b->l_level_bw1 = take(b->level_pages_bw1.size() * 4);
   b->l_scan = take(b->scan_pages.size() * 4);
@@ -1942,6 +1949,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
   l.n_level_pages_seg = b->n_level_seg;
   l.n_level_units_seg = b->n_level_units_seg;
+  l.n_level_units_hyb = b->n_level_units_hyb;
   l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
   l.lf_list = (const uint32_t *)(A + b->l_lf_list);
   l.n_lf_list = (uint32_t)b->lf_list.size();

@@ -77,6 +77,7 @@ struct LaunchLists {
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   uint32_t n_level_pages_seg;  // the first n of them go to k_levels_seg (def stream fits its LDS stage)
   uint32_t n_level_units_seg;  // the first n level_pages units go to k_levels_segw (stream fits its stage)
+  uint32_t n_level_units_hyb;  // the next n (repetition streams) to k_levels_hyb, the rest to k_levels
   uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
   const uint32_t *scan_pages; uint32_t n_scan_pages;     // pages with hybrid value streams (dict / rle bool)
   const uint32_t *base_chunks; uint32_t n_base_chunks;   // chunks needing value/record bases

@@ -148,7 +148,9 @@ struct ScanLDS {
   uint32_t ctl_pos, ctl_done, ctl_stop;
 };
 
-template <class Sink>
+// PRE: the stride prelude from global memory first (a stream that is one run shape throughout is
+// then walked without staging it); without it every step of the walk reads the LDS window.
+template <class Sink, bool PRE = true>
 DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink,
                       unsigned long long *dbg = nullptr) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
@@ -197,7 +199,7 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
   // page's payload is read later, by the tiles that decode it). Anything else (a short run, a run
   // that differs, the stream end, an error) stops the prelude; the windowed walk below takes over
   // at that position with the reference's exact semantics.
-  if (wv == 0) {
+  if (PRE && wv == 0) {
     const uint8_t *sg = gp_u64<const uint8_t>((uint64_t)(uintptr_t)s);
     while (done < need && pos < n) {
       const uint64_t x0 = ld64(sg + pos);  // bytes past the stream end are never used (checks below)
@@ -238,11 +240,13 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
       done += m * nv;
       pos += (uint32_t)(m * adv);
     }
-    if (lane == 0) { L.ctl_pos = pos; L.ctl_done = done; }
   }
-  wg_barrier();
-  pos = L.ctl_pos;
-  done = L.ctl_done;
+  if (PRE) {
+    if (threadIdx.x == 0) { L.ctl_pos = pos; L.ctl_done = done; }
+    wg_barrier();
+    pos = L.ctl_pos;
+    done = L.ctl_done;
+  }
   if (done >= need) {
     if (wv == 0) st.flush(56);
     return done;
@@ -654,67 +658,126 @@ DEV void lv_fill_run(LevelLDS &L, LevelSink &sk, uint32_t sb, uint32_t send, uin
 }
 
 // The stride prelude of lv_walk (generic widths; one wave, wave-uniform state): from chain position
-// `entry` (value `done`, run-table entry `runs_done`), follow runs of at least kLvStrideMin stream
-// bytes 64 at a time (lane k: the header k runs on, if the runs between have this run's header;
-// the leading lanes with exactly that header are chain nodes by induction, and lane m's position is
-// the true next header whatever it holds). Each taken run goes straight to the run table, with
-// the fill tiles whose first value it holds. A header the fast form does not take (long varint,
-// zero count, run past the stream, RLE value >= 2^bw), a short run or the stream end stops it;
-// runs past the one that reaches `need` are never read (decodePackedArray helpers.go:133-149).
+// `entry` (value `done`, run-table entry `runs_done`), follow the chain up to 256 runs per step.
+// Candidate k (four per lane) decodes the header k runs on, assuming the runs between have this
+// run's header; the leading candidates with exactly that header are chain nodes by induction, and
+// candidate m's position is the true next header whatever it holds. Writers emit maximal literal
+// runs back to back (Arrow's repetition streams: 64 B at bit width 1), so a step takes many runs;
+// a short run among them (an RLE run) is a step of its own. Each taken run goes straight to the
+// run table, with the fill tiles whose first value it holds. A header the fast form does not take
+// (long varint, zero count, run past the stream, RLE value >= 2^bw), kLvShortMax short-run steps
+// in a row or the stream end stop it and the chunk walk takes the chain from there; runs past the
+// one that reaches `need` are never read (decodePackedArray helpers.go:133-149).
+// Software-pipelined: a step's loads bring the next step's first header too (candidate m's bytes,
+// or candidate 0's, which reads 256 runs on), so the next step's loads are issued before this
+// step's run-table stores, and each step waits for one load round trip (vmcnt counts stores too).
 #ifndef PQ_LV_STRIDE
 #define PQ_LV_STRIDE 1
 #endif
-constexpr uint32_t kLvStrideMin = 32;
+constexpr uint32_t kLvStrideMin = 32;  // runs at least this long are "long"
+constexpr uint32_t kLvShortMax = 1;    // consecutive steps of short runs before the chunk walk takes over
+                                       // (each step is a memory round trip: repetition streams with RLE
+                                       // runs among the literal ones take k_levels_hyb instead)
+struct StrideHdr {
+  uint32_t Lv, h, cnt, isbp, val, ok;
+  uint64_t adv;
+};
+DEV StrideHdr stride_hdr(uint64_t x, uint32_t pos, uint32_t n, uint32_t bw, uint32_t rs) {
+  StrideHdr H;
+  const uint32_t u0 = (uint32_t)x;
+  const uint32_t tm = ~u0 & 0x80808080u;
+  H.Lv = (uint32_t)(__builtin_ctz(tm | 0x80000000u) >> 3) + 1;
+  const uint32_t y = (H.Lv >= 4 ? u0 : (u0 & ((1u << (8 * H.Lv)) - 1u))) & 0x7f7f7f7fu;
+  H.h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
+  H.cnt = H.h >> 1;
+  H.isbp = H.h & 1u;
+  H.adv = H.isbp ? H.Lv + (uint64_t)H.cnt * bw : (uint64_t)(H.Lv + rs);
+  const uint32_t rv = (uint32_t)(x >> (8 * H.Lv));
+  H.val = H.isbp ? pos + H.Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
+  H.ok = tm != 0 && H.cnt != 0 && (uint64_t)pos + H.adv <= n && (H.isbp || bw >= 32 || (H.val >> bw) == 0);
+  return H;
+}
+constexpr uint32_t kLvStrideJ = 4;  // headers per lane per step: up to 256 runs per step
 DEV void lv_stride(LevelSink &sk, uint32_t need, uint32_t &entry, uint32_t &done, uint32_t &runs_done) {
+  constexpr uint32_t J = kLvStrideJ, NJ = 64 * J;
   const uint8_t *sg = sk.s;
   const uint32_t n = sk.n, bw = sk.bw, rs = (bw + 7) >> 3, lane = lane_id();
   uint32_t pos = entry, dn = done, rd = runs_done;
-  while (dn < need && pos < n) {
-    const uint64_t x0 = ld64(sg + pos);  // bytes past the stream end are never used (checks below)
-    const uint32_t u0 = sgpr((uint32_t)x0), u1 = sgpr((uint32_t)(x0 >> 32));
-    const uint32_t tm = ~u0 & 0x80808080u;
-    if (!tm) break;
-    const uint32_t Lv = (uint32_t)(__builtin_ctz(tm) >> 3) + 1;
-    const uint32_t y = (Lv >= 4 ? u0 : (u0 & ((1u << (8 * Lv)) - 1u))) & 0x7f7f7f7fu;
-    const uint32_t h = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
-    const uint32_t cnt = h >> 1, isbp = h & 1u;
-    const uint64_t adv = isbp ? Lv + (uint64_t)cnt * bw : (uint64_t)(Lv + rs);
-    const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
-    const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
-    const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
-    if (!(ok && adv >= kLvStrideMin)) break;
-    const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - dn;
-    const uint64_t Pk = (uint64_t)pos + (uint64_t)lane * adv;
-    bool same = lane == 0;
-    uint32_t vk = val;
-    if (lane > 0 && Pk + adv <= n) {
-      const uint64_t xk = ld64(sg + Pk);
-      const uint32_t a0 = (uint32_t)xk;
-      const uint32_t tk = ~a0 & 0x80808080u;
-      const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
-      const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
-      const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
-      const uint32_t rk = (uint32_t)(xk >> (8 * Lk));
-      vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
-      same = tk != 0 && Lk == Lv && hk == h && (isbp || bw >= 32 || (vk >> bw) == 0);
-    }
-    const uint64_t nb = ~__ballot(same);
-    const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);  // runs that cover rem
-    const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, mneed);
-    if (lane < m) {
-      const uint32_t f = dn + lane * nv, c = min(nv, need - f), idx = rd + lane;
-      sk.runs[idx] = make_uint2(f, isbp ? 0x80000000u | vk : vk);
-      if (sk.ntiles) {  // fill tiles whose first value lies in [f, f + c): tile k > 0 starts at k * T - a
-        const uint64_t a = sk.tile_a;
-        uint64_t k = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
-        const uint64_t khi = min(((uint64_t)f + c - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
-        for (; k <= khi; k++) sk.trun[2 * k] = idx;
+  if (dn < need && pos < n) {
+    // candidate k = 64 j + lane reads the header k runs on; k = 0 (lane 0, j = 0) instead reads the
+    // one NJ runs on: the next step's first header when every candidate matches
+    auto load_lanes = [&](uint32_t at, uint64_t adv, uint64_t (&x)[J]) {
+#pragma unroll
+      for (uint32_t j = 0; j < J; j++) {
+        const uint32_t k = 64 * j + lane;
+        const uint64_t Pk = (uint64_t)at + (uint64_t)(k ? k : NJ) * adv;
+        x[j] = Pk < n ? ld64(sg + Pk) : 0ull;  // bytes past the stream end are never used (checks below)
+      }
+    };
+    const uint64_t x0 = ld64(sg + pos);
+    StrideHdr H = stride_hdr(((uint64_t)sgpr((uint32_t)(x0 >> 32)) << 32) | sgpr((uint32_t)x0), pos, n, bw, rs);
+    uint32_t shorts = 0;  // consecutive steps of short runs
+    if (H.ok && H.adv >= kLvStrideMin) {
+      uint64_t xk[J];
+      load_lanes(pos, H.adv, xk);
+      for (;;) {
+        const uint32_t nv = H.isbp ? H.cnt * 8 : H.cnt, rem = need - dn;
+        uint32_t vk[J];
+        uint32_t m = NJ;  // the first candidate that is not a node of this run shape
+#pragma unroll
+        for (uint32_t j = 0; j < J; j++) {
+          const uint32_t k = 64 * j + lane;
+          const uint64_t Pk = (uint64_t)pos + (uint64_t)k * H.adv;
+          bool same = k == 0;
+          vk[j] = H.isbp ? (uint32_t)Pk + H.Lv : H.val;
+          if (k > 0 && Pk + H.adv <= n) {
+            const StrideHdr K = stride_hdr(xk[j], (uint32_t)Pk, n, bw, rs);
+            vk[j] = K.val;
+            same = K.ok && K.Lv == H.Lv && K.h == H.h;
+          }
+          const uint64_t nb = ~__ballot(same);
+          if (m == NJ && nb) m = 64 * j + (uint32_t)__builtin_ctzll(nb);  // (wave-uniform)
+        }
+        const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);  // runs that cover rem
+        m = min(m, mneed);
+        const bool fin = m == mneed;
+        const uint32_t npos = pos + (uint32_t)(m * H.adv);
+        // the next step's first header (candidate m's bytes; candidate 0's NJ runs on) and its loads
+        const uint32_t jm = (m & (NJ - 1)) >> 6, lm = m & 63u;
+        uint64_t xm = xk[0];
+#pragma unroll
+        for (uint32_t j = 1; j < J; j++) xm = jm == j ? xk[j] : xm;
+        const uint64_t nx = ((uint64_t)rdlane((uint32_t)(xm >> 32), lm) << 32) | rdlane((uint32_t)xm, lm);
+        const StrideHdr N = stride_hdr(nx, npos, n, bw, rs);
+        // a short run (an RLE run among literal runs) is taken as a step of its own, while such steps
+        // are rare: after kLvShortMax of them in a row the chunk walk takes over
+        shorts = N.adv < kLvStrideMin ? shorts + 1 : 0;
+        const bool go = !fin && npos < n && N.ok && shorts <= kLvShortMax;
+        uint64_t nxk[J];
+        if (go) load_lanes(npos, N.adv, nxk);
+#pragma unroll
+        for (uint32_t j = 0; j < J; j++) {  // this step's runs (stores issued after the next step's loads)
+          const uint32_t k = 64 * j + lane;
+          if (k >= m) continue;
+          const uint32_t f = dn + k * nv, c = min(nv, need - f), idx = rd + k;
+          sk.runs[idx] = make_uint2(f, H.isbp ? 0x80000000u | vk[j] : vk[j]);
+          if (sk.ntiles) {  // fill tiles whose first value lies in [f, f + c): tile t > 0 starts at t * T - a
+            const uint64_t a = sk.tile_a;
+            uint64_t t = f == 0 ? 0 : ((uint64_t)f + a + kLfTile - 1) / kLfTile;
+            const uint64_t thi = min(((uint64_t)f + c - 1 + a) / kLfTile, (uint64_t)sk.ntiles - 1);
+            for (; t <= thi; t++) sk.trun[2 * t] = idx;
+          }
+        }
+        rd += m;
+        if (fin) { dn = need; break; }
+        dn += m * nv;
+        pos = npos;
+        if (!go) break;
+        H = N;
+#pragma unroll
+        for (uint32_t j = 0; j < J; j++) xk[j] = nxk[j];
       }
     }
-    rd += m;
-    if (m == mneed) { dn = need; break; }
-    dn += m * nv;
-    pos += (uint32_t)(m * adv);
   }
   entry = pos;
   done = dn;
@@ -774,12 +837,14 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
       atomicAdd(&L.nput, 1u);
     }
   };
-  fetch(0);
+  bool try_stride = true;  // (generic widths) the stride prelude at the top of the next chunk
+  if (BW1 || !PQ_LV_STRIDE) fetch(0);  // (with the stride prelude: fetched when the chunk walk needs it)
+  else fetched = ~0u;
   for (;;) {
     if (done >= need) break;
     if (entry >= n) { sk.error(done, PQ_ERR_EOF); break; }  // next header read at EOF
     if constexpr (!BW1) {
-      if (PQ_LV_STRIDE) {
+      if (PQ_LV_STRIDE && try_stride) {  // (workgroup-uniform)
         // Stride prelude (wave 0, straight from global memory; the run-header chain of hyb_scan's
         // prelude): while the chain's runs are long (>= kLvStrideMin stream bytes) and alike, lane k
         // decodes the header that would start k runs on if the runs between had this run's header.
@@ -791,6 +856,7 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         if (tid < 64) lv_stride(sk, need, entry, done, runs_done);
         if (tid == 0) { L.sp_e = entry; L.sp_d = done; L.sp_r = runs_done; }
         wg_barrier();
+        try_stride = L.sp_r != runs_done;  // (a chunk walk follows; try again only after a step that took runs)
         entry = L.sp_e;
         done = L.sp_d;
         runs_done = L.sp_r;
@@ -2186,6 +2252,65 @@ __global__ void __launch_bounds__(kLvThreads) __attribute__((amdgpu_waves_per_eu
   }
   st.lap(6);
   st.flush(0);
+}
+
+// k_levels_hyb: generic level streams made of long literal runs (repetition streams: Arrow writes
+// maximal literal runs, 64 B at bit width 1, with an RLE run now and then) walked by hyb_scan, the
+// dictionary index walker of k_scan_runs, from its 16 KiB LDS windows: runs of 64 stream bytes or
+// more by stride speculation (up to 64 per step), the others by speculative header decode 64
+// stream bytes at a time — every step an LDS round trip, where k_levels' list ranking pays ~10
+// workgroup barriers per 2 KiB and a walk from global memory a memory round trip per step. Writes
+// the same run table and fill-tile markers as k_levels (hybrid_decoder.go:81-165 through
+// decodePackedArray helpers.go:133-149: runs past the one that reaches num_values are never read,
+// an error is the page's at the value where next() meets it).
+struct LvRunSink {
+  uint2 *runs;
+  uint32_t *trun;
+  uint32_t tile_a, ntiles;
+  uint32_t nruns;  // uniform
+  uint32_t err_code, err_pos;
+  DEV void window(bool active, uint32_t first, uint32_t cnt, bool bp, uint32_t value, uint32_t, const uint32_t *,
+                  uint32_t) {
+    const uint64_t m = __ballot(active);
+    if (active) {
+      const uint32_t idx = nruns + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+      runs[idx] = make_uint2(first, bp ? 0x80000000u | value : value);
+      if (ntiles) {  // fill tiles whose first value lies in [first, first + cnt): tile k > 0 starts at k * T - a
+        const uint64_t a = tile_a;
+        uint64_t k = first == 0 ? 0 : ((uint64_t)first + a + kLfTile - 1) / kLfTile;
+        const uint64_t khi = min(((uint64_t)first + cnt - 1 + a) / kLfTile, (uint64_t)ntiles - 1);
+        for (; k <= khi; k++) trun[2 * k] = idx;
+      }
+    }
+    nruns += (uint32_t)__popcll(m);
+  }
+  DEV void error(uint32_t pos, uint32_t code) {
+    if (!err_code) { err_code = code; err_pos = pos; }
+  }
+};
+__global__ void __launch_bounds__(256) k_levels_hyb(BatchDev b_in, const uint32_t *units) {
+  const BatchDev b = global_view(b_in);
+  __shared__ ScanLDS lds;
+  const uint32_t u = units[blockIdx.x], pi = u >> 1, which = u & 1;
+  const bool rep = which == 0;
+  const PageDesc pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t ns = pd.num_slots;
+  LvRunSink sk{b.lv_runs + b.lv_run_base[2 * pi + which], b.lv_tile_run + 2 * (uint64_t)b.lv_tile0[pi] + which,
+               (uint32_t)(pd.slot_base & (kLfTile - 1)), lf_tiles(pd.slot_base, ns), 0u, 0u, 0u};
+  if (!rep && threadIdx.x == 0) b.page_nn[pi] = 0;  // the fill kernels add the page's non-null count
+  uint32_t done = 0;
+  if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
+    if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
+  } else if (ns) {
+    done = hyb_scan<LvRunSink, false>(lds, gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off),
+                                      rep ? pd.rep_len : pd.def_len, (uint32_t)(rep ? cd.rep_bw : cd.def_bw), ns, sk);
+  }
+  if (threadIdx.x == 0) {  // wave 0 walked: its sink holds the run count and the error
+    b.lv_meta[4 * pi + 2 * which] = sk.nruns;
+    b.lv_meta[4 * pi + 2 * which + 1] = sk.err_code ? 0u : min(done, ns);  // a failed page is not expanded
+    if (sk.err_code) report(b, pd.chunk, 1, pd.page_in_chunk, rep ? ST_REP : ST_DEF, sk.err_pos, sk.err_code);
+  }
 }
 
 // k_level_fill: the run tables of the generic level streams expanded, one workgroup per fill
@@ -4482,10 +4607,12 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
     const char *lw = getenv("PQ_LV_WAVE");
     if (lw && atoi(lw) == 1) {
       hipLaunchKernelGGL(k_levels_w, dim3(l.n_level_pages), dim3(64), 0, s, b, l.level_pages);
-    } else {  // streams that fit k_levels_segw's stage first (host order), then the list-ranking kernel
-      const uint32_t nseg = l.n_level_units_seg, nrest = l.n_level_pages - nseg;
+    } else {  // host order: streams that fit k_levels_segw's stage, repetition streams for k_levels_hyb,
+              // then the list-ranking kernel
+      const uint32_t nseg = l.n_level_units_seg, nhyb = l.n_level_units_hyb, nrest = l.n_level_pages - nseg - nhyb;
       if (nseg) hipLaunchKernelGGL(k_levels_segw, dim3(nseg), dim3(kSgwLanes), 0, s, b, l.level_pages);
-      if (nrest) hipLaunchKernelGGL(k_levels, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages + nseg);
+      if (nhyb) hipLaunchKernelGGL(k_levels_hyb, dim3(nhyb), dim3(256), 0, s, b, l.level_pages + nseg);
+      if (nrest) hipLaunchKernelGGL(k_levels, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages + nseg + nhyb);
     }
   }
   return hipGetLastError();

@@ -7,7 +7,8 @@ helpers.go:133-149; page_v1.go:33-63). The column is `l: optional group (LIST) {
 null elements). The streams are Arrow-style run mixes, the reference writer's single bit-packed run,
 long runs, non-minimal varint headers, a stream longer than the workgroup's LDS stage (the
 list-ranking kernel takes it), num_values ending inside a run, and errors at known values in either
-stream. The oracle gives levels, values and errors; the GPU must equal it with both level kernels."""
+stream. The oracle gives levels, values and errors; the GPU must equal it on every level-kernel route
+(k_levels_segw, k_levels_hyb, k_levels)."""
 import os
 import sys
 
@@ -162,12 +163,23 @@ def test_oracle_generic_streams(files):
                 assert isinstance(r, O.OracleError) and r.page == 1, (name, r)
 
 
+# level-kernel routes (host.cpp): "seg" every stream by k_levels_segw; "ranking" every stream by
+# k_levels (its stride prelude takes the repetition streams' literal runs); "hyb" repetition streams by
+# k_levels_hyb, definition streams by k_levels; "default" definition streams by k_levels_segw,
+# repetition streams by k_levels_hyb
+ROUTES = {"seg": {"PQ_LV_SEGW": "1"}, "ranking": {"PQ_LV_SEGW": "0", "PQ_LV_HYB": "0"},
+          "hyb": {"PQ_LV_SEGW": "0"}, "default": {}}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["seg", "ranking"])
+@pytest.mark.parametrize("kernel", list(ROUTES))
 def test_gpu_generic_streams(gpu_ctx, files, monkeypatch, kernel):
     import pqgpu
     import test_gpu_parity as P
-    monkeypatch.setenv("PQ_LV_SEGW", "1" if kernel == "seg" else "0")
+    for k in ("PQ_LV_SEGW", "PQ_LV_HYB"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in ROUTES[kernel].items():
+        monkeypatch.setenv(k, v)
     for name, data in files.items():
         gpu = P._gpu_decode(gpu_ctx, data)
         for rg, col, r in pqtest.oracle_decode(data):

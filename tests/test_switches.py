@@ -17,6 +17,7 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_LV_SEG=0        the list-ranking level kernels everywhere
 - PQ_LV_SEGW=1/0     generic level streams by segment speculation (k_levels_segw): all of them, or
                      none (default 2: the definition streams)
+- PQ_LV_HYB=0        repetition streams by k_levels' list ranking instead of k_levels_hyb
 """
 import pytest
 
@@ -46,6 +47,7 @@ SWITCHES = {
     "lv_listrank": {"PQ_LV_SEG": "0"},
     "lv_segw": {"PQ_LV_SEGW": "1"},
     "lv_segw_none": {"PQ_LV_SEGW": "0"},
+    "lv_hyb_off": {"PQ_LV_HYB": "0"},
 }
 
 
