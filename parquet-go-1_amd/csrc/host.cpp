@@ -2122,6 +2122,24 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
+  } else if (b->spec && any_delta && !any_nest && !b->one_stream && b->copy_mode == 0 && !b->levels_first &&
+             !l.n_scan_pages && !n_dict && !l2.n_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
+             b->ba_chunks.empty() && !l.n_rec_pages && !side) {
+    // Speculative mode whose values path is the DELTA launch alone (with its fused copies; cfg2):
+    // that launch is the critical path, so it runs on the batch stream right after the resets, and
+    // the level kernels and k_bases go to the DELTA stream beside it. No stream waits on the
+    // critical path but the final join of the (long finished) level stream: cfg2 lost ~20 us per
+    // step between k_reset and k_values_delta and ~13 us after it to cross-stream waits.
+    if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
+    HIPCHECK(hipEventRecord(b->ev_fork, s), err);
+    HIPCHECK(hipStreamWaitEvent(ds, b->ev_fork, 0), err);
+    HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, ds); }), err);
+    HIPCHECK(timed(b, 15, ds, l.n_lf_list, [&] { return launch_level_fill(d, l, ds); }), err);
+    HIPCHECK(timed(b, 3, ds, l.n_base_chunks, [&] { return launch_bases(d, l, ds); }), err);
+    HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
+    HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
+    HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s); }), err);
+    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else if (b->spec) {
     // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
     // side stream concurrently with the level decode; k_bases then checks the header counts

@@ -150,7 +150,7 @@ struct ScanLDS {
 
 // PRE: the stride prelude from global memory first (a stream that is one run shape throughout is
 // then walked without staging it); without it every step of the walk reads the LDS window.
-template <class Sink, bool PRE = true>
+template <class Sink, bool PRE = true, int SB = 56>  // SB: first diagnostic counter slot
 DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uint32_t need, Sink &sink,
                       unsigned long long *dbg = nullptr) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
@@ -248,7 +248,7 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
     done = L.ctl_done;
   }
   if (done >= need) {
-    if (wv == 0) st.flush(56);
+    if (wv == 0) st.flush(SB);
     return done;
   }
   uint32_t w = (pos + sbase) / kScanWin;  // the window holding the chain's position
@@ -376,7 +376,7 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
     wg_barrier();
     st.lap(4);
   }
-  if (wv == 0) st.flush(56);
+  if (wv == 0) st.flush(SB);
   return done;
 }
 
@@ -853,10 +853,13 @@ DEV void lv_walk(LevelLDS &L, LevelSink &sk, uint32_t need, Stamps &st) {
         // by induction: up to 64 runs per step go to the run table (and the fill-tile starts they
         // hold), with no LDS staging and no list ranking. Anything else stops the prelude and the
         // chunk walk below takes the chain from there with the exact semantics.
-        if (tid < 64) lv_stride(sk, need, entry, done, runs_done);
-        if (tid == 0) { L.sp_e = entry; L.sp_d = done; L.sp_r = runs_done; }
+        uint32_t pe = entry, pdn = done, pr = runs_done;  // (wave 0's walk; every wave reads the result)
+        if (tid < 64) lv_stride(sk, need, pe, pdn, pr);
+        if (tid == 0) { L.sp_e = pe; L.sp_d = pdn; L.sp_r = pr; }
         wg_barrier();
-        try_stride = L.sp_r != runs_done;  // (a chunk walk follows; try again only after a step that took runs)
+        // workgroup-uniform: every thread compares the same LDS value with the same old count (a
+        // chunk walk follows; the prelude is tried again only after one that took runs)
+        try_stride = L.sp_r != runs_done;
         entry = L.sp_e;
         done = L.sp_d;
         runs_done = L.sp_r;
@@ -2303,8 +2306,9 @@ __global__ void __launch_bounds__(256) k_levels_hyb(BatchDev b_in, const uint32_
   if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
     if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
   } else if (ns) {
-    done = hyb_scan<LvRunSink, false>(lds, gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off),
-                                      rep ? pd.rep_len : pd.def_len, (uint32_t)(rep ? cd.rep_bw : cd.def_bw), ns, sk);
+    done = hyb_scan<LvRunSink, false, 48>(lds, gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off),
+                                          rep ? pd.rep_len : pd.def_len, (uint32_t)(rep ? cd.rep_bw : cd.def_bw), ns, sk,
+                                          b.dbg);
   }
   if (threadIdx.x == 0) {  // wave 0 walked: its sink holds the run count and the error
     b.lv_meta[4 * pi + 2 * which] = sk.nruns;

@@ -54,3 +54,6 @@ sn = ["fast_hops", "decode", "chain", "sink", "window", "hops#", "steps#", "-"]
 for k, n in enumerate(sn[:7]):
     v = int(d[56 + k])
     print(f"scan   {n:12s} total {v:>14d}")
+for k, n in enumerate(sn[:7]):  # k_levels_hyb's hyb_scan (slots 48..; k_snappy's too where it runs)
+    v = int(d[48 + k])
+    print(f"lvhyb  {n:12s} total {v:>14d}")
