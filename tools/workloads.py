@@ -131,7 +131,7 @@ def gen_cfg4(records=16_777_216, rg_rows=RG_ROWS, page_rows=65_536, seed=5, firs
     vals = pa.array(rng.integers(-2**62, 2**62, nm), mask=rng.random(nm) < 0.05)
     mcol = pa.MapArray.from_arrays(pa.array(moffs), keys, vals, mask=pa.array(mnull))
     return _write(pa.table({"l": lcol, "m": mcol}), data_page_version="1.0", compression="NONE",
-                  use_dictionary=["m.key_value.key"], row_group_size=rg_rows, max_rows_per_page=page_rows), None
+                  use_dictionary=["m.key_value.key"], row_group_size=rg_rows, max_rows_per_page=page_rows), (lcol, mcol)
 
 
 GENERATORS = {"cfg1": gen_cfg1, "cfg2": gen_cfg2, "cfg3": gen_cfg3, "cfg4": gen_cfg4}
