@@ -1496,12 +1496,15 @@ struct SgOut {
     o += k;
     if (o >= 32) { put((uint32_t)acc); acc >>= 32; W++; o -= 32; }
   }
-  DEV void zeros(uint32_t c) {  // c null values: the bitmap already holds zeros
-    const uint32_t t = o + c;
-    if (t < 32) { o = t; return; }
-    put((uint32_t)acc);
-    acc = 0;
-    W += t >> 5;
+  DEV void step(uint32_t x, uint32_t k) {  // k values, bits x (x == 0 whenever k > 32)
+    ones += __popc(x);
+    acc |= (uint64_t)x << o;
+    const uint32_t t = o + k;
+    if (t >= 32) {  // (t >= 64 only for nulls: acc >> 32 is then 0 and the words between stay zero)
+      put((uint32_t)acc);
+      acc >>= 32;
+      W += t >> 5;
+    }
     o = t & 31;
   }
   DEV void end() {  // the range's last word, shared with whoever writes the bits after it
@@ -1684,8 +1687,11 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
         err = PQ_ERR_EOF;
       }
     }
-    // ---- D. every verified lane writes its values' validity bits (a failing page writes nothing):
-    // one run per step, a short bit-packed run's payload taken from its header's 8 bytes
+    // ---- D. every verified lane writes its values' validity bits (a failing page writes nothing).
+    // One uniform step per iteration: a lane whose run is spent takes the next header, then every
+    // lane appends up to 32 values of its run (a null run all at once: the cursor moves), so the
+    // wave runs one short path instead of the union of a per-run-kind branch chain (round 4's loop
+    // spent ~4,700 cycles per step in it: 74 % of the kernel, tools/diag.py seg_CD).
     if (!err && !PQ_ABLATE(b, 21)) {  // (diagnostic: bit 21 skips D)
       uint32_t P = entry, v = base;
       const bool mine = cnt > 0 && base < need;
@@ -1695,52 +1701,47 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
       out.ones = 0;
       out.nostore = PQ_ABLATE(b, 20);
       out.start(pd.slot_base + base);
+      uint32_t rem = 0, rpay = 0;  // the current run: values left, next payload bit (stage bits)
+      bool rbits = false, rone = false;  // bit-packed / RLE of ones (else RLE of nulls)
       for (;;) {
-        const bool act = mine && P < exit && v < vend;
+        const bool act = mine && (rem || (P < exit && v < vend));
         if (!__ballot(act)) break;
         stp.count(7);
-        const uint64_t x = sg_bytes8(L.stage, P + sa);
-        SgHop h = sg_decode(x, P, n);
-        bool slow = false;
-        if (act && !h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
-          const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
-          h.adv = eh.adv;
-          h.nv = eh.nvals;
-          h.bp = eh.bp;
-          h.val = eh.value;
-          slow = true;
-        }
-        if (act) {
-          const uint32_t c = min(h.nv, vend - v);
-          bool done = false;
-          if (c > kSgLong && (h.bp || h.val)) {  // long: the whole wave (the accumulator restarts after it)
+        if (act && !rem) {
+          SgHop h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
+          if (!h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
+            const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+            h.adv = eh.adv;
+            h.nv = eh.nvals;
+            h.bp = eh.bp;
+            h.val = eh.value;
+          }
+          rem = min(h.nv, vend - v);
+          rbits = h.bp != 0;
+          rone = !h.bp && h.val;
+          rpay = 8 * (h.val + sa);
+          P += h.adv;
+          if (rem > kSgLong && (rbits || rone)) {  // long: the whole wave (the accumulator restarts after it)
             const uint32_t q = atomicAdd(&L.nq, 1u);
             if (q < kSgQueue) {
               out.end();
               L.qg[q] = v;
-              L.qc[q] = c;
-              L.qv[q] = h.bp ? 0x80000000u | h.val : 1u;
-              out.start(pd.slot_base + v + c);
-              done = true;
+              L.qc[q] = rem;
+              L.qv[q] = rbits ? 0x80000000u | h.val : 1u;
+              v += rem;
+              out.start(pd.slot_base + v);
+              rem = 0;
             }
           }
-          if (done || PQ_ABLATE(b, 22)) {
-          } else if (!h.bp && !h.val) {
-            out.zeros(c);  // nulls: the cursor moves
-          } else if (h.bp && !slow && h.L + ((c + 7) >> 3) <= 8) {  // payload inside the header's 8 bytes
-            const uint64_t pb = x >> (8 * h.L);
-            const uint32_t k1 = min(c, 32u);
-            out.app((uint32_t)pb & (k1 == 32 ? ~0u : ((1u << k1) - 1u)), k1);
-            if (c > 32) out.app((uint32_t)(pb >> 32) & ((1u << (c - 32)) - 1u), c - 32);
-          } else {
-            for (uint32_t q = 0; q < c; q += 32) {
-              const uint32_t k = min(32u, c - q);
-              const uint32_t m = k == 32 ? ~0u : ((1u << k) - 1u);
-              out.app(h.bp ? (uint32_t)sg_bytes8(L.stage, h.val + sa + (q >> 3)) & m : m, k);
-            }
-          }
-          v += c;
-          P += h.adv;
+        }
+        if (act && rem) {
+          const uint32_t k = (rbits || rone) ? min(rem, 32u) : rem;
+          const uint32_t m = k >= 32 ? ~0u : ((1u << k) - 1u);
+          const uint32_t x = rbits ? (uint32_t)(sg_bytes8(L.stage, rpay >> 3) >> (rpay & 7)) & m : rone ? m : 0u;
+          out.step(x, k);
+          rpay += k;
+          rem -= k;
+          v += k;
         }
       }
       // a bit-packed run cut by EOF ends the last lane's range: its readable values (zero filled)

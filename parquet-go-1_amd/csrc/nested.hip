@@ -142,7 +142,7 @@ struct NestStage {
 // (bytes), eqd[q] the groups' definition == max_def masks; the u8 level arrays the chunk has are
 // written and the pages' counts (records, non-null values) added once per tile.
 DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, const NestFill &x, NestStage &T,
-                     uint32_t tid, uint64_t (&lw)[2][4], uint32_t (&eqd)[4], uint32_t &end_d) {
+                     uint32_t tid, uint64_t (&lw)[2][4], uint32_t (&eqd)[4], uint32_t &end_d, Stamps &st) {
   const uint32_t lane = lane_id(), wv = tid >> 6;
   LfStream S[2];
   S[0] = lf_stream(b, pd, cd, x, 0, T.run[0], tid);
@@ -151,6 +151,7 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
   reinterpret_cast<uint2 *>(T.grun[0])[tid] = make_uint2(0, 0);
   reinterpret_cast<uint2 *>(T.grun[1])[tid] = make_uint2(0, 0);
   wg_barrier();
+  st.lap(0);
   // run r > 0 starts in group ceil((x_r - t0) / 8) at the latest: the groups from there on begin in
   // it or later; of the runs that mark one group the last one writes (no atomics)
 #pragma unroll
@@ -190,6 +191,7 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
     e[w][0] = max(e[w][0], c0); e[w][1] = max(e[w][1], c0);
     e[w][2] = max(e[w][2], c1); e[w][3] = max(e[w][3], c1);
   }
+  st.lap(1);
   uint32_t nc[2] = {0, 0};
 #pragma unroll
   for (uint32_t w = 0; w < 2; w++) {
@@ -219,6 +221,7 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
       }
     }
   }
+  st.lap(2);
 #pragma unroll
   for (uint32_t w = 0; w < 2; w++) {  // page counts: one atomic per tile and stream
     const uint32_t wc = (uint32_t)wave_sum64(nc[w]);
@@ -229,6 +232,7 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
     const uint32_t c = T.cnt[tid][0] + T.cnt[tid][1] + T.cnt[tid][2] + T.cnt[tid][3];
     if (c) atomicAdd(tid ? &b.page_nn[x.pi] : &b.page_rec[x.pi], c);
   }
+  st.lap(3);
 }
 
 // Nibble packing of a slot's (rep, def) levels (rep_bw + def_bw <= 4): the low nibbles of the
@@ -266,9 +270,13 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
   const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
   const uint32_t R = cd.nest;
+  // diagnostic build (tools/diag_nest.py): 0 run staging, 1 group marks, 2 expansion, 3 page counts,
+  // 4 packed levels, 5 counters, 6 validity
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
   uint64_t lw[2][4];
   uint32_t eqd[4], end_d = 0;
-  nest_expand(b, pd, cd, x, L.st, tid, lw, eqd, end_d);
+  nest_expand(b, pd, cd, x, L.st, tid, lw, eqd, end_d, st);
   // slot validity (definition level == max_def) of the definition stream's covered values
   uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
   if (vbits && x.lo < end_d) {  // workgroup-uniform
@@ -293,6 +301,7 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
       q[1] = make_uint4((uint32_t)lw[1][2 * h], (uint32_t)(lw[1][2 * h] >> 32), (uint32_t)lw[1][2 * h + 1], (uint32_t)(lw[1][2 * h + 1] >> 32));
     }
   }
+  st.lap(4);
   constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
   auto ge = [&](uint64_t v, uint32_t t) -> uint64_t { return ((v | H) - L1 * t) & H; };  // bytes v >= t
   const bool swar = cd.max_def < 128;
@@ -331,6 +340,7 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
     const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
     b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j] = L.part[h][j][0] + L.part[h][j][1] + L.part[h][j][2] + L.part[h][j][3];
   }
+  st.lap(5);
   if (vbits && x.lo < end_d) {
     const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
     const int64_t w0 = x.t0 + 32 * (int64_t)w;
@@ -341,6 +351,8 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
       else if (v) atomicOr(dst, v);                                     // shared with a neighbouring page
     }
   }
+  st.lap(6);
+  st.flush(24);
 }
 
 // One 256-thread workgroup per chunk: thread i takes a contiguous run of the chunk's counting
@@ -458,6 +470,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   const uint32_t endc = min(x.hi, min(cov_r, cov_d));
   uint32_t *row = L.ent[wv];
   uint32_t *bits = L.brow[wv];
+  // diagnostic build (tools/diag_nest.py): 0 levels + flags, 1 entry indices, 2 offsets, 3 validity, 4 groups
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
 #pragma unroll 1
   for (uint32_t h = 0; h < 2; h++) {
     const int64_t g = nest_group(x, tid, 2 * h);
@@ -492,6 +507,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
         vm[j] |= (uint32_t)(j < R ? d >= cd.list_null_def[j] : d == maxd) << q;
       }
     }
+    st.lap(0);
     // entry indices: wave prefix sums, then the waves before this one in the half
     uint32_t P[C], T[C];
 #pragma unroll
@@ -510,6 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       for (uint32_t q = 0; q < wv; q++) v += L.wtot[h][j][q];
       run[j] = v;
     }
+    st.lap(1);
     // list offsets of each level, then the record offsets (level-1 list starts)
 #pragma unroll
     for (uint32_t j = 0; j <= R; j++) {
@@ -528,6 +545,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
       wave_lds_sync();
     }
+    st.lap(2);
     // validity bits of every counter's entries
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
@@ -544,6 +562,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
       wave_lds_sync();
     }
+    st.lap(3);
     // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
     // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
     // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
@@ -573,7 +592,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       nest_put_bits(gv, rj, bits, tj, lane);
       wave_lds_sync();
     }
+    st.lap(4);
   }
+  st.flush(32);
 }
 
 // Struct validity of the OPTIONAL groups of a leaf with max_rep == 0: entries are the leaf's slots,
