@@ -82,7 +82,7 @@ DEV BatchDev global_view(BatchDev b) {
   b.pages = gp(b.pages); b.chunks = gp(b.chunks); b.chunk_err = gp(b.chunk_err);
   b.page_nn = gp(b.page_nn); b.page_nn_v = gp(b.page_nn_v); b.spec_mismatch = gp(b.spec_mismatch);
   b.page_rec = gp(b.page_rec); b.page_vbase = gp(b.page_vbase); b.page_rbase = gp(b.page_rbase);
-  b.nest_cnt = gp(b.nest_cnt); b.nest_base = gp(b.nest_base); b.nest_tot = gp(b.nest_tot); b.nest_pk = gp(b.nest_pk);
+  b.nest_cnt = gp(b.nest_cnt); b.nest_base = gp(b.nest_base); b.nest_tot = gp(b.nest_tot); b.nest_done = gp(b.nest_done);
   b.runs = gp(b.runs); b.run_base = gp(b.run_base); b.run_count = gp(b.run_count);
   b.tile_first = gp(b.tile_first); b.tile_desc = gp(b.tile_desc); b.tile_base = gp(b.tile_base); b.ba_tile_sum = gp(b.ba_tile_sum);
   b.ba_tile_page = gp(b.ba_tile_page); b.ba_tile_order = gp(b.ba_tile_order);

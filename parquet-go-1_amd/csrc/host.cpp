@@ -237,7 +237,8 @@ struct HostChunk {
   // device outputs (offsets into the arena)
   uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0;
   // nested (Arrow-style) output: list levels (0: none), per level offsets / validity, elements
-  uint32_t nest = 0, nest_tile0 = 0, nest_ntiles = 0;
+  uint32_t nest = 0, nest_tile0 = 0, nest_ntiles = 0, nest_nmask = 0;
+  uint64_t o_nest_mask = 0;
   uint64_t o_lvl_off[PQGPU_MAX_NEST] = {}, o_lvl_valid[PQGPU_MAX_NEST] = {}, o_elem_valid = 0;
   int64_t num_lists[PQGPU_MAX_NEST] = {}, num_elems = 0;
   // struct validity of the OPTIONAL groups on the path (pqgpu_chunk_result group_*): own bitmap
@@ -485,7 +486,9 @@ struct pqgpu_batch {
   std::vector<uint4> nest_tiles;  // nested fill tiles: {global fill tile, page, tile of the page, chunk}
   std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
   uint64_t l_grp_tiles = 0;
-  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, o_nest_pk = 0, l_nest_tiles = 0, l_nest_chunks = 0;
+  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0;
+  uint64_t o_nest_done = 0;
+  uint32_t n_nest_empty = 0;  // nested chunks without fill tiles (first in nest_chunks)
   uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
   std::vector<uint64_t> run_base, tile_base;
   uint64_t run_total = 0, tile_total = 0;
@@ -1214,6 +1217,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
   b->o_spec_flag = take(4);
+  b->o_nest_done = take((uint64_t)nc * 4);
   uint64_t n_ba_tiles = 0;  // byte-array tiles (for the look-back state, zeroed per decode)
   for (uint32_t c = 0; c < nc; c++) {
     const HostChunk &hc = b->chunks[c];
@@ -1392,6 +1396,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
   }
   b->nest_first[PQGPU_MAX_NEST + 1] = (uint32_t)b->nest_tiles.size();
+  // chunks with tiles are scanned by their last k_nest_count tile; the others by k_nest_scan
+  std::stable_partition(b->nest_chunks.begin(), b->nest_chunks.end(), [&](uint32_t c) { return b->chunks[c].nest_ntiles == 0; });
+  b->n_nest_empty = 0;
+  for (uint32_t c : b->nest_chunks) b->n_nest_empty += b->chunks[c].nest_ntiles == 0;
   // k_ba_emit block order: class 0 / 1 = chunks whose pages are all dictionary pages with a
   // slot table of 16/32-byte / 64-byte slots, class 2 = the rest. Within a class, chunk c's
   // tiles (in order) go to queue c mod 8 and block b takes tile b / 8 of queue b mod 8: blocks
@@ -1672,7 +1680,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
   b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 4);  // every entry written by k_nest_count
   b->o_nest_base = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 8);
-  b->o_nest_pk = take((uint64_t)b->nest_tiles.size() * kNestPkWords * 8);  // written by k_nest_count
+  for (uint32_t c : b->nest_chunks) {  // the slots' flag masks (written by k_nest_count)
+    HostChunk &hc = b->chunks[c];
+    hc.nest_nmask = 2 * (hc.nest + 1) + hc.ngroups;
+    hc.o_nest_mask = take((uint64_t)hc.nest_ntiles * hc.nest_nmask * 1024);
+  }
   b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
   b->arena_size = a;
   if (a > b->d_arena_cap) {
@@ -1783,7 +1795,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.nest = hc.nest;
     cd.nest_tile0 = hc.nest_tile0;
     cd.nest_ntiles = hc.nest_ntiles;
-    cd.nest_pkb = cd.rep_bw + cd.def_bw > 4 ? 1u : 0u;
+    cd.nest_nmask = hc.nest ? hc.nest_nmask : 0u;
+    cd.nest_masks = hc.nest ? dp(hc.o_nest_mask) : 0;
     for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) {
       cd.list_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_def[k] : 0);
       cd.list_null_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_null_def[k] : 0);
@@ -1903,7 +1916,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.nest_cnt = (uint32_t *)(A + b->o_nest_cnt);
   d.nest_base = (uint64_t *)(A + b->o_nest_base);
   d.nest_tot = (uint64_t *)(A + b->o_nest_tot);
-  d.nest_pk = (uint64_t *)(A + b->o_nest_pk);
+  d.nest_done = (uint32_t *)(A + b->o_nest_done);
   d.runs = (HybRun *)(A + b->o_runs);
   d.lv_runs = (uint2 *)(A + b->o_lv_runs);
   d.lv_run_base = (const uint64_t *)(A + b->o_lv_run_base);
@@ -1977,6 +1990,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
   l.nest_chunks = (const uint32_t *)(A + b->l_nest_chunks);
   l.n_nest_chunks = (uint32_t)b->nest_chunks.size();
+  l.n_nest_empty = b->n_nest_empty;
   l.grp_tiles = (const uint32_t *)(A + b->l_grp_tiles);
   l.n_grp_tiles = (uint32_t)b->grp_tiles.size();
   l.delta_pages = (const uint32_t *)(A + b->l_delta);
@@ -2014,10 +2028,19 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // per-decode state: two contiguous fills (validity bitmaps + counters; error keys + tile table).
   // page_nn of pages without level streams is constant and was uploaded with the descriptors.
   (void)np;
-  HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
   BatchDev d = batch_dev(b);
   LaunchLists l = launch_lists(b);
   const PbaLists pl = pba_lists(b);
+  const char *dside = getenv("PQ_DELTA_SIDE");  // 1: the DELTA stream in every batch (comparison runs)
+  const bool side = dside && atoi(dside) != 0;
+  const bool any_delta = b->n_delta_items || l.n_delta_pages;
+  const bool any_nest = l.n_nest_chunks || l.n_nest_tiles || l.n_grp_tiles;
+  // Speculative mode whose values path is the DELTA launch alone (with its fused copies; cfg2): see below
+  const bool delta_major = b->n_groups == 0 && b->spec && any_delta && !any_nest && !b->one_stream &&
+                           b->copy_mode == 0 && !b->levels_first && !l.n_scan_pages && !b->n_dict_items &&
+                           l.n_items == b->n_delta_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
+                           b->ba_chunks.empty() && !l.n_rec_pages && !side;
+  HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
   // SNAPPY pages first: every later kernel reads page data (column-group pipeline: one launch per
   // group, each followed by an event the group's values work waits for)
   const uint32_t G = b->n_groups;
@@ -2051,12 +2074,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // a batch without level streams and column groups keeps its DELTA pages on the batch stream: with
   // nothing to overlap but the other values kinds they only compete with them (cfg5 6.19 -> 6.08 ms)
   const bool lvl_any = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
-  const char *dside = getenv("PQ_DELTA_SIDE");  // 1: the DELTA stream in every batch (comparison runs)
-  const bool side = dside && atoi(dside) != 0;
   hipStream_t ds = b->one_stream || (!lvl_any && b->n_groups == 0 && !side) ? s : b->ctx->delta;
   if (!b->ev_delta_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_delta_join, hipEventDisableTiming), err);
   // streams with nothing to run are neither forked nor joined (a cross-stream wait costs latency)
-  const bool any_delta = l1.n_items || l.n_delta_pages;
   auto fork_delta = [&](hipEvent_t after) -> hipError_t {
     if (!any_delta) return hipSuccess;
     hipError_t e = hipStreamWaitEvent(ds, after, 0);
@@ -2071,12 +2091,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // queued; the batch stream joins them at the end.
   if (!b->ev_levels) HIPCHECK(hipEventCreateWithFlags(&b->ev_levels, hipEventDisableTiming), err);
   if (!b->ev_nest_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_nest_join, hipEventDisableTiming), err);
-  const bool any_nest = l.n_nest_chunks || l.n_nest_tiles || l.n_grp_tiles;
   auto fork_nest = [&]() -> hipError_t {
     if (!any_nest) return hipSuccess;
     hipError_t e = hipEventRecord(b->ev_levels, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(ds, b->ev_levels, 0);
-    if (e == hipSuccess) e = timed(b, 16, ds, l.n_nest_chunks, [&] { return launch_nest_scan(d, l, ds); });
+    if (e == hipSuccess) e = timed(b, 16, ds, l.n_nest_empty, [&] { return launch_nest_scan(d, l, ds); });
     if (e == hipSuccess) e = timed(b, 14, ds, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, ds); });
     if (e == hipSuccess) e = timed(b, 21, ds, l.n_grp_tiles, [&] { return launch_group_flat(d, l, ds); });  // flat leaves
     if (e == hipSuccess) e = hipEventRecord(b->ev_nest_join, ds);
@@ -2087,8 +2106,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   hipStream_t cs = b->one_stream ? s : b->ctx->copy;
   if (!b->ev_copy) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming), err);
   if (!b->ev_copy_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_copy_join, hipEventDisableTiming), err);
+  bool copies_out = false;  // forked and not yet joined by the batch stream
   auto fork_copies = [&](hipStream_t from) -> hipError_t {
     if (!l.n_copy_items) return hipSuccess;
+    copies_out = true;
     hipError_t e = hipEventRecord(b->ev_copy, from);
     if (e == hipSuccess) e = hipStreamWaitEvent(cs, b->ev_copy, 0);
     if (e == hipSuccess) e = timed(b, 20, cs, l.n_copy_items, [&] { return launch_values_copy(d, l, cs); });
@@ -2122,9 +2143,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
-  } else if (b->spec && any_delta && !any_nest && !b->one_stream && b->copy_mode == 0 && !b->levels_first &&
-             !l.n_scan_pages && !n_dict && !l2.n_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
-             b->ba_chunks.empty() && !l.n_rec_pages && !side) {
+  } else if (delta_major) {
     // Speculative mode whose values path is the DELTA launch alone (with its fused copies; cfg2):
     // that launch is the critical path, so it runs on the batch stream right after the resets, and
     // the level kernels and k_bases go to the DELTA stream beside it. No stream waits on the
@@ -2179,7 +2198,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
     if (v != s) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);
-    if (l.n_copy_items) HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    // the byte-array path reads no copied values: it goes ahead of the copy stream's join (cfg4: it
+    // waited ~140 us for the INT32 / INT64 copies)
+    if (copies_out && b->ba_chunks.empty()) {
+      HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+      copies_out = false;
+    }
     if (any_delta) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
@@ -2203,7 +2227,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values
     if (b->copy_mode >= 3) HIPCHECK(fork_copies(s), err);  // PQ_COPY_MODE=3: after everything (profiling)
-    if (l.n_copy_items) HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+    if (copies_out && b->ba_chunks.empty()) {
+      HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);
+      copies_out = false;
+    }
     if (any_delta && !b->split_values) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   }
   if (!b->ba_chunks.empty()) {
@@ -2245,6 +2272,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 6, s, l.n_ba_tiles, [&] { return launch_ba_emit(d, l, s); }), err);
     HIPCHECK(timed(b, 19, s, l.n_ba_delta, [&] { return launch_dba_gather(d, l, s); }), err);
     if (b->any_ba_sync) HIPCHECK(hipStreamSynchronize(s), err);  // chunk_desc copies above read host memory
+    if (copies_out) HIPCHECK(hipStreamWaitEvent(s, b->ev_copy_join, 0), err);  // (see above)
+    copies_out = false;
   }
   HIPCHECK(timed(b, 7, s, l.n_rec_pages, [&] { return launch_records(d, l, s); }), err);
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)

@@ -23,7 +23,7 @@ struct BatchDev {
   uint32_t *nest_cnt;             // [nested tiles][2][kNestCnt] lists starting per level, then elements, per half tile
   uint64_t *nest_base;            // [nested tiles][2][kNestCnt] their exclusive prefix within the chunk
   uint64_t *nest_tot;             // [nchunks][kNestCnt] chunk totals
-  uint64_t *nest_pk;              // [nested tiles][kNestPkWords] the tiles' levels, packed by k_nest_count for k_nest_emit
+  uint32_t *nest_done;            // [nchunks] k_nest_count tiles finished (zeroed per decode)
   HybRun *runs;                   // run tables of hybrid value streams
   const uint64_t *run_base;       // [npages] first entry of each page's run table
   uint32_t *run_count;            // [npages]
@@ -58,7 +58,6 @@ struct BatchDev {
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
 constexpr uint32_t kNestCnt = 9;       // nested counters per page: lists of levels 1..8, then elements
-constexpr uint32_t kNestPkWords = 2048; // u64 words of packed levels per nested tile (nested.hip)
 constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
 constexpr uint32_t kDictEarlyHost = 4096;  // kernels.hip kDictEarly: dictionaries staged with their tile
 constexpr uint32_t kDictGroupHost = 2;     // kernels.hip kDictGroup: tiles per WI_DICT2 item (at most)
@@ -92,7 +91,7 @@ struct LaunchLists {
   const uint4 *nest_desc; uint32_t n_nest_tiles;         // fill tiles of the nested chunks (k_nest_count / k_nest_emit):
                                                          // {global fill tile, page, tile of the page, chunk}
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
-  const uint32_t *nest_chunks; uint32_t n_nest_chunks;
+  const uint32_t *nest_chunks; uint32_t n_nest_chunks, n_nest_empty;  // nested chunks, those without tiles first
   const uint32_t *grp_tiles; uint32_t n_grp_tiles;       // chunk of every k_group_flat tile
   const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)
   uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE

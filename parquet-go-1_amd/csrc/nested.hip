@@ -15,7 +15,7 @@
 //   a leaf element is non-null     iff d == maxD
 // Three launches over the fill tiles of the chunks' pages (level_fill.h: kLfTile slots aligned on
 // the chunk's slot index, one per page that holds slots of it), each cut into two 4,096-slot
-// halves: counts per half (k_nest_count), per-chunk exclusive scans over the halves (k_nest_scan),
+// halves: counts per half (k_nest_count, whose last tile per chunk scans the chunk's halves),
 // then the outputs (k_nest_emit): u8 levels, slot validity, list / record offsets and bitmaps.
 // Both tile kernels expand the two level streams from the run tables the level kernels wrote
 // (reading the compressed streams, ~0.4 B per slot) and keep the levels of their slots in
@@ -235,32 +235,67 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
   st.lap(3);
 }
 
-// Nibble packing of a slot's (rep, def) levels (rep_bw + def_bw <= 4): the low nibbles of the
-// eight bytes of x to 32 bits, and back.
-DEV uint32_t nib_pack(uint64_t x) {
-  x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
-  x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
-  return (uint32_t)(x | (x >> 16));
+// A chunk's scan by one 256-thread workgroup: thread i takes a contiguous run of the chunk's
+// counting units (two per fill tile), sums its counters, one workgroup scan per counter gives the
+// run's bases, and a second pass over the run writes every unit's base. The chunk's totals close
+// every level's offsets and the record offsets. Run by the chunk's last tile of k_nest_count to
+// finish (k_nest_scan: chunks without tiles).
+DEV void nest_scan_chunk(const BatchDev &b, uint32_t c, uint64_t *wsum) {
+  const ChunkDesc &cd = b.chunks[c];
+  const uint32_t nt = 2 * cd.nest_ntiles;
+  const uint32_t per = (nt + blockDim.x - 1) / blockDim.x;
+  const uint32_t k0 = min(nt, threadIdx.x * per), k1 = min(nt, k0 + per);
+  uint32_t *cnt = b.nest_cnt + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;  // (published by atomics)
+  uint64_t *base = b.nest_base + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
+  const uint32_t C = cd.nest + 1;  // counters in use (lists of levels 1..R, elements)
+  uint64_t acc[kNestCnt], tot[kNestCnt];
+#pragma unroll
+  for (uint32_t j = 0; j < kNestCnt; j++) acc[j] = 0;
+  for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++)
+      if (j < C) acc[j] += __hip_atomic_load(&cnt[(uint64_t)k * kNestCnt + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (uint32_t j = 0; j < kNestCnt; j++) {
+    tot[j] = 0;
+    if (j < C) {  // workgroup-uniform
+      acc[j] = block_excl_scan64(acc[j], wsum, &tot[j]);
+      if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot[j];
+    }
+  }
+  for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+    for (uint32_t j = 0; j < kNestCnt; j++)
+      if (j < C) {
+        base[(uint64_t)k * kNestCnt + j] = acc[j];
+        acc[j] += __hip_atomic_load(&cnt[(uint64_t)k * kNestCnt + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  // closing entries: offsets[num_lists] = the next level's entries (elements), records -> slots
+  int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
+#pragma unroll
+  for (uint32_t j = 0; j + 1 < kNestCnt; j++)
+    if (threadIdx.x == j && j < cd.nest) gp_u64<int32_t>(cd.lvl_offsets[j])[tot[j]] = (int32_t)tot[j + 1];
+  if (threadIdx.x == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
 }
-DEV uint64_t nib_unpack(uint32_t v) {
-  uint64_t x = v;
-  x = (x | (x << 16)) & 0x0000ffff0000ffffull;
-  x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
-  return (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+
+__global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t *chunks) {
+  const BatchDev b = global_view(b_in);
+  __shared__ uint64_t wsum[4];
+  nest_scan_chunk(b, chunks[blockIdx.x], wsum);
 }
 
 // Pass 1 over the nested chunks' fill tiles: both level streams expanded (the u8 level arrays,
-// the slot validity and the pages' record / non-null counts written from registers), the tile's
-// levels packed for pass 2 (nest_pk: per thread and half, sixteen (rep, def) pairs as nibbles in
-// one u64, or as two byte words each when the widths exceed a nibble), and per 4,096-slot half
-// how many entries of each counter (lists of levels 1..R starting, then leaf elements), stored at
-// the tile's position in the launch list (every half is written: no zeroing). Eight levels per
-// 64-bit word are compared at once (SWAR: levels below 128; wider levels take the byte loop); the
-// counters ride in 5-bit fields (at most 16 slots per thread and half).
+// the slot validity and the pages' record / non-null counts written from registers), the slots'
+// flag masks for pass 2 (cd.nest_masks: which counters count at a slot, the entries' validity,
+// the groups' validity), and per 4,096-slot half how many entries of each counter (lists of
+// levels 1..R starting, then leaf elements), stored at the tile's position in the launch list
+// (every half is written: no zeroing).
 struct NestCountLDS {
   NestStage st;
   uint32_t vb[kLfTile / 32];  // slot validity of the tile (16 bits per thread and half)
   uint32_t part[2][kNestCnt][4];
+  uint64_t wsum[4];
+  uint32_t last;
 };
 __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *tiles) {
   const BatchDev b = global_view(b_in);
@@ -283,63 +318,87 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
     reinterpret_cast<uint16_t *>(L.vb)[tid] = (uint16_t)(eqd[0] | (eqd[1] << 8));
     reinterpret_cast<uint16_t *>(L.vb)[256 + tid] = (uint16_t)(eqd[2] | (eqd[3] << 8));
   }
-  // the levels for k_nest_emit
-  uint64_t *pk = b.nest_pk + (uint64_t)pos * kNestPkWords;
-  if (!cd.nest_pkb) {
-    const uint32_t sr = (uint32_t)cd.rep_bw;
-#pragma unroll
-    for (uint32_t h = 0; h < 2; h++) {
-      const uint32_t lo = nib_pack(lw[0][2 * h] | (lw[1][2 * h] << sr));
-      const uint32_t hi = nib_pack(lw[0][2 * h + 1] | (lw[1][2 * h + 1] << sr));
-      pk[h * 256 + tid] = ((uint64_t)hi << 32) | lo;
-    }
-  } else {
-#pragma unroll
-    for (uint32_t h = 0; h < 2; h++) {
-      uint4 *q = reinterpret_cast<uint4 *>(pk) + 2 * (h * 256 + tid);
-      q[0] = make_uint4((uint32_t)lw[0][2 * h], (uint32_t)(lw[0][2 * h] >> 32), (uint32_t)lw[0][2 * h + 1], (uint32_t)(lw[0][2 * h + 1] >> 32));
-      q[1] = make_uint4((uint32_t)lw[1][2 * h], (uint32_t)(lw[1][2 * h] >> 32), (uint32_t)lw[1][2 * h + 1], (uint32_t)(lw[1][2 * h + 1] >> 32));
-    }
-  }
-  st.lap(4);
+  // The slots' flag masks for k_nest_emit, 32 bits per thread (bits 8q..8q+7: group q; 0-15 the first
+  // half's sixteen slots, 16-31 the second's): mask j < C, the covered slots where counter j counts
+  // (a level-(j+1) list starts, j < R; a leaf element slot, j == R); C + j the validity of those
+  // entries (list j non-null; the element non-null); 2C + g, group g's validity (def >= group_def).
+  // Eight levels per 64-bit word are compared at once (SWAR: levels below 128; wider levels take
+  // the byte loop). The counters per half are the masks' popcounts, in 5-bit fields (at most 16
+  // slots per thread and half).
   constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
   auto ge = [&](uint64_t v, uint32_t t) -> uint64_t { return ((v | H) - L1 * t) & H; };  // bytes v >= t
+  auto pack8 = [](uint64_t hx) -> uint32_t {  // the high bits of the eight bytes, in byte order
+    const uint32_t lo = (uint32_t)hx >> 7, hi = (uint32_t)(hx >> 32) >> 7;
+    return ((lo * 0x01020408u) >> 24) | (((hi * 0x01020408u) >> 24) << 4);
+  };
   const bool swar = cd.max_def < 128;
   const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
   const uint32_t endc = min(x.hi, min(cov_r, cov_d));
-  uint64_t pa = 0, pb = 0;
+  uint32_t inm = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < 4; q++) {
-    const uint32_t vm = nest_inmask(nest_group(x, tid, q), 8, x.lo, endc);
-    const uint64_t rwq = lw[0][q], dwq = lw[1][q];
-    uint64_t acc = 0;
+  for (uint32_t q = 0; q < 4; q++) inm |= nest_inmask(nest_group(x, tid, q), 8, x.lo, endc) << (8 * q);
+  const uint32_t C = R + 1, M = cd.nest_nmask;
+  uint32_t *mk = gp_u64<uint32_t>(cd.nest_masks) + (uint64_t)(pos - cd.nest_tile0) * M * 256 + tid;
+  uint64_t pa = 0, pb = 0;
+#pragma unroll 1
+  for (uint32_t k = 0; k < M; k++) {
+    // mask k: kind (0 flag, 1 validity, 2 group) and its level j / group g
+    const uint32_t kind = k < C ? 0u : k < 2 * C ? 1u : 2u, j = kind == 0 ? k : k - C, g = k - 2 * C;
+    uint32_t m = 0;
     if (swar) {
-      const uint64_t mb = ((((uint64_t)vm * L1) & 0x8040201008040201ull) + 0x7f7f7f7f7f7f7f7full) & H;  // covered slots
-      for (uint32_t j = 0; j <= R; j++) {
-        const uint64_t th = j ? cd.list_def[j - 1] : 0u;
-        const uint64_t f = j < R ? ge(dwq, (uint32_t)th) & ~ge(rwq, j + 1) : ge(dwq, cd.list_def[R - 1]);
-        acc += (uint64_t)__popcll(f & mb) << (5 * j);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t rw = lw[0][q], dw = lw[1][q];
+        uint64_t f;
+        if (kind == 0) f = j < R ? ge(dw, j ? cd.list_def[j - 1] : 0u) & ~ge(rw, j + 1) : ge(dw, cd.list_def[R - 1]);
+        else if (kind == 1) f = j < R ? ge(dw, cd.list_null_def[j]) : ge(dw, cd.max_def) & ~ge(dw, cd.max_def + 1);
+        else f = ge(dw, cd.group_def[g]);
+        m |= pack8(f) << (8 * q);
       }
     } else {
 #pragma unroll 1
-      for (uint32_t i = 0; i < 8; i++) {
-        if (!((vm >> i) & 1u)) continue;
-        const uint32_t r = (uint32_t)(rwq >> (8 * i)) & 0xffu, d = (uint32_t)(dwq >> (8 * i)) & 0xffu;
-        for (uint32_t j = 0; j <= R; j++) acc += (uint64_t)nest_flag(cd, j, r, d) << (5 * j);
+      for (uint32_t i = 0; i < 32; i++) {
+        const uint32_t r = (uint32_t)(lw[0][i >> 3] >> (8 * (i & 7))) & 0xffu, d = (uint32_t)(lw[1][i >> 3] >> (8 * (i & 7))) & 0xffu;
+        const bool bit = kind == 0 ? nest_flag(cd, j, r, d)
+                         : kind == 1 ? (j < R ? d >= cd.list_null_def[j] : d == (uint32_t)cd.max_def)
+                                     : d >= cd.group_def[g];
+        m |= (uint32_t)bit << i;
       }
     }
-    if (q < 2) pa += acc; else pb += acc;
+    if (kind == 0) {
+      m &= inm;
+      pa += (uint64_t)__popc(m & 0xffffu) << (5 * j);
+      pb += (uint64_t)__popc(m >> 16) << (5 * j);
+    }
+    mk[(uint64_t)k * 256] = m;
   }
+  st.lap(4);
 #pragma unroll
   for (uint32_t j = 0; j < kNestCnt; j++) {
     const uint32_t a2 = (uint32_t)wave_sum64((pa >> (5 * j)) & 31u), b2 = (uint32_t)wave_sum64((pb >> (5 * j)) & 31u);
     if (lane == 0) { L.part[0][j][wv] = a2; L.part[1][j][wv] = b2; }
   }
   wg_barrier();
-  if (tid < 2 * kNestCnt) {
-    const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
-    b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j] = L.part[h][j][0] + L.part[h][j][1] + L.part[h][j][2] + L.part[h][j][3];
+  static_assert(2 * kNestCnt <= 64, "wave 0 publishes the counts");
+  // The chunk's last tile to finish scans its counts (no launch of its own, no order assumed:
+  // whichever tile arrives last finds every other tile's counts). The counts are published by
+  // agent-scope atomics whose results the arrival count waits for (an agent-scope release fence
+  // per tile would write back the XCD's whole L2: 0.39 -> 1.16 ms), and read by atomic loads.
+  if (wv == 0) {
+    uint32_t seen = 0;
+    if (tid < 2 * kNestCnt) {
+      const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
+      const uint32_t v = L.part[h][j][0] + L.part[h][j][1] + L.part[h][j][2] + L.part[h][j][3];
+      seen = __hip_atomic_exchange(&b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("; the exchanges have returned: %0" ::"v"(seen));  // (a use: the wave waits for them)
+    if (lane == 0)
+      L.last = __hip_atomic_fetch_add(&b.nest_done[x.chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+               cd.nest_ntiles;
   }
+  wg_barrier();
+  if (L.last) nest_scan_chunk(b, x.chunk, L.wsum);  // workgroup-uniform
   st.lap(5);
   if (vbits && x.lo < end_d) {
     const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
@@ -353,51 +412,6 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
   }
   st.lap(6);
   st.flush(24);
-}
-
-// One 256-thread workgroup per chunk: thread i takes a contiguous run of the chunk's counting
-// units (two per fill tile), sums its counters, one workgroup scan per counter gives the run's
-// bases, and a second pass over the run writes every unit's base. The chunk's totals close every
-// level's offsets and the record offsets.
-__global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t *chunks) {
-  const BatchDev b = global_view(b_in);
-  __shared__ uint64_t wsum[4];
-  const uint32_t c = chunks[blockIdx.x];
-  const ChunkDesc &cd = b.chunks[c];
-  const uint32_t nt = 2 * cd.nest_ntiles;
-  const uint32_t per = (nt + blockDim.x - 1) / blockDim.x;
-  const uint32_t k0 = min(nt, threadIdx.x * per), k1 = min(nt, k0 + per);
-  const uint32_t *cnt = b.nest_cnt + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
-  uint64_t *base = b.nest_base + 2 * (uint64_t)cd.nest_tile0 * kNestCnt;
-  const uint32_t C = cd.nest + 1;  // counters in use (lists of levels 1..R, elements)
-  uint64_t acc[kNestCnt], tot[kNestCnt];
-#pragma unroll
-  for (uint32_t j = 0; j < kNestCnt; j++) acc[j] = 0;
-  for (uint32_t k = k0; k < k1; k++)
-#pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++)
-      if (j < C) acc[j] += cnt[(uint64_t)k * kNestCnt + j];
-#pragma unroll
-  for (uint32_t j = 0; j < kNestCnt; j++) {
-    tot[j] = 0;
-    if (j < C) {  // workgroup-uniform
-      acc[j] = block_excl_scan64(acc[j], wsum, &tot[j]);
-      if (threadIdx.x == 0) b.nest_tot[(uint64_t)c * kNestCnt + j] = tot[j];
-    }
-  }
-  for (uint32_t k = k0; k < k1; k++)
-#pragma unroll
-    for (uint32_t j = 0; j < kNestCnt; j++)
-      if (j < C) {
-        base[(uint64_t)k * kNestCnt + j] = acc[j];
-        acc[j] += cnt[(uint64_t)k * kNestCnt + j];
-      }
-  // closing entries: offsets[num_lists] = the next level's entries (elements), records -> slots
-  int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
-#pragma unroll
-  for (uint32_t j = 0; j + 1 < kNestCnt; j++)
-    if (threadIdx.x == j && j < cd.nest) gp_u64<int32_t>(cd.lvl_offsets[j])[tot[j]] = (int32_t)tot[j + 1];
-  if (threadIdx.x == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
 }
 
 // Bits of x at the positions set in m, packed towards bit 0 (Hacker's Delight 7-4, compress).
@@ -455,57 +469,36 @@ struct NestEmitLDS {
   uint32_t brow[4][kNestWaveSlots / 32 + 1];
 };
 template <uint32_t R>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 6 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint4 *tiles, uint32_t first) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 8 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint4 *tiles, uint32_t first) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestEmitLDS<R> L;
   const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const NestFill x = nest_fill(b, gp(tiles)[pos]);
-  const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
   int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
-  const uint32_t maxd = (uint32_t)cd.max_def;
-  const uint64_t *pk = b.nest_pk + (uint64_t)pos * kNestPkWords;
-  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
-  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
+  // the thread's flag and validity masks (k_nest_count): bits 16 h .. 16 h + 15 for half h
+  const uint32_t *mk = gp_u64<const uint32_t>(cd.nest_masks) + (uint64_t)(pos - cd.nest_tile0) * cd.nest_nmask * 256 + tid;
+  uint32_t fm[C], vmm[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    fm[j] = mk[j * 256];
+    vmm[j] = mk[(C + j) * 256];
+  }
   uint32_t *row = L.ent[wv];
   uint32_t *bits = L.brow[wv];
-  // diagnostic build (tools/diag_nest.py): 0 levels + flags, 1 entry indices, 2 offsets, 3 validity, 4 groups
+  // diagnostic build (tools/diag_nest.py): 0 masks, 1 entry indices, 2 offsets, 3 validity, 4 groups
   PQ_STAMPS(st, b.dbg);
   st.begin();
 #pragma unroll 1
   for (uint32_t h = 0; h < 2; h++) {
     const int64_t g = nest_group(x, tid, 2 * h);
-    const uint32_t inm = nest_inmask(g, 16, x.lo, endc);
     const uint64_t s = (uint64_t)((int64_t)x.sbase + g);  // the chunk slot of the lane's first slot
-    // the lane's levels (bytes) of its two groups: repetition r0, r1, definition d0, d1
-    uint64_t r0, r1, d0, d1;
-    if (!cd.nest_pkb) {
-      const uint32_t sr = (uint32_t)cd.rep_bw;
-      const uint64_t mr = 0x0101010101010101ull * ((1u << sr) - 1u), md = 0x0101010101010101ull * (0xfu >> sr);
-      const uint64_t v = pk[h * 256 + tid];
-      const uint64_t a0 = nib_unpack((uint32_t)v), a1 = nib_unpack((uint32_t)(v >> 32));
-      r0 = a0 & mr; d0 = (a0 >> sr) & md; r1 = a1 & mr; d1 = (a1 >> sr) & md;
-    } else {
-      const uint4 *q = reinterpret_cast<const uint4 *>(pk) + 2 * (h * 256 + tid);
-      const uint4 u = q[0], v = q[1];
-      r0 = ((uint64_t)u.y << 32) | u.x; r1 = ((uint64_t)u.w << 32) | u.z;
-      d0 = ((uint64_t)v.y << 32) | v.x; d1 = ((uint64_t)v.w << 32) | v.z;
-    }
-    // the lane's flag and validity masks per counter
     uint32_t f[C], vm[C];
 #pragma unroll
-    for (uint32_t j = 0; j < C; j++) f[j] = vm[j] = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 16; q++) {
-      const uint32_t r = (uint32_t)((q < 8 ? r0 : r1) >> (8 * (q & 7))) & 0xffu;
-      const uint32_t d = (uint32_t)((q < 8 ? d0 : d1) >> (8 * (q & 7))) & 0xffu;
-      const uint32_t in = (inm >> q) & 1u;
-#pragma unroll
-      for (uint32_t j = 0; j < C; j++) {
-        f[j] |= (in & (uint32_t)nest_flag(cd, j, r, d)) << q;
-        vm[j] |= (uint32_t)(j < R ? d >= cd.list_null_def[j] : d == maxd) << q;
-      }
+    for (uint32_t j = 0; j < C; j++) {
+      f[j] = (fm[j] >> (16 * h)) & 0xffffu;
+      vm[j] = (vmm[j] >> (16 * h)) & 0xffffu;
     }
     st.lap(0);
     // entry indices: wave prefix sums, then the waves before this one in the half
@@ -570,16 +563,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     for (uint32_t gi = 0; gi < cd.ngroups; gi++) {
       uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[gi]);
       if (!gv) continue;  // shares list / element validity (workgroup-uniform)
-      const uint32_t j = cd.group_depth[gi], dg = cd.group_def[gi];
+      const uint32_t j = cd.group_depth[gi];
       uint32_t fj = 0, pj = 0, tj = 0;
       uint64_t rj = 0;
 #pragma unroll
       for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
         if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
-      uint32_t vg = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < 16; q++)
-        vg |= (uint32_t)(((uint32_t)((q < 8 ? d0 : d1) >> (8 * (q & 7))) & 0xffu) >= dg) << q;
+      const uint32_t vg = (mk[(2 * C + gi) * 256] >> (16 * h)) & 0xffffu;
       if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
       wave_lds_sync();
       const uint32_t c = (uint32_t)__popc(fj);
@@ -676,8 +666,8 @@ hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_
   return hipGetLastError();
 }
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
-  if (!l.n_nest_chunks) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_scan, dim3(l.n_nest_chunks), dim3(256), 0, s, b, l.nest_chunks);
+  if (!l.n_nest_empty) return hipSuccess;  // (chunks with tiles are scanned by k_nest_count)
+  hipLaunchKernelGGL(k_nest_scan, dim3(l.n_nest_empty), dim3(256), 0, s, b, l.nest_chunks);
   return hipGetLastError();
 }
 template <uint32_t R>

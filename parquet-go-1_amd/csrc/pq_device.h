@@ -121,7 +121,7 @@ struct ChunkDesc {       // 192 B
   // nested (Arrow-style) output, max_rep > 0: nest = number of list levels (0: not produced)
   uint32_t nest, nest_tile0;      // list levels; the chunk's first entry of the nested tile list
   uint32_t nest_ntiles;           // the chunk's fill tiles (nested.hip: two counting units each)
-  uint32_t nest_pkb;              // packed levels: 0 a nibble per slot (rep_bw + def_bw <= 4), 1 two bytes
+  uint32_t nest_nmask;            // flag masks per slot: 2 (nest + 1) + ngroups (k_nest_count -> k_nest_emit)
   uint8_t list_null_def[8], list_def[8];  // per REPEATED node: non-null from / has an element from
   uint64_t lvl_offsets[8];       // int32[num_lists + 1] per level
   uint64_t lvl_validity[8];      // uint32 bitmap per level
@@ -131,6 +131,7 @@ struct ChunkDesc {       // 192 B
   uint32_t ngroups, grp_tile0;    // k_group_flat: the chunk's first tile
   uint8_t group_def[8], group_depth[8];
   uint64_t group_validity[8];
+  uint64_t nest_masks;            // device u32 [nest_ntiles][nest_nmask][256]: a thread's 32 slots per mask
 };
 
 // Chunk flags

@@ -14,9 +14,13 @@ import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/trace/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 rows = [r for r in rows if "rocclr" not in r["Kernel_Name"]]
-# the last 3 steps: from the third-last k_bases backwards to the previous step's end
+# the timed loop's steps (untimed launches; the bench's per-kernel event pass comes after them): a
+# step starts with the launch that started the first (warm-up) step; print timed steps 1 and 2
 names = [r["Kernel_Name"].split("(")[0].split("::")[-1] for r in rows]
-tail = rows[-40:]
+grid = lambda r: int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+r0 = next((i for i, n in enumerate(names) if n == "k_reset"), 0)
+steps = [i for i in range(len(rows)) if names[i] == names[r0] and grid(rows[i]) == grid(rows[r0])]
+tail = rows[steps[1]:steps[3]] if len(steps) >= 4 else rows[-40:]
 t0 = int(tail[0]["Start_Timestamp"])
 for r in tail:
     s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
