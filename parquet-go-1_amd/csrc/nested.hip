@@ -297,14 +297,16 @@ struct NestCountLDS {
   uint64_t wsum[4];
   uint32_t last;
 };
-__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *tiles) {
+// R: the chunks' list levels (one launch per group of tiles, as k_nest_emit).
+template <uint32_t R>
+__global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *tiles, uint32_t first) {
+  constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestCountLDS L;
-  const uint32_t pos = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
-  const uint32_t R = cd.nest;
   // diagnostic build (tools/diag_nest.py): 0 run staging, 1 group marks, 2 expansion, 3 page counts,
   // 4 packed levels, 5 counters, 6 validity
   PQ_STAMPS(st, b.dbg);
@@ -337,13 +339,11 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
   uint32_t inm = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 4; q++) inm |= nest_inmask(nest_group(x, tid, q), 8, x.lo, endc) << (8 * q);
-  const uint32_t C = R + 1, M = cd.nest_nmask;
+  const uint32_t M = cd.nest_nmask;  // 2 C + the groups
   uint32_t *mk = gp_u64<uint32_t>(cd.nest_masks) + (uint64_t)(pos - cd.nest_tile0) * M * 256 + tid;
   uint64_t pa = 0, pb = 0;
-#pragma unroll 1
-  for (uint32_t k = 0; k < M; k++) {
-    // mask k: kind (0 flag, 1 validity, 2 group) and its level j / group g
-    const uint32_t kind = k < C ? 0u : k < 2 * C ? 1u : 2u, j = kind == 0 ? k : k - C, g = k - 2 * C;
+  // mask k < 2 C + ngroups: kind 0 (flag j = k), 1 (validity j = k - C) or 2 (group g = k - 2 C)
+  auto mask_of = [&](uint32_t kind, uint32_t j, uint32_t g) -> uint32_t {
     uint32_t m = 0;
     if (swar) {
 #pragma unroll
@@ -365,16 +365,22 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
         m |= (uint32_t)bit << i;
       }
     }
-    if (kind == 0) {
-      m &= inm;
-      pa += (uint64_t)__popc(m & 0xffffu) << (5 * j);
-      pb += (uint64_t)__popc(m >> 16) << (5 * j);
-    }
-    mk[(uint64_t)k * 256] = m;
+    return m;
+  };
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    const uint32_t m = mask_of(0, j, 0) & inm;
+    pa += (uint64_t)__popc(m & 0xffffu) << (5 * j);
+    pb += (uint64_t)__popc(m >> 16) << (5 * j);
+    mk[(uint64_t)j * 256] = m;
   }
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) mk[(uint64_t)(C + j) * 256] = mask_of(1, j, 0);
+#pragma unroll 1
+  for (uint32_t g = 0; g + 2 * C < M; g++) mk[(uint64_t)(2 * C + g) * 256] = mask_of(2, 0, g);
   st.lap(4);
 #pragma unroll
-  for (uint32_t j = 0; j < kNestCnt; j++) {
+  for (uint32_t j = 0; j < C; j++) {
     const uint32_t a2 = (uint32_t)wave_sum64((pa >> (5 * j)) & 31u), b2 = (uint32_t)wave_sum64((pb >> (5 * j)) & 31u);
     if (lane == 0) { L.part[0][j][wv] = a2; L.part[1][j][wv] = b2; }
   }
@@ -386,7 +392,7 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
   // per tile would write back the XCD's whole L2: 0.39 -> 1.16 ms), and read by atomic loads.
   if (wv == 0) {
     uint32_t seen = 0;
-    if (tid < 2 * kNestCnt) {
+    if (tid < 2 * kNestCnt && tid % kNestCnt < C) {  // (the scan reads counters j < C)
       const uint32_t h = tid / kNestCnt, j = tid % kNestCnt;
       const uint32_t v = L.part[h][j][0] + L.part[h][j][1] + L.part[h][j][2] + L.part[h][j][3];
       seen = __hip_atomic_exchange(&b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j], v, __ATOMIC_RELAXED,
@@ -485,6 +491,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     fm[j] = mk[j * 256];
     vmm[j] = mk[(C + j) * 256];
   }
+  uint64_t base0[C], base1[C];  // the halves' entry bases (k_nest_count's scan), loaded up front
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    base0[j] = b.nest_base[(2 * (uint64_t)pos) * kNestCnt + j];
+    base1[j] = b.nest_base[(2 * (uint64_t)pos + 1) * kNestCnt + j];
+  }
+  uint32_t gown = 0;  // the groups with a bitmap of their own
+  for (uint32_t gi = 0; gi < cd.ngroups; gi++) gown |= (cd.group_validity[gi] != 0 ? 1u : 0u) << gi;
   uint32_t *row = L.ent[wv];
   uint32_t *bits = L.brow[wv];
   // diagnostic build (tools/diag_nest.py): 0 masks, 1 entry indices, 2 offsets, 3 validity, 4 groups
@@ -515,7 +529,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     uint64_t run[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
-      uint64_t v = b.nest_base[(2 * (uint64_t)pos + h) * kNestCnt + j];
+      uint64_t v = h ? base1[j] : base0[j];
       for (uint32_t q = 0; q < wv; q++) v += L.wtot[h][j][q];
       run[j] = v;
     }
@@ -560,9 +574,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
     // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
     // bits go where that counter's validity goes
-    for (uint32_t gi = 0; gi < cd.ngroups; gi++) {
+    for (uint32_t gm = gown; gm; gm &= gm - 1) {  // (groups that share list / element validity: none)
+      const uint32_t gi = (uint32_t)__builtin_ctz(gm);
       uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[gi]);
-      if (!gv) continue;  // shares list / element validity (workgroup-uniform)
       const uint32_t j = cd.group_depth[gi];
       uint32_t fj = 0, pj = 0, tj = 0;
       uint64_t rj = 0;
@@ -660,9 +674,22 @@ hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_
   return hipGetLastError();
 }
 
+template <uint32_t R>
+static void launch_count_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
+  if (n) hipLaunchKernelGGL(k_nest_count<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
+}
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_nest_count, dim3(l.n_nest_tiles), dim3(256), 0, s, b, l.nest_desc);
+  // tiles are grouped by list levels (host.cpp): one instantiation per group
+  launch_count_r<1>(b, l, s);
+  launch_count_r<2>(b, l, s);
+  launch_count_r<3>(b, l, s);
+  launch_count_r<4>(b, l, s);
+  launch_count_r<5>(b, l, s);
+  launch_count_r<6>(b, l, s);
+  launch_count_r<7>(b, l, s);
+  launch_count_r<8>(b, l, s);
   return hipGetLastError();
 }
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
