@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SLOT_KERNELS = {  # bench / library timer slot -> the kernels it brackets
     "k_ba_emit": ["k_ba_emit", "k_ba_emit_slots", "k_ba_emit_slots64", "k_ba_emit_lds"],
-    "k_levels": ["k_levels", "k_levels_bw1", "k_levels_seg", "k_levels_segw", "k_levels_bw1w", "k_levels_w"],
+    "k_levels": ["k_levels", "k_levels_bw1", "k_levels_seg", "k_levels_segw", "k_levels_hyb", "k_levels_bw1w", "k_levels_w"],
     "k_values_delta": ["k_values_delta"],
     "k_values_dict": ["k_values_dict", "k_values_dict2"],
 }
