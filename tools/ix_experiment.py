@@ -1,10 +1,11 @@
 """Page-index result visibility experiment.
 
-Builds the device page index of a few fixtures `--builds` times each, in ONE process, under the
-scratch / fence knobs given in the environment (PQ_IX_POOL=1: scratch from hipMallocAsync's pool;
-PQ_IX_FENCE=1: system-scope release fences around the walk's result stores), and counts per build
-the re-reads the host needed (polls), the chunks whose completion marker never arrived
-(unreported) and the chunks that fell back. Prints one JSON line."""
+Builds the device page index of a few fixtures `--builds` times each, in ONE process, and counts per
+build the re-reads the host needed (polls), the chunks whose completion marker never arrived
+(unreported) and the chunks that fell back. Prints one JSON line. Round 3 ran it under two scratch /
+fence knobs (PQ_IX_POOL=1: scratch from hipMallocAsync's pool; PQ_IX_FENCE=1: system-scope release
+fences around the walk's result stores; profiles/r03_ix_visibility_experiment.jsonl); round 5
+removed both from the library, so today it measures the product configuration only."""
 import json
 import os
 import sys
