@@ -386,7 +386,7 @@ static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values_dict", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
-    "k_values_copy", "k_group_flat"};
+    "k_values_copy", "k_group_flat", "k_nest_tile"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -511,6 +511,9 @@ struct pqgpu_batch {
   // PQ_ONE_STREAM=1 (profiling): every launch on the batch stream, so each kernel is timed alone
   bool one_stream = getenv("PQ_ONE_STREAM") && atoi(getenv("PQ_ONE_STREAM")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
+  // Nested arrays in one pass (k_nest_tile: counts, a decoupled look-back over the chunk's earlier
+  // tiles, then the outputs) instead of k_nest_count + k_nest_emit; PQ_NEST_FUSED=0: the two passes
+  bool nest_fused = getenv("PQ_NEST_FUSED") && atoi(getenv("PQ_NEST_FUSED")) != 0;  // (on once measured)
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
   // k_values_delta) or as their own zero-LDS launch on the copy stream: fused in the speculative
   // schedule (cfg2: 0.51-0.53 ms fused against 0.56-0.58 split), split in the serial one.
@@ -562,7 +565,7 @@ struct pqgpu_batch {
   uint64_t o_pages = 0, o_chunks = 0, o_err = 0, o_nn = 0, o_rec = 0, o_vbase = 0, o_rbase = 0, o_runs = 0,
            o_run_base = 0, o_run_count = 0, o_tile_first = 0, o_tile_desc = 0, o_tile_base = 0, o_items = 0, o_lists = 0,
            o_ba_tile_sum = 0, o_ba_tile_page = 0, o_ba_tile_order = 0, o_ba_totals = 0, l_slot = 0,
-           o_ba_state = 0;
+           o_ba_state = 0, o_nest_state = 0;
   uint64_t l_level_bw1 = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
@@ -1226,6 +1229,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       n_ba_tiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
   }
   b->o_ba_state = take(n_ba_tiles * 128);  // one 128-B line per tile (bytearray.hip kStStride)
+  uint64_t n_nest_tiles = 0;  // nested tiles (k_nest_tile's look-back state, zeroed per decode)
+  for (uint32_t c = 0; c < nc; c++) {
+    const HostChunk &hc = b->chunks[c];
+    if (!hc.nest) continue;
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+      const uint64_t sb = b->pages[p].slot_base, ns = b->pages[p].num_slots;
+      n_nest_tiles += ns ? (sb + ns - 1) / kLfTileHost - sb / kLfTileHost + 1 : 0;
+    }
+  }
+  b->o_nest_state = take(n_nest_tiles * 128);  // one 128-B line per tile (nested.hip kNsStride)
   b->z_end = a;
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
@@ -1917,6 +1930,7 @@ static BatchDev batch_dev(pqgpu_batch *b) {
   d.nest_base = (uint64_t *)(A + b->o_nest_base);
   d.nest_tot = (uint64_t *)(A + b->o_nest_tot);
   d.nest_done = (uint32_t *)(A + b->o_nest_done);
+  d.nest_state = (uint64_t *)(A + b->o_nest_state);
   d.runs = (HybRun *)(A + b->o_runs);
   d.lv_runs = (uint2 *)(A + b->o_lv_runs);
   d.lv_run_base = (const uint64_t *)(A + b->o_lv_run_base);
@@ -2091,12 +2105,18 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // queued; the batch stream joins them at the end.
   if (!b->ev_levels) HIPCHECK(hipEventCreateWithFlags(&b->ev_levels, hipEventDisableTiming), err);
   if (!b->ev_nest_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_nest_join, hipEventDisableTiming), err);
+  // nested tiles on stream st: the fused pass (k_nest_tile), or k_nest_count (k_nest_emit in fork_nest)
+  auto launch_nest_pass = [&](hipStream_t st) -> hipError_t {
+    if (b->nest_fused) return timed(b, 22, st, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, st); });
+    return timed(b, 13, st, l.n_nest_tiles, [&] { return launch_nest_count(d, l, st); });
+  };
   auto fork_nest = [&]() -> hipError_t {
     if (!any_nest) return hipSuccess;
     hipError_t e = hipEventRecord(b->ev_levels, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(ds, b->ev_levels, 0);
     if (e == hipSuccess) e = timed(b, 16, ds, l.n_nest_empty, [&] { return launch_nest_scan(d, l, ds); });
-    if (e == hipSuccess) e = timed(b, 14, ds, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, ds); });
+    if (e == hipSuccess && !b->nest_fused)
+      e = timed(b, 14, ds, l.n_nest_tiles, [&] { return launch_nest_emit(d, l, ds); });
     if (e == hipSuccess) e = timed(b, 21, ds, l.n_grp_tiles, [&] { return launch_group_flat(d, l, ds); });  // flat leaves
     if (e == hipSuccess) e = hipEventRecord(b->ev_nest_join, ds);
     return e;
@@ -2192,7 +2212,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!b->levels_first && !lv_then_val)
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
-    HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
+    HIPCHECK(launch_nest_pass(s), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     HIPCHECK(fork_nest(), err);
     if (b->copy_mode == 2) HIPCHECK(fork_copies(s), err);
@@ -2208,7 +2228,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   } else {
     HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
-    HIPCHECK(timed(b, 13, s, l.n_nest_tiles, [&] { return launch_nest_count(d, l, s); }), err);
+    HIPCHECK(launch_nest_pass(s), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
@@ -2464,6 +2484,10 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
   }
   kb[0] = lvl_bytes;
+  if (b->nest_fused) {  // k_nest_tile: both passes' bytes (the flag masks between them never exist)
+    kb[22] = kb[13] + kb[14];
+    kb[13] = kb[14] = 0;
+  }
   kb[20] = b->copy_fused ? 0 : cp_bytes;            // k_values_copy
   kb[1] = dl_bytes + (b->copy_fused ? cp_bytes : 0);  // k_values_delta: DELTA pages (+ the fused copies)
   val_bytes -= snappy_direct_bytes;

@@ -24,6 +24,8 @@ struct BatchDev {
   uint64_t *nest_base;            // [nested tiles][2][kNestCnt] their exclusive prefix within the chunk
   uint64_t *nest_tot;             // [nchunks][kNestCnt] chunk totals
   uint32_t *nest_done;            // [nchunks] k_nest_count tiles finished (zeroed per decode)
+  uint64_t *nest_state;           // [nested tiles][16] k_nest_tile look-back words, one 128-B line per
+                                  // tile (zeroed per decode)
   HybRun *runs;                   // run tables of hybrid value streams
   const uint64_t *run_base;       // [npages] first entry of each page's run table
   uint32_t *run_count;            // [npages]
@@ -119,6 +121,8 @@ hipError_t launch_records(const BatchDev &b, const LaunchLists &l, hipStream_t s
 hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+// the two passes in one (count, look-back over the chunk's earlier tiles, emit): k_nest_tile
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 constexpr uint32_t kGrpTileHost = 8192;  // nested.hip kGrpTile: slots per k_group_flat workgroup
 hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // *flag |= 1 when the n words at a and b differ (pqgpu_batch_share_ancestors)

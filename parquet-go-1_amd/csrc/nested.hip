@@ -284,6 +284,53 @@ __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t
   nest_scan_chunk(b, chunks[blockIdx.x], wsum);
 }
 
+// The slots' flag masks, 32 bits per thread (bits 8q..8q+7: group q; 0-15 the first half's sixteen
+// slots, 16-31 the second's), from the thread's expanded levels lw: kind 0, the slots where counter j
+// counts (a level-(j+1) list starts, j < R; a leaf element slot, j == R); kind 1, the validity of
+// those entries (list j non-null; the element non-null); kind 2, group g's validity (def >=
+// group_def). Eight levels per 64-bit word are compared at once (SWAR: levels below 128; wider
+// levels take the byte loop).
+template <uint32_t R>
+DEV uint32_t nest_mask(const ChunkDesc &cd, const uint64_t (&lw)[2][4], bool swar, uint32_t kind, uint32_t j, uint32_t g) {
+  constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
+  auto ge = [&](uint64_t v, uint32_t t) -> uint64_t { return ((v | H) - L1 * t) & H; };  // bytes v >= t
+  auto pack8 = [](uint64_t hx) -> uint32_t {  // the high bits of the eight bytes, in byte order
+    const uint32_t lo = (uint32_t)hx >> 7, hi = (uint32_t)(hx >> 32) >> 7;
+    return ((lo * 0x01020408u) >> 24) | (((hi * 0x01020408u) >> 24) << 4);
+  };
+  uint32_t m = 0;
+  if (swar) {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint64_t rw = lw[0][q], dw = lw[1][q];
+      uint64_t f;
+      if (kind == 0) f = j < R ? ge(dw, j ? cd.list_def[j - 1] : 0u) & ~ge(rw, j + 1) : ge(dw, cd.list_def[R - 1]);
+      else if (kind == 1) f = j < R ? ge(dw, cd.list_null_def[j]) : ge(dw, cd.max_def) & ~ge(dw, cd.max_def + 1);
+      else f = ge(dw, cd.group_def[g]);
+      m |= pack8(f) << (8 * q);
+    }
+  } else {
+#pragma unroll 1
+    for (uint32_t i = 0; i < 32; i++) {
+      const uint32_t r = (uint32_t)(lw[0][i >> 3] >> (8 * (i & 7))) & 0xffu, d = (uint32_t)(lw[1][i >> 3] >> (8 * (i & 7))) & 0xffu;
+      const bool bit = kind == 0 ? nest_flag(cd, j, r, d)
+                       : kind == 1 ? (j < R ? d >= cd.list_null_def[j] : d == (uint32_t)cd.max_def)
+                                   : d >= cd.group_def[g];
+      m |= (uint32_t)bit << i;
+    }
+  }
+  return m;
+}
+// The thread's slots that both level streams cover (a failing stream covers none past its error).
+DEV uint32_t nest_cover_mask(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, const NestFill &x, uint32_t tid) {
+  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
+  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
+  uint32_t inm = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) inm |= nest_inmask(nest_group(x, tid, q), 8, x.lo, endc) << (8 * q);
+  return inm;
+}
+
 // Pass 1 over the nested chunks' fill tiles: both level streams expanded (the u8 level arrays,
 // the slot validity and the pages' record / non-null counts written from registers), the slots'
 // flag masks for pass 2 (cd.nest_masks: which counters count at a slot, the entries' validity,
@@ -327,46 +374,13 @@ __global__ void __launch_bounds__(256) k_nest_count(BatchDev b_in, const uint4 *
   // Eight levels per 64-bit word are compared at once (SWAR: levels below 128; wider levels take
   // the byte loop). The counters per half are the masks' popcounts, in 5-bit fields (at most 16
   // slots per thread and half).
-  constexpr uint64_t H = 0x8080808080808080ull, L1 = 0x0101010101010101ull;
-  auto ge = [&](uint64_t v, uint32_t t) -> uint64_t { return ((v | H) - L1 * t) & H; };  // bytes v >= t
-  auto pack8 = [](uint64_t hx) -> uint32_t {  // the high bits of the eight bytes, in byte order
-    const uint32_t lo = (uint32_t)hx >> 7, hi = (uint32_t)(hx >> 32) >> 7;
-    return ((lo * 0x01020408u) >> 24) | (((hi * 0x01020408u) >> 24) << 4);
-  };
   const bool swar = cd.max_def < 128;
-  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
-  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
-  uint32_t inm = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 4; q++) inm |= nest_inmask(nest_group(x, tid, q), 8, x.lo, endc) << (8 * q);
+  const uint32_t inm = nest_cover_mask(b, pd, cd, x, tid);
   const uint32_t M = cd.nest_nmask;  // 2 C + the groups
   uint32_t *mk = gp_u64<uint32_t>(cd.nest_masks) + (uint64_t)(pos - cd.nest_tile0) * M * 256 + tid;
   uint64_t pa = 0, pb = 0;
   // mask k < 2 C + ngroups: kind 0 (flag j = k), 1 (validity j = k - C) or 2 (group g = k - 2 C)
-  auto mask_of = [&](uint32_t kind, uint32_t j, uint32_t g) -> uint32_t {
-    uint32_t m = 0;
-    if (swar) {
-#pragma unroll
-      for (uint32_t q = 0; q < 4; q++) {
-        const uint64_t rw = lw[0][q], dw = lw[1][q];
-        uint64_t f;
-        if (kind == 0) f = j < R ? ge(dw, j ? cd.list_def[j - 1] : 0u) & ~ge(rw, j + 1) : ge(dw, cd.list_def[R - 1]);
-        else if (kind == 1) f = j < R ? ge(dw, cd.list_null_def[j]) : ge(dw, cd.max_def) & ~ge(dw, cd.max_def + 1);
-        else f = ge(dw, cd.group_def[g]);
-        m |= pack8(f) << (8 * q);
-      }
-    } else {
-#pragma unroll 1
-      for (uint32_t i = 0; i < 32; i++) {
-        const uint32_t r = (uint32_t)(lw[0][i >> 3] >> (8 * (i & 7))) & 0xffu, d = (uint32_t)(lw[1][i >> 3] >> (8 * (i & 7))) & 0xffu;
-        const bool bit = kind == 0 ? nest_flag(cd, j, r, d)
-                         : kind == 1 ? (j < R ? d >= cd.list_null_def[j] : d == (uint32_t)cd.max_def)
-                                     : d >= cd.group_def[g];
-        m |= (uint32_t)bit << i;
-      }
-    }
-    return m;
-  };
+  auto mask_of = [&](uint32_t kind, uint32_t j, uint32_t g) -> uint32_t { return nest_mask<R>(cd, lw, swar, kind, j, g); };
 #pragma unroll
   for (uint32_t j = 0; j < C; j++) {
     const uint32_t m = mask_of(0, j, 0) & inm;
@@ -474,15 +488,128 @@ struct NestEmitLDS {
   uint32_t wtot[2][R + 1][4];
   uint32_t brow[4][kNestWaveSlots / 32 + 1];
 };
+// Half h of a tile's outputs (see k_nest_emit): f[j] / vm[j], the thread's 16-bit flag and validity
+// masks of counter j in this half; base[j], the half's first entry of counter j in the chunk;
+// gown, the groups with a bitmap of their own; gmask(gi), group gi's 16-bit validity mask.
+template <uint32_t R, class GM>
+DEV void nest_emit_half(const BatchDev &b, const ChunkDesc &cd, const NestFill &x, uint32_t tid, uint32_t h,
+                        const uint32_t (&f)[R + 1], const uint32_t (&vm)[R + 1], const uint64_t (&base)[R + 1],
+                        uint32_t gown, GM gmask, NestEmitLDS<R> &L, Stamps &st) {
+  constexpr uint32_t C = R + 1;
+  const uint32_t lane = lane_id(), wv = tid >> 6;
+  int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
+  uint32_t *row = L.ent[wv];
+  uint32_t *bits = L.brow[wv];
+  const int64_t g = nest_group(x, tid, 2 * h);
+  const uint64_t s = (uint64_t)((int64_t)x.sbase + g);  // the chunk slot of the lane's first slot
+  st.lap(0);
+  // entry indices: wave prefix sums, then the waves before this one in the half
+  uint32_t P[C], T[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    const uint32_t c = (uint32_t)__popc(f[j]);
+    const uint32_t incl = (uint32_t)wave_incl_scan64_dpp(c);
+    P[j] = incl - c;
+    T[j] = (uint32_t)__shfl(incl, 63);
+    if (lane == 0) L.wtot[h][j][wv] = T[j];
+  }
+  wg_barrier();  // wtot[h] complete (double-buffered: no barrier before the next half's stores)
+  uint64_t run[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    uint64_t v = base[j];
+    for (uint32_t q = 0; q < wv; q++) v += L.wtot[h][j][q];
+    run[j] = v;
+  }
+  st.lap(1);
+  // list offsets of each level, then the record offsets (level-1 list starts)
+#pragma unroll
+  for (uint32_t j = 0; j <= R; j++) {
+    const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
+    if (j == R && !rec) break;
+    if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
+    uint32_t m = f[lv], k = P[lv];
+    const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
+    while (m) {
+      const uint32_t i = __builtin_ctz(m);
+      m &= m - 1;
+      row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
+    }
+    wave_lds_sync();
+    int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
+    for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
+    wave_lds_sync();
+  }
+  st.lap(2);
+  // validity bits of every counter's entries
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    if (PQ_ABLATE(b, 17)) break;  // diagnostic bit 17: no bitmaps
+    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+    wave_lds_sync();
+    const uint32_t c = (uint32_t)__popc(f[j]);
+    if (c) {
+      const uint32_t comp = compress32(vm[j], f[j]), p = P[j], sh = p & 31;
+      atomicOr(&bits[p >> 5], comp << sh);
+      if (sh && sh + c > 32) atomicOr(&bits[(p >> 5) + 1], comp >> (32 - sh));
+    }
+    wave_lds_sync();
+    nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
+    wave_lds_sync();
+  }
+  st.lap(3);
+  // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
+  // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
+  // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
+  // bits go where that counter's validity goes
+  for (uint32_t gm = gown; gm; gm &= gm - 1) {  // (groups that share list / element validity: none)
+    const uint32_t gi = (uint32_t)__builtin_ctz(gm);
+    uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[gi]);
+    const uint32_t j = cd.group_depth[gi];
+    uint32_t fj = 0, pj = 0, tj = 0;
+    uint64_t rj = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
+      if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
+    const uint32_t vg = gmask(gi);
+    if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
+    wave_lds_sync();
+    const uint32_t c = (uint32_t)__popc(fj);
+    if (c) {
+      const uint32_t comp = compress32(vg, fj), sh = pj & 31;
+      atomicOr(&bits[pj >> 5], comp << sh);
+      if (sh && sh + c > 32) atomicOr(&bits[(pj >> 5) + 1], comp >> (32 - sh));
+    }
+    wave_lds_sync();
+    nest_put_bits(gv, rj, bits, tj, lane);
+    wave_lds_sync();
+  }
+  st.lap(4);
+}
+DEV uint32_t nest_groups_owned(const ChunkDesc &cd) {  // the groups with a bitmap of their own
+  uint32_t gown = 0;
+  for (uint32_t gi = 0; gi < cd.ngroups; gi++) gown |= (cd.group_validity[gi] != 0 ? 1u : 0u) << gi;
+  return gown;
+}
+
+// Pass 2: per fill tile and 4,096-slot half, from the levels k_nest_count packed: wave w owns
+// 1,024 consecutive slots, lane i sixteen of them. Per counter j a lane holds the 16-bit mask of
+// its flagged slots; wave prefix sums of their counts (and one workgroup exchange of the wave
+// totals) give every entry its index. List offsets (the child counter's index at the list's first
+// slot) and record offsets (counter 0: a level-1 list starts at rep == 0, ColumnStore.get's record
+// split) are staged in a per-wave LDS row in entry order and leave as contiguous stores; the
+// entries' validity bits are compressed out of the lane's slot mask, placed at their index in a
+// per-wave LDS bit row and written with a funnel shift to their place in the bitmap.
+// R: the chunks' list levels (the launch covers the tiles of chunks with nest == R, so every
+// per-counter array is indexed by compile-time constants and stays in registers).
 template <uint32_t R>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 8 : R <= 3 ? 4 : 2))) k_nest_emit(BatchDev b_in, const uint4 *tiles, uint32_t first) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestEmitLDS<R> L;
-  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x;
   const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const ChunkDesc &cd = b.chunks[x.chunk];
-  int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
   // the thread's flag and validity masks (k_nest_count): bits 16 h .. 16 h + 15 for half h
   const uint32_t *mk = gp_u64<const uint32_t>(cd.nest_masks) + (uint64_t)(pos - cd.nest_tile0) * cd.nest_nmask * 256 + tid;
   uint32_t fm[C], vmm[C];
@@ -497,106 +624,193 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     base0[j] = b.nest_base[(2 * (uint64_t)pos) * kNestCnt + j];
     base1[j] = b.nest_base[(2 * (uint64_t)pos + 1) * kNestCnt + j];
   }
-  uint32_t gown = 0;  // the groups with a bitmap of their own
-  for (uint32_t gi = 0; gi < cd.ngroups; gi++) gown |= (cd.group_validity[gi] != 0 ? 1u : 0u) << gi;
-  uint32_t *row = L.ent[wv];
-  uint32_t *bits = L.brow[wv];
+  const uint32_t gown = nest_groups_owned(cd);
   // diagnostic build (tools/diag_nest.py): 0 masks, 1 entry indices, 2 offsets, 3 validity, 4 groups
   PQ_STAMPS(st, b.dbg);
   st.begin();
 #pragma unroll 1
   for (uint32_t h = 0; h < 2; h++) {
-    const int64_t g = nest_group(x, tid, 2 * h);
-    const uint64_t s = (uint64_t)((int64_t)x.sbase + g);  // the chunk slot of the lane's first slot
     uint32_t f[C], vm[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
       f[j] = (fm[j] >> (16 * h)) & 0xffffu;
       vm[j] = (vmm[j] >> (16 * h)) & 0xffffu;
     }
-    st.lap(0);
-    // entry indices: wave prefix sums, then the waves before this one in the half
-    uint32_t P[C], T[C];
+    auto gmask = [&](uint32_t gi) -> uint32_t { return (mk[(2 * C + gi) * 256] >> (16 * h)) & 0xffffu; };
+    nest_emit_half<R>(b, cd, x, tid, h, f, vm, h ? base1 : base0, gown, gmask, L, st);
+  }
+  st.flush(32);
+}
+
+// ---------------------------------------------------------------------------
+// k_nest_tile: both passes in one launch. A tile expands its levels and computes its flag masks and
+// per-half counts as k_nest_count does, publishes the tile's counts, finds its entry bases by a
+// decoupled look-back over the chunk's earlier tiles (wave 0; one 64-bit word per counter carrying
+// its own state: aggregate, then inclusive prefix), and emits as k_nest_emit does from the masks it
+// holds in registers: no flag masks, counts or bases go through memory, no per-chunk scan and no
+// second launch. The chunk's last tile writes the chunk totals and the closing offsets. A tile waits
+// only for tiles of its chunk with lower block indices (dispatched before it).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kNsStride = 16;  // u64 per tile: one 128-B line (no two tiles' atomics share a line)
+constexpr uint32_t kNsWin = 16;     // predecessors read per look-back round trip
+constexpr uint64_t kNsAgg = 1ull << 62, kNsIncl = 2ull << 62, kNsMask = (1ull << 62) - 1;
+
+template <uint32_t C>
+DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
+  uint64_t *st = b.nest_state;
+  const uint32_t lane = lane_id(), j0 = pos - cd.nest_tile0;
+  auto publish = [&](uint64_t flag, const uint64_t (&v)[C]) {
+    uint64_t w = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < C; q++)
+      if (lane == q) w = flag | v[q];  // (selects: no dynamic register index)
+    if (lane < C)
+      __hip_atomic_exchange(&st[(uint64_t)pos * kNsStride + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+#pragma unroll
+  for (uint32_t q = 0; q < C; q++) pre[q] = 0;
+  if (j0 == 0) {
+    publish(kNsIncl, agg);
+    return;
+  }
+  publish(kNsAgg, agg);
+  int64_t k = (int64_t)pos - 1;  // the nearest tile not yet added
+  for (;;) {
+    const int64_t my = k - (int64_t)lane;
+    const bool win = lane < kNsWin, valid = win && my >= (int64_t)cd.nest_tile0;
+    uint64_t s[C];
+    bool rdy = true, inc = true;
+#pragma unroll
+    for (uint32_t q = 0; q < C; q++) {
+      // past the chunk's first tile: an inclusive prefix of 0
+      s[q] = valid ? __hip_atomic_load(&st[(uint64_t)my * kNsStride + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kNsIncl;
+      rdy &= s[q] != 0;
+      inc &= (s[q] & ~kNsMask) == kNsIncl;
+    }
+    const uint64_t incl = __ballot(win && rdy && inc), hole = __ballot(win && !rdy);
+    const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+    const uint32_t h = hole ? (uint32_t)__builtin_ctzll(hole) : 64u;
+    const uint32_t upto = min(min(stop + 1, h), kNsWin);  // lanes [0, upto) are added
+#pragma unroll
+    for (uint32_t q = 0; q < C; q++) pre[q] += wave_sum64(lane < upto ? (s[q] & kNsMask) : 0);
+    if (stop < h) break;  // reached an inclusive prefix (or the chunk's first tile)
+    k -= upto;
+    if (h < 64) __builtin_amdgcn_s_sleep(2);
+  }
+  uint64_t inc[C];
+#pragma unroll
+  for (uint32_t q = 0; q < C; q++) inc[q] = pre[q] + agg[q];
+  publish(kNsIncl, inc);
+}
+
+template <uint32_t R>
+struct NestTileLDS {
+  union {
+    struct {
+      NestStage st;
+      uint32_t vb[kLfTile / 32];  // slot validity of the tile (16 bits per thread and half)
+    } a;                          // counting
+    NestEmitLDS<R> e;             // emission
+  } u;
+  uint32_t part[2][R + 1][4];
+  uint32_t gmk[PQGPU_MAX_NEST][256];  // the owned groups' validity masks (the levels are not kept)
+  uint64_t base[R + 1];  // the tile's first entry of each counter (the look-back's prefix)
+  uint32_t half0[R + 1]; // the first half's entries of each counter
+};
+template <uint32_t R>
+#ifndef PQ_NEST_TILE_WPE1
+#define PQ_NEST_TILE_WPE1 5
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first) {
+  constexpr uint32_t C = R + 1;
+  const BatchDev b = global_view(b_in);
+  __shared__ NestTileLDS<R> L;
+  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const NestFill x = nest_fill(b, gp(tiles)[pos]);
+  const PageDesc &pd = b.pages[x.pi];
+  const ChunkDesc &cd = b.chunks[x.chunk];
+  // diagnostic build: k_nest_count's stamps 0-3 (expansion), then 0-4 of the emission
+  PQ_STAMPS(st, b.dbg);
+  st.begin();
+  uint64_t lw[2][4];
+  uint32_t eqd[4], end_d = 0;
+  nest_expand(b, pd, cd, x, L.u.a.st, tid, lw, eqd, end_d, st);
+  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  const bool vtile = vbits && x.lo < end_d;  // workgroup-uniform
+  if (vtile) {
+    reinterpret_cast<uint16_t *>(L.u.a.vb)[tid] = (uint16_t)(eqd[0] | (eqd[1] << 8));
+    reinterpret_cast<uint16_t *>(L.u.a.vb)[256 + tid] = (uint16_t)(eqd[2] | (eqd[3] << 8));
+  }
+  const bool swar = cd.max_def < 128;
+  const uint32_t inm = nest_cover_mask(b, pd, cd, x, tid);
+  const uint32_t gown = nest_groups_owned(cd);
+  for (uint32_t gm = gown; gm; gm &= gm - 1) {
+    const uint32_t gi = (uint32_t)__builtin_ctz(gm);
+    L.gmk[gi][tid] = nest_mask<R>(cd, lw, swar, 2, 0, gi);
+  }
+  uint32_t fm[C], vmm[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    fm[j] = nest_mask<R>(cd, lw, swar, 0, j, 0) & inm;
+    vmm[j] = nest_mask<R>(cd, lw, swar, 1, j, 0);
+    const uint32_t a2 = (uint32_t)wave_sum64((uint32_t)__popc(fm[j] & 0xffffu)), b2 = (uint32_t)wave_sum64((uint32_t)__popc(fm[j] >> 16));
+    if (lane == 0) { L.part[0][j][wv] = a2; L.part[1][j][wv] = b2; }
+  }
+  wg_barrier();  // part and vb complete
+  if (wv == 0) {
+    uint64_t agg[C], pre[C];
+    uint32_t h0[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
-      const uint32_t c = (uint32_t)__popc(f[j]);
-      const uint32_t incl = (uint32_t)wave_incl_scan64_dpp(c);
-      P[j] = incl - c;
-      T[j] = (uint32_t)__shfl(incl, 63);
-      if (lane == 0) L.wtot[h][j][wv] = T[j];
+      h0[j] = L.part[0][j][0] + L.part[0][j][1] + L.part[0][j][2] + L.part[0][j][3];
+      agg[j] = h0[j] + L.part[1][j][0] + L.part[1][j][1] + L.part[1][j][2] + L.part[1][j][3];
     }
-    wg_barrier();  // wtot[h] complete (double-buffered: no barrier before the next half's stores)
-    uint64_t run[C];
+    nest_lookback<C>(b, cd, pos, agg, pre);
+#pragma unroll
+    for (uint32_t j = 0; j < C; j++)
+      if (lane == j) { L.base[j] = pre[j]; L.half0[j] = h0[j]; }
+    if (pos - cd.nest_tile0 == cd.nest_ntiles - 1) {  // the chunk's last tile: totals, closing entries
+      uint64_t tot[C];
+#pragma unroll
+      for (uint32_t j = 0; j < C; j++) {
+        tot[j] = pre[j] + agg[j];
+        if (lane == j) b.nest_tot[(uint64_t)x.chunk * kNestCnt + j] = tot[j];
+      }
+      int32_t *rec = gp_u64<int32_t>(cd.list_offsets);
+#pragma unroll
+      for (uint32_t j = 0; j < R; j++)
+        if (lane == j) gp_u64<int32_t>(cd.lvl_offsets[j])[tot[j]] = (int32_t)tot[j + 1];
+      if (lane == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
+    }
+  }
+  // slot validity (definition level == max_def) of the definition stream's covered values
+  if (vtile) {
+    const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
+    const int64_t w0 = x.t0 + 32 * (int64_t)w;
+    if (w0 + 32 > (int64_t)x.lo && w0 < (int64_t)end_d) {
+      const uint32_t v = L.u.a.vb[w];
+      uint32_t *dst = vbits + ((x.sbase + (uint64_t)w0) >> 5);
+      if (w0 >= (int64_t)x.lo && w0 + 32 <= (int64_t)end_d) *dst = v;  // the tile owns the whole word
+      else if (v) atomicOr(dst, v);                                     // shared with a neighbouring page
+    }
+  }
+  wg_barrier();  // base complete; the counting LDS is free for the emission
+  uint64_t base0[C], base1[C];
+#pragma unroll
+  for (uint32_t j = 0; j < C; j++) {
+    base0[j] = L.base[j];
+    base1[j] = base0[j] + L.half0[j];
+  }
+#pragma unroll 1
+  for (uint32_t h = 0; h < 2; h++) {
+    uint32_t f[C], vm[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
-      uint64_t v = h ? base1[j] : base0[j];
-      for (uint32_t q = 0; q < wv; q++) v += L.wtot[h][j][q];
-      run[j] = v;
+      f[j] = (fm[j] >> (16 * h)) & 0xffffu;
+      vm[j] = (vmm[j] >> (16 * h)) & 0xffffu;
     }
-    st.lap(1);
-    // list offsets of each level, then the record offsets (level-1 list starts)
-#pragma unroll
-    for (uint32_t j = 0; j <= R; j++) {
-      const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
-      if (j == R && !rec) break;
-      if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
-      uint32_t m = f[lv], k = P[lv];
-      const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
-      while (m) {
-        const uint32_t i = __builtin_ctz(m);
-        m &= m - 1;
-        row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
-      }
-      wave_lds_sync();
-      int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
-      for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
-      wave_lds_sync();
-    }
-    st.lap(2);
-    // validity bits of every counter's entries
-#pragma unroll
-    for (uint32_t j = 0; j < C; j++) {
-      if (PQ_ABLATE(b, 17)) break;  // diagnostic bit 17: no bitmaps
-      if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
-      wave_lds_sync();
-      const uint32_t c = (uint32_t)__popc(f[j]);
-      if (c) {
-        const uint32_t comp = compress32(vm[j], f[j]), p = P[j], sh = p & 31;
-        atomicOr(&bits[p >> 5], comp << sh);
-        if (sh && sh + c > 32) atomicOr(&bits[(p >> 5) + 1], comp >> (32 - sh));
-      }
-      wave_lds_sync();
-      nest_put_bits(gp_u64<uint32_t>(j < R ? cd.lvl_validity[j] : cd.elem_validity), run[j], bits, T[j], lane);
-      wave_lds_sync();
-    }
-    st.lap(3);
-    // struct validity of the OPTIONAL groups that own a bitmap (Column.getNextData schema.go:216-260:
-    // a group is non-nil iff a child is defined at or below it, def >= group_def): its entries are
-    // those of counter group_depth (the level-(depth + 1) lists, or the leaf's element slots), so the
-    // bits go where that counter's validity goes
-    for (uint32_t gm = gown; gm; gm &= gm - 1) {  // (groups that share list / element validity: none)
-      const uint32_t gi = (uint32_t)__builtin_ctz(gm);
-      uint32_t *gv = gp_u64<uint32_t>(cd.group_validity[gi]);
-      const uint32_t j = cd.group_depth[gi];
-      uint32_t fj = 0, pj = 0, tj = 0;
-      uint64_t rj = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < C; q++)  // selects: a dynamic index would put the arrays in scratch
-        if (q == j) { fj = f[q]; pj = P[q]; tj = T[q]; rj = run[q]; }
-      const uint32_t vg = (mk[(2 * C + gi) * 256] >> (16 * h)) & 0xffffu;
-      if (lane <= kNestWaveSlots / 32) bits[lane] = 0;
-      wave_lds_sync();
-      const uint32_t c = (uint32_t)__popc(fj);
-      if (c) {
-        const uint32_t comp = compress32(vg, fj), sh = pj & 31;
-        atomicOr(&bits[pj >> 5], comp << sh);
-        if (sh && sh + c > 32) atomicOr(&bits[(pj >> 5) + 1], comp >> (32 - sh));
-      }
-      wave_lds_sync();
-      nest_put_bits(gv, rj, bits, tj, lane);
-      wave_lds_sync();
-    }
-    st.lap(4);
+    auto gmask = [&](uint32_t gi) -> uint32_t { return (L.gmk[gi][tid] >> (16 * h)) & 0xffffu; };
+    nest_emit_half<R>(b, cd, x, tid, h, f, vm, h ? base1 : base0, gown, gmask, L.u.e, st);
   }
   st.flush(32);
 }
@@ -701,6 +915,25 @@ template <uint32_t R>
 static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
   if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
+}
+template <uint32_t R>
+static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
+  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
+}
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_nest_tiles) return hipSuccess;
+  // tiles are grouped by list levels (host.cpp): one instantiation per group; a chunk's tiles are
+  // contiguous and in slot order within one launch (the look-back's predecessors)
+  launch_tile_r<1>(b, l, s);
+  launch_tile_r<2>(b, l, s);
+  launch_tile_r<3>(b, l, s);
+  launch_tile_r<4>(b, l, s);
+  launch_tile_r<5>(b, l, s);
+  launch_tile_r<6>(b, l, s);
+  launch_tile_r<7>(b, l, s);
+  launch_tile_r<8>(b, l, s);
+  return hipGetLastError();
 }
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_nest_tiles) return hipSuccess;

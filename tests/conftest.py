@@ -24,3 +24,14 @@ def pytest_configure(config):
 def gpu_ctx():
     import pqgpu
     return pqgpu.Context(0)
+
+
+@pytest.fixture(params=["fused", "two_pass"])
+def nest_mode(request, monkeypatch):
+    """Nested arrays by k_nest_tile (one pass with a decoupled look-back, the default) and by
+    k_nest_count + k_nest_emit (PQ_NEST_FUSED=0): both must give the reference's arrays."""
+    if request.param == "two_pass":
+        monkeypatch.setenv("PQ_NEST_FUSED", "0")
+    else:
+        monkeypatch.delenv("PQ_NEST_FUSED", raising=False)
+    return request.param

@@ -135,7 +135,7 @@ def _gpu_nested_all(gpu_ctx, data):
 @pytest.mark.gpu
 @pytest.mark.parametrize("doc", sorted({d for d, _ in GOLDEN}))
 @pytest.mark.parametrize("v2", [False, True])
-def test_gpu_ref_documents(gpu_ctx, doc, v2):
+def test_gpu_ref_documents(gpu_ctx, nest_mode, doc, v2):
     f, b, ids = _gpu_nested_all(gpu_ctx, G.build(doc, v2))
     for (rg, col), cid in ids.items():
         path = f.column_paths()[col]
@@ -149,7 +149,7 @@ def test_gpu_ref_documents(gpu_ctx, doc, v2):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", _nested_fixtures() + ["edge_nulls_v1", "types_v2"])
-def test_gpu_nested_vs_ref(gpu_ctx, name):
+def test_gpu_nested_vs_ref(gpu_ctx, nest_mode, name):
     if name not in pqtest.ALL:
         pytest.skip("fixture absent")
     data = pqtest.load(name)
@@ -202,7 +202,7 @@ def _deep_file(version):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
-def test_gpu_deep_nesting(gpu_ctx, version):
+def test_gpu_deep_nesting(gpu_ctx, nest_mode, version):
     """Nested arrays, levels and values of a two-list-level leaf with maxD 6 (byte-packed levels in
     k_nest_count / k_nest_emit) against the oracle, over pages that share fill tiles."""
     data = _deep_file(version)

@@ -138,7 +138,7 @@ def _decode_all(gpu_ctx, data):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", STRUCT_FIXTURES + ["cfg4_small", "cfg4_v2", "types_v1", "edge_nulls_v2"])
-def test_gpu_groups_vs_tree_ref(gpu_ctx, name):
+def test_gpu_groups_vs_tree_ref(gpu_ctx, nest_mode, name):
     data = pqtest.load(name)
     f, b, ids = _decode_all(gpu_ctx, data)
     for rg, col, path, reps, o in _oracle_chunks(data):
@@ -160,7 +160,7 @@ def test_gpu_groups_vs_tree_ref(gpu_ctx, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("v2", [False, True])
-def test_gpu_links_group(gpu_ctx, v2):
+def test_gpu_links_group(gpu_ctx, nest_mode, v2):
     data = G.build("dremel", v2)
     f, b, ids = _decode_all(gpu_ctx, data)
     paths = f.column_paths()
@@ -178,7 +178,7 @@ def _sibling_pairs(paths):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", STRUCT_FIXTURES + ["cfg4_small"])
-def test_gpu_share_ancestors(gpu_ctx, name):
+def test_gpu_share_ancestors(gpu_ctx, nest_mode, name):
     """Sibling leaves of one group (a MAP's key and value; struct fields) decode identical arrays
     for their common ancestors; after the check the second leaf's result carries the first's
     (one offsets array per shared list level, one bitmap per shared group)."""
@@ -263,7 +263,7 @@ def _three_leaf_file():
 
 
 @pytest.mark.gpu
-def test_gpu_share_ancestors_mixed_depths(gpu_ctx):
+def test_gpu_share_ancestors_mixed_depths(gpu_ctx, nest_mode):
     """Leaf b.y first shares one list level with the shallower leaf x, then two list levels with its
     sibling b.z: b.z must take levels it shares with b.y from b.y (whose own result resolves level 0
     through x), not from the chain's root x, which has no level 1. Every result keeps its contents."""

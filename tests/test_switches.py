@@ -18,6 +18,7 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_LV_SEGW=1/0     generic level streams by segment speculation (k_levels_segw): all of them, or
                      none (default 2: the definition streams)
 - PQ_LV_HYB=0        repetition streams by k_levels' list ranking instead of k_levels_hyb
+- PQ_NEST_FUSED=0    nested arrays by k_nest_count + k_nest_emit instead of k_nest_tile
 """
 import pytest
 
@@ -48,6 +49,7 @@ SWITCHES = {
     "lv_segw": {"PQ_LV_SEGW": "1"},
     "lv_segw_none": {"PQ_LV_SEGW": "0"},
     "lv_hyb_off": {"PQ_LV_HYB": "0"},
+    "nest_two_pass": {"PQ_NEST_FUSED": "0"},
 }
 
 
