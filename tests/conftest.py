@@ -30,8 +30,5 @@ def gpu_ctx():
 def nest_mode(request, monkeypatch):
     """Nested arrays by k_nest_tile (one pass with a decoupled look-back, the default) and by
     k_nest_count + k_nest_emit (PQ_NEST_FUSED=0): both must give the reference's arrays."""
-    if request.param == "two_pass":
-        monkeypatch.setenv("PQ_NEST_FUSED", "0")
-    else:
-        monkeypatch.delenv("PQ_NEST_FUSED", raising=False)
+    monkeypatch.setenv("PQ_NEST_FUSED", "0" if request.param == "two_pass" else "1")
     return request.param
