@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dev_util.h"
+#include "dict_slots.h"
 #include "dict_tile.h"
 
 namespace pq {
@@ -233,31 +234,11 @@ DEV void global_put(uint8_t *dst, const uint8_t *src, uint32_t len) {
 }
 
 // ---------------------------------------------------------------------------
-// Dictionary slots: entry i at slots + (i << slot_shift) = [u32 length | bytes | zero pad].
-// One thread per entry; blockIdx.y = the chunk (list of chunks with a slot table).
+// Dictionary slots (dict_slots.h); blockIdx.y = the chunk (list of chunks with a slot table).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_dict_slots(BatchDev b_in, const uint32_t *chunks) {
   const BatchDev b = global_view(b_in);
-  const ChunkDesc &cd = b.chunks[chunks[blockIdx.y]];
-  const uint32_t S = cd.slot_shift;
-  const uint2 *ent = gp_u64<const uint2>(cd.dict_offsets);
-  const uint8_t *raw = gp_u64<const uint8_t>(cd.dict_raw);
-  uint4 *slots = gp_u64<uint4>(cd.dict_slots);
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cd.dict_count; i += gridDim.x * 256) {
-    const uint2 e = ent[i];
-    const uint32_t n = e.y + 4;  // slot bytes in use; slot byte o holds entry byte o - 4
-    for (uint32_t q = 0; q < (1u << S) / 16; q++) {
-      uint32_t w[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t o = 16 * q + 4 * j;
-        if (o == 0) { w[j] = e.y; continue; }
-        const uint32_t x = o < n ? ld32(raw + e.x + (o - 4)) : 0u;
-        w[j] = o + 4 <= n ? x : (o < n ? x & ((1u << (8 * (n - o))) - 1u) : 0u);
-      }
-      slots[((uint64_t)i << (S - 4)) + q] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-  }
+  dict_slots_block(b, chunks[blockIdx.y], blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------

@@ -513,6 +513,9 @@ struct pqgpu_batch {
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
   // Nested arrays in one pass (k_nest_tile: counts, a decoupled look-back over the chunk's earlier
   // tiles, then the outputs) instead of k_nest_count + k_nest_emit; PQ_NEST_FUSED=0: the two passes
+  // The byte-array dictionaries' slot tables built by the run scan's launch (k_scan_slots) instead
+  // of their own launch in front of k_ba_emit; PQ_SCAN_SLOTS=0: k_dict_slots
+  bool scan_slots = !getenv("PQ_SCAN_SLOTS") || atoi(getenv("PQ_SCAN_SLOTS")) != 0;
   bool nest_fused = getenv("PQ_NEST_FUSED") && atoi(getenv("PQ_NEST_FUSED")) != 0;  // (on once measured)
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
   // k_values_delta) or as their own zero-LDS launch on the copy stream: fused in the speculative
@@ -2058,6 +2061,13 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // SNAPPY pages first: every later kernel reads page data (column-group pipeline: one launch per
   // group, each followed by an event the group's values work waits for)
   const uint32_t G = b->n_groups;
+  // the slot tables beside the run scan (one launch; never in the column-group pipeline, whose
+  // scans go out per group)
+  const bool slots_early = b->scan_slots && !G && l.n_slot_chunks && l.n_scan_pages;
+  auto scan_runs = [&](hipStream_t st) -> hipError_t {
+    if (slots_early) return timed(b, 2, st, l.n_scan_pages, [&] { return launch_scan_slots(d, l, st); });
+    return timed(b, 2, st, l.n_scan_pages, [&] { return launch_scan_runs(d, l, st); });
+  };
   if (G) {
     // flat REQUIRED pages only: k_bases needs no page data, and every group's values follow it
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
@@ -2198,7 +2208,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
     if (v != s) HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(fork_delta(b->ev_fork), err);
-    HIPCHECK(timed(b, 2, v, l.n_scan_pages, [&] { return launch_scan_runs(d, l, v); }), err);
+    HIPCHECK(scan_runs(v), err);
     if (b->copy_mode == 0) HIPCHECK(fork_copies(s), err);
     if (b->copy_mode == 6)  // the copies first on the side stream, then the LDS kinds
       HIPCHECK(timed(b, 20, v, l.n_copy_items, [&] { return launch_values_copy(d, l, v); }), err);
@@ -2241,7 +2251,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(fork_delta(b->ev_fork), err);
     }
     HIPCHECK(fork_nest(), err);  // on the DELTA stream after its pages
-    HIPCHECK(timed(b, 2, s, l.n_scan_pages, [&] { return launch_scan_runs(d, l, s); }), err);
+    HIPCHECK(scan_runs(s), err);
     HIPCHECK(timed(b, 8, s, n_dict, [&] { return launch_values_dict(d, dict_items, b->n_dict2_items, n_dict, s); }), err);
     HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
@@ -2255,7 +2265,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   if (!b->ba_chunks.empty()) {
     // byte-array outputs: tile payload sums, per-chunk scan, offsets + payload (bytearray.hip)
-    HIPCHECK(timed(b, 12, s, l.n_slot_chunks, [&] { return launch_dict_slots(d, l, s); }), err);
+    if (!slots_early) HIPCHECK(timed(b, 12, s, l.n_slot_chunks, [&] { return launch_dict_slots(d, l, s); }), err);
     if (b->any_ba_sync || b->ba_presum) {
       HIPCHECK(timed(b, 4, s, l.n_ba_tiles, [&] { return launch_ba_sums(d, l, s); }), err);
       HIPCHECK(timed(b, 5, s, l.n_ba_chunks, [&] { return launch_ba_scan(d, l, s); }), err);
@@ -2484,6 +2494,10 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
   }
   kb[0] = lvl_bytes;
+  if (b->scan_slots && !b->n_groups && !b->slot_chunks.empty() && !b->scan_pages.empty()) {  // k_scan_slots
+    kb[2] += kb[12];
+    kb[12] = 0;
+  }
   if (b->nest_fused) {  // k_nest_tile: both passes' bytes (the flag masks between them never exist)
     kb[22] = kb[13] + kb[14];
     kb[13] = kb[14] = 0;

@@ -106,6 +106,7 @@ constexpr uint32_t kSgStageHost = 10240;  // k_levels_seg's LDS stage (kernels.h
 constexpr uint32_t kSgwStageHost = 57344; // k_levels_segw's LDS stage (kernels.hip kSgwStage)
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_scan_slots(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // k_scan_runs + k_dict_slots
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values_copy(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_values_delta(const BatchDev &b, const WorkItem *items, uint32_t n, hipStream_t s);  // DELTA items only

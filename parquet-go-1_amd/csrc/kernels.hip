@@ -19,6 +19,7 @@
 
 #include "../../include/pqgpu.h"
 #include "dev_util.h"
+#include "dict_slots.h"
 #include "dict_tile.h"
 #include "kernels.h"
 #include "level_fill.h"
@@ -2515,10 +2516,27 @@ struct RunSink {
   }
 };
 
+DEV void scan_runs_page(const BatchDev &b, uint32_t pi, ScanLDS &lds);
 __global__ void __launch_bounds__(256) k_scan_runs(BatchDev b_in, const uint32_t *pages) {
   const BatchDev b = global_view(b_in);
   __shared__ ScanLDS lds;
-  const uint32_t pi = pages[blockIdx.x];
+  scan_runs_page(b, pages[blockIdx.x], lds);
+}
+// The run scan and the byte-array dictionaries' slot tables (dict_slots.h) in one launch: blocks
+// [0, n_scan) scan pages, the next n_slot_chunks x gx blocks fill slots (no launch of their own, and
+// the slot blocks fill the CUs the page walks leave idle).
+__global__ void __launch_bounds__(256) k_scan_slots(BatchDev b_in, const uint32_t *pages, uint32_t n_scan,
+                                                    const uint32_t *slot_chunks, uint32_t gx) {
+  const BatchDev b = global_view(b_in);
+  __shared__ ScanLDS lds;
+  if (blockIdx.x < n_scan) {
+    scan_runs_page(b, pages[blockIdx.x], lds);
+  } else {
+    const uint32_t k = blockIdx.x - n_scan;
+    dict_slots_block(b, slot_chunks[k / gx], k % gx, gx);
+  }
+}
+DEV void scan_runs_page(const BatchDev &b, uint32_t pi, ScanLDS &lds) {
   const PageDesc pd = b.pages[pi];
   const uint32_t nn = b.page_nn_v[pi];
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
@@ -4635,6 +4653,12 @@ hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s) 
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
   if (!l.n_scan_pages) return hipSuccess;
   hipLaunchKernelGGL(k_scan_runs, dim3(l.n_scan_pages), dim3(256), 0, s, b, l.scan_pages);
+  return hipGetLastError();
+}
+hipError_t launch_scan_slots(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  const uint32_t n = l.n_scan_pages + l.n_slot_chunks * l.slot_grid_x;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_scan_slots, dim3(n), dim3(256), 0, s, b, l.scan_pages, l.n_scan_pages, l.slot_chunks, l.slot_grid_x);
   return hipGetLastError();
 }
 hipError_t launch_values(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

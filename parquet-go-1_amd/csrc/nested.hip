@@ -654,6 +654,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
 constexpr uint32_t kNsStride = 16;  // u64 per tile: one 128-B line (no two tiles' atomics share a line)
 constexpr uint32_t kNsWin = 16;     // predecessors read per look-back round trip
 constexpr uint64_t kNsAgg = 1ull << 62, kNsIncl = 2ull << 62, kNsMask = (1ull << 62) - 1;
+constexpr uint32_t kNsMaxPolls = 1u << 22;  // look-back polls before giving up (seconds: a bound, not a wait)
 
 template <uint32_t C>
 DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
@@ -675,19 +676,29 @@ DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, con
   }
   publish(kNsAgg, agg);
   int64_t k = (int64_t)pos - 1;  // the nearest tile not yet added
+  uint32_t polls = 0;
   for (;;) {
+    if (++polls > kNsMaxPolls) {  // never (a predecessor that does not publish): prefixes past any
+#pragma unroll                   // chunk's slots make the caller write nothing and report it
+      for (uint32_t q = 0; q < C; q++) pre[q] = kNsMask;
+      return;
+    }
     const int64_t my = k - (int64_t)lane;
     const bool win = lane < kNsWin, valid = win && my >= (int64_t)cd.nest_tile0;
     uint64_t s[C];
-    bool rdy = true, inc = true;
+    bool set = true, any_agg = false, any_inc = false;
 #pragma unroll
     for (uint32_t q = 0; q < C; q++) {
       // past the chunk's first tile: an inclusive prefix of 0
       s[q] = valid ? __hip_atomic_load(&st[(uint64_t)my * kNsStride + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kNsIncl;
-      rdy &= s[q] != 0;
-      inc &= (s[q] & ~kNsMask) == kNsIncl;
+      set &= s[q] != 0;
+      any_agg |= (s[q] & ~kNsMask) == kNsAgg;
+      any_inc |= (s[q] & ~kNsMask) == kNsIncl;
     }
-    const uint64_t incl = __ballot(win && rdy && inc), hole = __ballot(win && !rdy);
+    // a predecessor's C words become visible one by one: one caught between its aggregates and its
+    // inclusive prefixes (some of each) is read again, like one not yet published
+    const bool rdy = set && !(any_agg && any_inc), inc = rdy && !any_agg;
+    const uint64_t incl = __ballot(win && inc), hole = __ballot(win && !rdy);
     const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
     const uint32_t h = hole ? (uint32_t)__builtin_ctzll(hole) : 64u;
     const uint32_t upto = min(min(stop + 1, h), kNsWin);  // lanes [0, upto) are added
@@ -716,6 +727,7 @@ struct NestTileLDS {
   uint32_t gmk[PQGPU_MAX_NEST][256];  // the owned groups' validity masks (the levels are not kept)
   uint64_t base[R + 1];  // the tile's first entry of each counter (the look-back's prefix)
   uint32_t half0[R + 1]; // the first half's entries of each counter
+  uint32_t bad;          // the prefixes exceed the chunk's slots (never: no output is written then)
 };
 template <uint32_t R>
 #ifndef PQ_NEST_TILE_WPE1
@@ -766,10 +778,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       agg[j] = h0[j] + L.part[1][j][0] + L.part[1][j][1] + L.part[1][j][2] + L.part[1][j][3];
     }
     nest_lookback<C>(b, cd, pos, agg, pre);
+    bool over = false;  // a counter's entries are at most the chunk's slots (the arrays' capacity)
 #pragma unroll
-    for (uint32_t j = 0; j < C; j++)
+    for (uint32_t j = 0; j < C; j++) {
+      over |= pre[j] > cd.num_slots || pre[j] + agg[j] > cd.num_slots;
       if (lane == j) { L.base[j] = pre[j]; L.half0[j] = h0[j]; }
-    if (pos - cd.nest_tile0 == cd.nest_ntiles - 1) {  // the chunk's last tile: totals, closing entries
+    }
+    if (lane == 0) {
+      L.bad = over;
+      if (over) report(b, x.chunk, 1, pd.page_in_chunk, ST_VALUES, 0, PQ_ERR_UNSUPPORTED);  // internal error
+    }
+    if (pos - cd.nest_tile0 == cd.nest_ntiles - 1 && !over) {  // the chunk's last tile: totals, closing entries
       uint64_t tot[C];
 #pragma unroll
       for (uint32_t j = 0; j < C; j++) {
@@ -795,6 +814,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     }
   }
   wg_barrier();  // base complete; the counting LDS is free for the emission
+  if (L.bad) return;  // workgroup-uniform
   uint64_t base0[C], base1[C];
 #pragma unroll
   for (uint32_t j = 0; j < C; j++) {

@@ -18,7 +18,8 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_LV_SEGW=1/0     generic level streams by segment speculation (k_levels_segw): all of them, or
                      none (default 2: the definition streams)
 - PQ_LV_HYB=0        repetition streams by k_levels' list ranking instead of k_levels_hyb
-- PQ_NEST_FUSED=0    nested arrays by k_nest_count + k_nest_emit instead of k_nest_tile
+- PQ_NEST_FUSED=0/1  nested arrays by k_nest_count + k_nest_emit, or by k_nest_tile
+- PQ_SCAN_SLOTS=0    byte-array slot tables by their own k_dict_slots launch instead of k_scan_slots
 """
 import pytest
 
@@ -50,6 +51,8 @@ SWITCHES = {
     "lv_segw_none": {"PQ_LV_SEGW": "0"},
     "lv_hyb_off": {"PQ_LV_HYB": "0"},
     "nest_two_pass": {"PQ_NEST_FUSED": "0"},
+    "nest_fused": {"PQ_NEST_FUSED": "1"},
+    "slots_own_launch": {"PQ_SCAN_SLOTS": "0"},
 }
 
 
