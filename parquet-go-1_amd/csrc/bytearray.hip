@@ -107,38 +107,6 @@ DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
   }
 }
 
-// The same with plain stores except one ds_or: a destination word is written whole by the value that
-// owns its first byte (zeros past the value, from the slot padding); a value that starts inside a word
-// ORs that first word in afterwards (the same wave's LDS accesses execute in order, so the owner's
-// plain store lands first). Every word of a round's range is written, so the buffer needs no zeroing
-// between rounds: the carried unfinished piece holds zeros past the round's last byte.
-#ifndef PQ_BA_PLAIN
-#define PQ_BA_PLAIN 0
-#endif
-template <int NP>
-DEV void lds_put_slot_plain(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
-  constexpr int NW = 4 * NP;
-  uint32_t W[NW];
-#pragma unroll
-  for (int q = 0; q < NW / 4; q++) {
-    const uint32_t x[4] = {sl[q].x, sl[q].y, sl[q].z, sl[q].w};
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (4 * q + i >= 1) W[4 * q + i - 1] = x[i];
-  }
-  W[NW - 1] = 0;
-  const uint32_t sh = d & 3u, d0 = d >> 2, end = sh + len;
-#pragma unroll
-  for (int m = 0; m < NW; m++) {
-    if (4u * m >= end) break;
-    const uint32_t prev = m ? W[m - 1] : 0u;
-    const uint32_t word = sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m];
-    if (m || !sh) lw[d0 + m] = word;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (order: the plain stores, then the ORs)
-  if (sh && len) atomicOr(&lw[d0], __builtin_amdgcn_alignbyte(W[0], 0u, 4 - sh));
-}
-
 #ifndef PQ_BA_STORES
 #define PQ_BA_STORES 0  // 1: pass B writes slot bytes with plain LDS stores (no atomics, no zeroing);
                         // cfg3 k_ba_emit 0.55 ms against 0.43-0.46 ms with ds_or (byte stores at the edges)
@@ -432,8 +400,10 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // P0 (16- and 32-B slots): pass A loads every value's first slot piece (its length and first 12
 // bytes) instead of the length word, and keeps it; pass B loads only the second piece of entries
 // longer than 12 bytes: 1 + P(len > 12) texture requests per value instead of 2 + P(len > 12).
+// At 5 waves per SIMD (96 VGPRs) cfg3's k_ba_emit 0.358 -> 0.346 ms (profiles/r05_s29_probe_ba_p0.txt;
+// at 6 the pieces spill, at 4 it measured the same as 5).
 #ifndef PQ_BA_P0
-#define PQ_BA_P0 0
+#define PQ_BA_P0 1
 #endif
 template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool PA = false, class EL, bool P0 = false>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,
@@ -443,7 +413,6 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   constexpr uint32_t G = 2;              // rounds per load group
   const uint32_t s4 = cd.slot_shift - 4; // SLOT: uint4 per slot = 1 << s4
   constexpr uint32_t R = kRounds;
-  constexpr bool PLAIN = PQ_BA_PLAIN && SLOT && SV == 2 && !PA;  // (ds_or assembly otherwise)
   const uint64_t vb = b.page_vbase[p];
   int32_t *offs = gp_u64<int32_t>(cd.offsets) + vb;
   uint8_t *P = gp_u64<uint8_t>(cd.payload);
@@ -594,7 +563,6 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         } else if (l) {
           if constexpr (SLOT) {
             if (PQ_BA_STORES) lds_put_slot_st<SV>(lb, cur + ex, sl[rr], l);
-            else if (PLAIN) lds_put_slot_plain<SV>(lw, cur + ex, sl[rr], l);
             else lds_put_slot<SV>(lw, cur + ex, sl[rr], l);
           } else if (src[rr]) {
             lds_put(lb, cur + ex, src[rr], l);
@@ -609,7 +577,7 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         if (full) {
           if (lane == 0) wb[0] = wb[full];  // the unfinished piece becomes piece 0
           wave_lds_sync();
-          if (!PQ_BA_STORES && !PLAIN) {
+          if (!PQ_BA_STORES) {
             for (uint32_t k = 1 + lane; k <= full; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
             wave_lds_sync();
           }
@@ -673,9 +641,10 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
 }
 
 // class 0: with the slots kept in registers (PQ_BA_PA) 4 waves per SIMD (two 8-wave workgroups per
-// CU, <= 128 VGPRs); without, 6 (three workgroups: <= 80 VGPRs, 46 KB LDS each)
+// CU, <= 128 VGPRs); with the first pieces (PQ_BA_P0) <= 96 VGPRs, which still seats two 8-wave
+// workgroups per CU; with neither, 6 (three workgroups: <= 80 VGPRs, 46 KB LDS each)
 #ifndef PQ_BA_WPE
-#define PQ_BA_WPE (PQ_BA_PA ? 4 : 6)
+#define PQ_BA_WPE (PQ_BA_PA ? 4 : PQ_BA_P0 ? 5 : 6)
 #endif
 __global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(PQ_BA_WPE))) k_ba_emit_slots(BatchDev b_in) {
   const BatchDev b = global_view(b_in);

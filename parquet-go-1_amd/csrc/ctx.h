@@ -14,6 +14,8 @@ struct pqgpu_ctx {
   hipStream_t side = nullptr;  // values kernels run here concurrently with k_levels (speculative mode)
   hipStream_t copy = nullptr;  // PLAIN / BOOLEAN copies (k_values_copy) beside both
   hipStream_t delta = nullptr; // DELTA_BINARY_PACKED pages (k_values_delta) beside all three
+  hipStream_t aux = nullptr;   // repetition-stream level kernels beside the definition streams', then
+                               // the nested arrays (k_nest_tile) beside the values path
   // Device scratch of the page index builds, kept between calls (hipMalloc'd: kernel stores into
   // stream-ordered hipMallocAsync memory from workgroups off the first XCD were observed never to
   // reach a later device-to-host copy of it)

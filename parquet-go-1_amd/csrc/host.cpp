@@ -386,7 +386,7 @@ static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values_dict", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
-    "k_values_copy", "k_group_flat", "k_nest_tile"};
+    "k_values_copy", "k_group_flat", "k_nest_tile", "k_nest_pcount"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -483,6 +483,7 @@ struct pqgpu_batch {
   uint64_t dblk_total = 0;
   uint32_t n_delta_tiles = 0;
   std::vector<uint32_t> level_pages, scan_pages, base_chunks, ba_chunks, rec_pages, nest_chunks;
+  std::vector<uint32_t> pc_pages;  // pages of the nested chunks (k_nest_pcount)
   std::vector<uint4> nest_tiles;  // nested fill tiles: {global fill tile, page, tile of the page, chunk}
   std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
   uint64_t l_grp_tiles = 0;
@@ -516,7 +517,14 @@ struct pqgpu_batch {
   // The byte-array dictionaries' slot tables built by the run scan's launch (k_scan_slots) instead
   // of their own launch in front of k_ba_emit; PQ_SCAN_SLOTS=0: k_dict_slots
   bool scan_slots = !getenv("PQ_SCAN_SLOTS") || atoi(getenv("PQ_SCAN_SLOTS")) != 0;
-  bool nest_fused = getenv("PQ_NEST_FUSED") && atoi(getenv("PQ_NEST_FUSED")) != 0;  // (on once measured)
+  // Nested batches: the repetition streams' level kernels on the aux stream beside the definition
+  // streams' (PQ_LV_SPLIT=0: one after the other), and the nested pages' counts by k_nest_pcount so
+  // that k_bases and the values path go ahead while k_nest_tile runs on the aux stream
+  // (PQ_NEST_PCOUNT=0: k_nest_tile counts them, and k_bases waits for it)
+  bool level_split = !getenv("PQ_LV_SPLIT") || atoi(getenv("PQ_LV_SPLIT")) != 0;
+  bool nest_pcount = !getenv("PQ_NEST_PCOUNT") || atoi(getenv("PQ_NEST_PCOUNT")) != 0;
+  // (cfg4: 1.59 -> 1.47 ms, profiles/r05_s29_probe_cfg4_fused.txt)
+  bool nest_fused = !getenv("PQ_NEST_FUSED") || atoi(getenv("PQ_NEST_FUSED")) != 0;
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
   // k_values_delta) or as their own zero-LDS launch on the copy stream: fused in the speculative
   // schedule (cfg2: 0.51-0.53 ms fused against 0.56-0.58 split), split in the serial one.
@@ -530,6 +538,7 @@ struct pqgpu_batch {
   int copy_mode = getenv("PQ_COPY_MODE") ? atoi(getenv("PQ_COPY_MODE")) : 0;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_copy = nullptr, ev_copy_join = nullptr, ev_delta_join = nullptr;
   hipEvent_t ev_levels = nullptr, ev_nest_join = nullptr;
+  hipEvent_t ev_lv_fork = nullptr, ev_lv_join = nullptr, ev_aux_fork = nullptr, ev_aux_join = nullptr;
   // Column-group pipeline (speculative batches of flat REQUIRED columns with device SNAPPY pages):
   // the chunks are cut into n_groups contiguous groups; group g's SNAPPY launch is followed on the
   // values streams by its run scan, dictionary tiles and DELTA pages while group g+1 decompresses.
@@ -570,7 +579,7 @@ struct pqgpu_batch {
            o_ba_tile_sum = 0, o_ba_tile_page = 0, o_ba_tile_order = 0, o_ba_totals = 0, l_slot = 0,
            o_ba_state = 0, o_nest_state = 0;
   uint64_t l_level_bw1 = 0;
-  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0;
+  uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0, l_pc = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
   uint32_t n_delta_items = 0;
   uint64_t o_dbg = 0;
@@ -1159,6 +1168,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->base_chunks.clear();
   b->ba_chunks.clear();
   b->rec_pages.clear();
+  b->pc_pages.clear();
   b->nest_tiles.clear();
   b->nest_chunks.clear();
   b->grp_tiles.clear();
@@ -1325,6 +1335,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         b->page_nn_init[p] = pd.num_slots;
       }
       if (hc.col.max_rep > 0 && !hc.nest) b->rec_pages.push_back(p);  // nested chunks: k_nest_emit
+      if (hc.nest && pd.num_slots) b->pc_pages.push_back(p);
       const uint32_t ns_p = pd.num_slots;
       auto tiles = [&](uint8_t kind, uint32_t tile) {
         for (uint32_t v0 = 0; v0 < ns_p; v0 += tile) b->items.push_back(WorkItem{p, v0, std::min(v0 + tile, ns_p), kind, {0, 0, 0}});
@@ -1691,6 +1702,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_base = take(b->base_chunks.size() * 4);
   b->l_ba = take(b->ba_chunks.size() * 4);
   b->l_rec = take(b->rec_pages.size() * 4);
+  b->l_pc = take(b->pc_pages.size() * 4);
   b->l_nest_tiles = take(b->nest_tiles.size() * 16);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
@@ -1889,6 +1901,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_base, b->base_chunks.data(), b->base_chunks.size() * 4), err);
   HIPCHECK(up(b->l_ba, b->ba_chunks.data(), b->ba_chunks.size() * 4), err);
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
+  HIPCHECK(up(b->l_pc, b->pc_pages.data(), b->pc_pages.size() * 4), err);
   HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 16), err);
   HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
   HIPCHECK(up(b->l_grp_tiles, b->grp_tiles.data(), b->grp_tiles.size() * 4), err);
@@ -2002,6 +2015,8 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.slot_grid_x = b->slot_grid_x;
   l.rec_pages = (const uint32_t *)(A + b->l_rec);
   l.n_rec_pages = (uint32_t)b->rec_pages.size();
+  l.pc_pages = (const uint32_t *)(A + b->l_pc);
+  l.n_pc_pages = (uint32_t)b->pc_pages.size();
   l.nest_desc = (const uint4 *)(A + b->l_nest_tiles);
   l.n_nest_tiles = (uint32_t)b->nest_tiles.size();
   for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
@@ -2116,9 +2131,39 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (!b->ev_levels) HIPCHECK(hipEventCreateWithFlags(&b->ev_levels, hipEventDisableTiming), err);
   if (!b->ev_nest_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_nest_join, hipEventDisableTiming), err);
   // nested tiles on stream st: the fused pass (k_nest_tile), or k_nest_count (k_nest_emit in fork_nest)
+  const bool pc_sched = b->nest_fused && b->nest_pcount && l.n_pc_pages && l.n_nest_tiles && !b->one_stream;
+  bool aux_out = false;  // k_nest_tile on the aux stream, not yet joined
   auto launch_nest_pass = [&](hipStream_t st) -> hipError_t {
-    if (b->nest_fused) return timed(b, 22, st, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, st); });
+    if (pc_sched) {  // counts first (k_bases waits for them only), the arrays beside the rest
+      hipError_t e = timed(b, 23, st, l.n_pc_pages, [&] { return launch_nest_pcount(d, l, st); });
+      if (e == hipSuccess && !b->ev_aux_fork) e = hipEventCreateWithFlags(&b->ev_aux_fork, hipEventDisableTiming);
+      if (e == hipSuccess && !b->ev_aux_join) e = hipEventCreateWithFlags(&b->ev_aux_join, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(b->ev_aux_fork, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(b->ctx->aux, b->ev_aux_fork, 0);
+      if (e == hipSuccess)
+        e = timed(b, 22, b->ctx->aux, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, b->ctx->aux, true); });
+      if (e == hipSuccess) e = hipEventRecord(b->ev_aux_join, b->ctx->aux);
+      aux_out = e == hipSuccess;
+      return e;
+    }
+    if (b->nest_fused) return timed(b, 22, st, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, st, false); });
     return timed(b, 13, st, l.n_nest_tiles, [&] { return launch_nest_count(d, l, st); });
+  };
+  // the level kernels on st; with a split, the generic streams past k_levels_segw's on the aux stream
+  const bool lv_split = b->level_split && !b->one_stream && l.n_level_units_seg && l.n_level_pages > l.n_level_units_seg;
+  auto levels = [&](hipStream_t st) -> hipError_t {
+    if (!lv_split) return timed(b, 0, st, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, st); });
+    hipError_t e = hipSuccess;
+    if (!b->ev_lv_fork) e = hipEventCreateWithFlags(&b->ev_lv_fork, hipEventDisableTiming);
+    if (e == hipSuccess && !b->ev_lv_join) e = hipEventCreateWithFlags(&b->ev_lv_join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(b->ev_lv_fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b->ctx->aux, b->ev_lv_fork, 0);
+    // (the timer slot brackets the launches on st: with the split it times k_levels_segw's part)
+    if (e == hipSuccess)
+      e = timed(b, 0, st, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, st, b->ctx->aux); });
+    if (e == hipSuccess) e = hipEventRecord(b->ev_lv_join, b->ctx->aux);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, b->ev_lv_join, 0);
+    return e;
   };
   auto fork_nest = [&]() -> hipError_t {
     if (!any_nest) return hipSuccess;
@@ -2202,10 +2247,10 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     // 5: the copies beside the values path, the level kernels after it (profiling)
     const bool lv_then_val = b->copy_mode == 4, val_then_lv = b->copy_mode == 5;
     if (lv_then_val || val_then_lv) HIPCHECK(fork_copies(s), err);
-    if (lv_then_val) HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    if (lv_then_val) HIPCHECK(levels(s), err);
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
-      HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+      HIPCHECK(levels(s), err);
     if (v != s) HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
     HIPCHECK(fork_delta(b->ev_fork), err);
     HIPCHECK(scan_runs(v), err);
@@ -2219,8 +2264,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 18, v, l.n_ba_delta, [&] { return launch_ba_delta(d, l, v); }), err);
     if (v != s) HIPCHECK(hipEventRecord(b->ev_join, v), err);
     if (val_then_lv && v != s) HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
-    if (!b->levels_first && !lv_then_val)
-      HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    if (!b->levels_first && !lv_then_val) HIPCHECK(levels(s), err);
     HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(launch_nest_pass(s), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
@@ -2236,7 +2280,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     if (any_delta) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
-    HIPCHECK(timed(b, 0, s, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, s); }), err);
+    HIPCHECK(levels(s), err);
     HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(launch_nest_pass(s), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
@@ -2309,6 +2353,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // nested (Arrow-style) arrays of repeated leaves (nested.hip)
   // (k_nest_count counted the fill tiles' halves beside k_level_fill; k_nest_emit writes the levels)
   if (any_nest) HIPCHECK(hipStreamWaitEvent(s, b->ev_nest_join, 0), err);  // nested arrays (fork_nest)
+  if (aux_out) HIPCHECK(hipStreamWaitEvent(s, b->ev_aux_join, 0), err);     // k_nest_tile (pc_sched)
   b->decoded = true;
   return PQ_OK;
 }
@@ -2560,11 +2605,22 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->delta, hipStreamNonBlocking);
+  // PQ_DELTA_STREAM_PRIO=1 (probe): the DELTA stream (cfg2: the level kernels beside the values
+  // launch) at the device's highest stream priority, so its workgroups are dispatched first
+  const char *dsp = getenv("PQ_DELTA_STREAM_PRIO");
+  if (e == hipSuccess && dsp && atoi(dsp) != 0) {
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->delta, hipStreamNonBlocking, hi);
+  } else if (e == hipSuccess) {
+    e = hipStreamCreateWithFlags(&c->delta, hipStreamNonBlocking);
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->delta) (void)hipStreamDestroy(c->delta);
     delete c;
     set_err(err, PQ_ERR_HIP, -1, -1, hipGetErrorString(e));
     return PQ_ERR_HIP;
@@ -2580,6 +2636,7 @@ void pqgpu_ctx_destroy(pqgpu_ctx *c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   if (c->delta) (void)hipStreamDestroy(c->delta);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   c->scratch_release();
   delete c;
 }
@@ -2699,6 +2756,8 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   for (auto &e : b->ev_snap)
     if (e) (void)hipEventDestroy(e);
   if (b->ev_nest_join) (void)hipEventDestroy(b->ev_nest_join);
+  for (hipEvent_t ev : {b->ev_lv_fork, b->ev_lv_join, b->ev_aux_fork, b->ev_aux_join})
+    if (ev) (void)hipEventDestroy(ev);
   if (b->d_arena) (void)hipFree(b->d_arena);
   if (b->d_payload) (void)hipFree(b->d_payload);
   if (b->d_stage) (void)hipFree(b->d_stage);

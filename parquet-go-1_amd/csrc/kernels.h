@@ -90,6 +90,7 @@ struct LaunchLists {
   const uint32_t *slot_chunks; uint32_t n_slot_chunks;   // chunks whose dictionary gets a slot table
   uint32_t slot_grid_x;
   const uint32_t *rec_pages; uint32_t n_rec_pages;       // pages of chunks with max_rep > 0
+  const uint32_t *pc_pages; uint32_t n_pc_pages;         // pages of the nested chunks (k_nest_pcount)
   const uint4 *nest_desc; uint32_t n_nest_tiles;         // fill tiles of the nested chunks (k_nest_count / k_nest_emit):
                                                          // {global fill tile, page, tile of the page, chunk}
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
@@ -99,7 +100,8 @@ struct LaunchLists {
   uint32_t n_delta_tiles;                                // the first n_delta_tiles items are WI_DELTA_TILE
 };
 
-hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+// s2 (when given): the generic streams past k_levels_segw's (k_levels_hyb, k_levels) go there
+hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s, hipStream_t s2 = nullptr);
 hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // generic level run tables
 constexpr uint32_t kLfTileHost = 8192;  // k_level_fill tile (kernels.hip kLfTile)
 constexpr uint32_t kSgStageHost = 10240;  // k_levels_seg's LDS stage (kernels.hip kSgStage)
@@ -123,7 +125,9 @@ hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // the two passes in one (count, look-back over the chunk's earlier tiles, emit): k_nest_tile
-hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s);
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted);
+// the nested pages' record and non-null counts from the level run tables (k_nest_pcount)
+hipError_t launch_nest_pcount(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 constexpr uint32_t kGrpTileHost = 8192;  // nested.hip kGrpTile: slots per k_group_flat workgroup
 hipError_t launch_group_flat(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // *flag |= 1 when the n words at a and b differ (pqgpu_batch_share_ancestors)

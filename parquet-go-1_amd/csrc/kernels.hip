@@ -1537,9 +1537,13 @@ DEV uint32_t sg_run_wave(uint32_t *vb, const uint32_t *stage, uint32_t sa, uint6
   return ones;
 }
 
+#ifndef PQ_SEG_PRIO
+#define PQ_SEG_PRIO 0  // k_levels_seg's wave priority (probe: beside the values launch)
+#endif
 __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages) {
   const BatchDev b = global_view(b_in);
   __shared__ LevelSegLDS L;
+  if (PQ_SEG_PRIO) __builtin_amdgcn_s_setprio(PQ_SEG_PRIO);
   const uint32_t pi = pages[blockIdx.x], lane = lane_id();
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
@@ -4613,7 +4617,8 @@ hipError_t launch_snappy(const BatchDev &b, const SnappyJob *jobs, uint32_t njob
   hipLaunchKernelGGL(k_snappy, dim3(njobs), dim3(64 * kSnappyWaves), 0, s, b, jobs);
   return hipGetLastError();
 }
-hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s, hipStream_t s2) {
+  if (!s2) s2 = s;
   if (l.n_level_pages_bw1) {
     // default: verified segment speculation (k_levels_seg); PQ_LV_SEG=0: the list-ranking workgroup
     // kernel; PQ_LV_WAVE=1: the lane-to-lane wave walk (both slower: DESIGN.md §5)
@@ -4634,8 +4639,8 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s)
               // then the list-ranking kernel
       const uint32_t nseg = l.n_level_units_seg, nhyb = l.n_level_units_hyb, nrest = l.n_level_pages - nseg - nhyb;
       if (nseg) hipLaunchKernelGGL(k_levels_segw, dim3(nseg), dim3(kSgwLanes), 0, s, b, l.level_pages);
-      if (nhyb) hipLaunchKernelGGL(k_levels_hyb, dim3(nhyb), dim3(256), 0, s, b, l.level_pages + nseg);
-      if (nrest) hipLaunchKernelGGL(k_levels, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages + nseg + nhyb);
+      if (nhyb) hipLaunchKernelGGL(k_levels_hyb, dim3(nhyb), dim3(256), 0, s2, b, l.level_pages + nseg);
+      if (nrest) hipLaunchKernelGGL(k_levels, dim3(nrest), dim3(kLvThreads), 0, s2, b, l.level_pages + nseg + nhyb);
     }
   }
   return hipGetLastError();

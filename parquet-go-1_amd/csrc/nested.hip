@@ -142,7 +142,8 @@ struct NestStage {
 // (bytes), eqd[q] the groups' definition == max_def masks; the u8 level arrays the chunk has are
 // written and the pages' counts (records, non-null values) added once per tile.
 DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, const NestFill &x, NestStage &T,
-                     uint32_t tid, uint64_t (&lw)[2][4], uint32_t (&eqd)[4], uint32_t &end_d, Stamps &st) {
+                     uint32_t tid, uint64_t (&lw)[2][4], uint32_t (&eqd)[4], uint32_t &end_d, Stamps &st,
+                     bool count_pages = true) {
   const uint32_t lane = lane_id(), wv = tid >> 6;
   LfStream S[2];
   S[0] = lf_stream(b, pd, cd, x, 0, T.run[0], tid);
@@ -228,7 +229,7 @@ DEV void nest_expand(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd,
     if (lane == 0) T.cnt[w][wv] = wc;
   }
   wg_barrier();  // cnt complete
-  if (tid < 2 && (tid ? S[1].on : S[0].on)) {
+  if (count_pages && tid < 2 && (tid ? S[1].on : S[0].on)) {
     const uint32_t c = T.cnt[tid][0] + T.cnt[tid][1] + T.cnt[tid][2] + T.cnt[tid][3];
     if (c) atomicAdd(tid ? &b.page_nn[x.pi] : &b.page_rec[x.pi], c);
   }
@@ -282,6 +283,59 @@ __global__ void __launch_bounds__(256) k_nest_scan(BatchDev b_in, const uint32_t
   const BatchDev b = global_view(b_in);
   __shared__ uint64_t wsum[4];
   nest_scan_chunk(b, chunks[blockIdx.x], wsum);
+}
+
+// The nested pages' counts from the level run tables alone: records (repetition level 0) and
+// non-null values (definition level max_def) among the slots each stream covers — the counts
+// k_nest_count / k_nest_tile otherwise add while expanding, so that k_bases (value and record bases:
+// ColumnStore.readNextPage's per-page split) does not wait for the nested arrays. One workgroup per
+// page: threads 0-127 the repetition stream, 128-255 the definition stream, a run per thread and
+// step; RLE runs count whole, bit-packed runs 64 bits at a time (fields equal to the level by SWAR).
+__global__ void __launch_bounds__(256) k_nest_pcount(BatchDev b_in, const uint32_t *pages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ uint32_t part[4];
+  const uint32_t pi = gp(pages)[blockIdx.x], tid = threadIdx.x, w = tid >> 7, t = tid & 127;
+  const PageDesc &pd = b.pages[pi];
+  const ChunkDesc &cd = b.chunks[pd.chunk];
+  const uint32_t nr = b.lv_meta[4 * pi + 2 * w], cov = b.lv_meta[4 * pi + 2 * w + 1];
+  const uint32_t end = min(cov, pd.num_slots);
+  const uint32_t bw = w ? (uint32_t)cd.def_bw : (uint32_t)cd.rep_bw, cmp = w ? (uint32_t)cd.max_def : 0u;
+  const bool on = (w ? cd.max_def : cd.max_rep) != 0;
+  uint32_t c = 0;
+  if (on && nr && end && bw) {
+    const uint2 *runs = b.lv_runs + b.lv_run_base[2 * pi + w];
+    const uint8_t *src = gp_u64<const uint8_t>(pd.data) + (w ? pd.def_off : pd.rep_off);
+    const uint32_t n = w ? pd.def_len : pd.rep_len;
+    const uint32_t k = 56 / bw;  // fields per 64-bit read (bw <= 8: k >= 7)
+    uint64_t lo = 0, rc = 0;     // the field pattern: bit 0 of every field; the level in every field
+    for (uint32_t i = 0; i < k; i++) { lo |= 1ull << (i * bw); }
+    rc = lo * cmp;
+    for (uint32_t r = t; r < nr; r += 128) {
+      const uint2 run = runs[r];
+      const uint32_t x0 = run.x, x1 = min(r + 1 < nr ? runs[r + 1].x : end, end);
+      if (x0 >= x1) continue;
+      if (!(run.y >> 31)) {  // RLE
+        c += run.y == cmp ? x1 - x0 : 0u;
+        continue;
+      }
+      const uint64_t pb = (uint64_t)(run.y & 0x7fffffffu) * 8;
+      for (uint32_t v = x0; v < x1; v += k) {
+        const uint32_t m = min(k, x1 - v);
+        const uint64_t y = bits64c(src, n, pb + (uint64_t)(v - x0) * bw, m * bw) ^ (rc & ((m * bw >= 64) ? ~0ull : ((1ull << (m * bw)) - 1ull)));
+        uint64_t z = y;  // a field is zero (equal to the level) iff no bit of it is set
+        for (uint32_t q = 1; q < bw; q++) z |= y >> q;
+        const uint64_t fm = lo & ((m * bw >= 64) ? ~0ull : ((1ull << (m * bw)) - 1ull));
+        c += (uint32_t)__popcll(~z & fm);
+      }
+    }
+  }
+  c = (uint32_t)wave_sum64(c);
+  if (lane_id() == 0) part[tid >> 6] = c;
+  wg_barrier();
+  if (tid == 0) {
+    if (cd.max_rep) b.page_rec[pi] = part[0] + part[1];
+    b.page_nn[pi] = part[2] + part[3];
+  }
 }
 
 // The slots' flag masks, 32 bits per thread (bits 8q..8q+7: group q; 0-15 the first half's sixteen
@@ -733,7 +787,8 @@ template <uint32_t R>
 #ifndef PQ_NEST_TILE_WPE1
 #define PQ_NEST_TILE_WPE1 5
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
+                                                                                                                                     uint32_t counted) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestTileLDS<R> L;
@@ -746,7 +801,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   st.begin();
   uint64_t lw[2][4];
   uint32_t eqd[4], end_d = 0;
-  nest_expand(b, pd, cd, x, L.u.a.st, tid, lw, eqd, end_d, st);
+  nest_expand(b, pd, cd, x, L.u.a.st, tid, lw, eqd, end_d, st, !counted);  // (counted: k_nest_pcount's)
   uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
   const bool vtile = vbits && x.lo < end_d;  // workgroup-uniform
   if (vtile) {
@@ -937,22 +992,28 @@ static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s
   if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
 }
 template <uint32_t R>
-static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
+  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], counted);
 }
-hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted) {
   if (!l.n_nest_tiles) return hipSuccess;
   // tiles are grouped by list levels (host.cpp): one instantiation per group; a chunk's tiles are
   // contiguous and in slot order within one launch (the look-back's predecessors)
-  launch_tile_r<1>(b, l, s);
-  launch_tile_r<2>(b, l, s);
-  launch_tile_r<3>(b, l, s);
-  launch_tile_r<4>(b, l, s);
-  launch_tile_r<5>(b, l, s);
-  launch_tile_r<6>(b, l, s);
-  launch_tile_r<7>(b, l, s);
-  launch_tile_r<8>(b, l, s);
+  const uint32_t c = counted ? 1u : 0u;
+  launch_tile_r<1>(b, l, s, c);
+  launch_tile_r<2>(b, l, s, c);
+  launch_tile_r<3>(b, l, s, c);
+  launch_tile_r<4>(b, l, s, c);
+  launch_tile_r<5>(b, l, s, c);
+  launch_tile_r<6>(b, l, s, c);
+  launch_tile_r<7>(b, l, s, c);
+  launch_tile_r<8>(b, l, s, c);
+  return hipGetLastError();
+}
+hipError_t launch_nest_pcount(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  if (!l.n_pc_pages) return hipSuccess;
+  hipLaunchKernelGGL(k_nest_pcount, dim3(l.n_pc_pages), dim3(256), 0, s, b, l.pc_pages);
   return hipGetLastError();
 }
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

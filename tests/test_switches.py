@@ -20,6 +20,8 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_LV_HYB=0        repetition streams by k_levels' list ranking instead of k_levels_hyb
 - PQ_NEST_FUSED=0/1  nested arrays by k_nest_count + k_nest_emit, or by k_nest_tile
 - PQ_SCAN_SLOTS=0    byte-array slot tables by their own k_dict_slots launch instead of k_scan_slots
+- PQ_LV_SPLIT=0      nested batches' repetition-stream level kernels on the batch stream, not beside
+- PQ_NEST_PCOUNT=0   k_nest_tile counts the nested pages (k_bases waits for it) instead of k_nest_pcount
 """
 import pytest
 
@@ -53,6 +55,8 @@ SWITCHES = {
     "nest_two_pass": {"PQ_NEST_FUSED": "0"},
     "nest_fused": {"PQ_NEST_FUSED": "1"},
     "slots_own_launch": {"PQ_SCAN_SLOTS": "0"},
+    "lv_no_split": {"PQ_LV_SPLIT": "0"},
+    "nest_no_pcount": {"PQ_NEST_PCOUNT": "0"},
 }
 
 
