@@ -518,11 +518,12 @@ struct pqgpu_batch {
   // of their own launch in front of k_ba_emit; PQ_SCAN_SLOTS=0: k_dict_slots
   bool scan_slots = !getenv("PQ_SCAN_SLOTS") || atoi(getenv("PQ_SCAN_SLOTS")) != 0;
   // Nested batches: the repetition streams' level kernels on the aux stream beside the definition
-  // streams' (PQ_LV_SPLIT=0: one after the other), and the nested pages' counts by k_nest_pcount so
-  // that k_bases and the values path go ahead while k_nest_tile runs on the aux stream
-  // (PQ_NEST_PCOUNT=0: k_nest_tile counts them, and k_bases waits for it)
+  // streams' (PQ_LV_SPLIT=0: one after the other; cfg4 1.47 -> 1.41 ms). PQ_NEST_PCOUNT=1: the nested
+  // pages' counts by k_nest_pcount, so that k_bases and the values path go ahead while k_nest_tile
+  // runs on the aux stream -- slower (cfg4 1.41 -> 1.64 ms: the byte-array path beside k_nest_tile
+  // 0.38 -> 1.1 ms, profiles/r05_s30_probe_cfg4_sched.txt), so k_nest_tile counts them by default.
   bool level_split = !getenv("PQ_LV_SPLIT") || atoi(getenv("PQ_LV_SPLIT")) != 0;
-  bool nest_pcount = !getenv("PQ_NEST_PCOUNT") || atoi(getenv("PQ_NEST_PCOUNT")) != 0;
+  bool nest_pcount = getenv("PQ_NEST_PCOUNT") && atoi(getenv("PQ_NEST_PCOUNT")) != 0;
   // (cfg4: 1.59 -> 1.47 ms, profiles/r05_s29_probe_cfg4_fused.txt)
   bool nest_fused = !getenv("PQ_NEST_FUSED") || atoi(getenv("PQ_NEST_FUSED")) != 0;
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
@@ -581,6 +582,14 @@ struct pqgpu_batch {
   uint64_t l_level_bw1 = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0, l_pc = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
+  // Chunk error keys, two buffers (o_err, o_err2) at the two ends of the 0xff region. A decode in the
+  // DELTA-major schedule takes the buffer reset during the decode before it and resets the other one
+  // (with the rest of the per-decode state) on the level stream, beside its values launch: no reset
+  // in front of the critical path. err_sel: the buffer the last decode reported into (sync reads it);
+  // err_ready[k]: buffer k's reset is enqueued and it has not been used since.
+  uint64_t o_err2 = 0;
+  uint32_t err_sel = 0;
+  bool err_ready[2] = {false, false};
   uint32_t n_delta_items = 0;
   uint64_t o_dbg = 0;
   bool debug_stamps = getenv("PQ_DEBUG_STAMPS") && atoi(getenv("PQ_DEBUG_STAMPS")) != 0;
@@ -1451,7 +1460,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     for (uint32_t c : b->ba_chunks) {
       HostChunk &hc = b->chunks[c];
       hc.ba_class = cls[c];
-      const int mode = b->ba_presum_mode >= 0 ? b->ba_presum_mode : (!b->one_stream && !b->nest_chunks.empty()) ? 1 : 0;
+      // default: the pre-pass when nested arrays are emitted beside the byte-array path (k_nest_emit on
+      // the DELTA stream, or k_nest_tile on the aux stream with k_nest_pcount), else the look-back
+      const bool nest_beside = !b->one_stream && !b->nest_chunks.empty() && (!b->nest_fused || b->nest_pcount);
+      const int mode = b->ba_presum_mode >= 0 ? b->ba_presum_mode : nest_beside ? 1 : 0;
       hc.ba_presum = !hc.ba_sync && (mode == 1 || (mode == 2 && cls[c] == 3));
       b->ba_presum |= hc.ba_presum;
     }
@@ -1530,7 +1542,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->f_begin = b->o_err;
   b->o_tile_first = take(b->tile_total * 4);
   b->o_tile_desc = take(b->tile_total * 32);  // (filled too: a descriptor k_scan_runs did not write reads invalid)
+  b->o_err2 = take((uint64_t)nc * 8);
   b->f_end = a;
+  b->err_sel = 0;
+  b->err_ready[0] = b->err_ready[1] = false;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
   // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
@@ -2072,7 +2087,22 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                            b->copy_mode == 0 && !b->levels_first && !l.n_scan_pages && !b->n_dict_items &&
                            l.n_items == b->n_delta_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
                            b->ba_chunks.empty() && !l.n_rec_pages && !side;
-  HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
+  // the error keys of this decode (see err_sel): the DELTA-major schedule resets the state on its
+  // level stream (below) and reports into the buffer its predecessor reset; the others reset all on s
+  uint32_t eu = 0;
+  if (delta_major) {
+    eu = b->err_sel ^ 1u;
+    if (!b->err_ready[eu]) {  // (the first such decode): this buffer alone, in front
+      const uint64_t o = eu ? b->o_err2 : b->o_err;
+      HIPCHECK(launch_reset(nullptr, 0, A + o, align_up((uint64_t)nc * 8, 16), s), err);
+    }
+    d.chunk_err = (unsigned long long *)(A + (eu ? b->o_err2 : b->o_err));
+  } else {
+    HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
+    b->err_ready[1] = true;  // (o_err2 is inside the region)
+  }
+  b->err_sel = eu;
+  b->err_ready[eu] = false;
   // SNAPPY pages first: every later kernel reads page data (column-group pipeline: one launch per
   // group, each followed by an event the group's values work waits for)
   const uint32_t G = b->n_groups;
@@ -2227,6 +2257,12 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     HIPCHECK(hipStreamWaitEvent(ds, b->ev_fork, 0), err);
+    {  // the per-decode state, and the other key buffer for the next decode, on the level stream:
+       // [o_err, o_tile_desc end) or [o_tile_first, o_err2 end) -- never the buffer in use
+      const uint64_t f0 = eu ? b->o_err : b->o_tile_first, f1 = eu ? b->o_err2 : b->f_end;
+      HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + f0, f1 - f0, ds), err);
+      b->err_ready[eu ^ 1u] = true;
+    }
     HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, ds); }), err);
     HIPCHECK(timed(b, 15, ds, l.n_lf_list, [&] { return launch_level_fill(d, l, ds); }), err);
     HIPCHECK(timed(b, 3, ds, l.n_base_chunks, [&] { return launch_bases(d, l, ds); }), err);
@@ -2398,7 +2434,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   std::vector<uint64_t> keys(nc), vbase(np), rbase(np);
   std::vector<uint32_t> nn(np), rec(np);
   uint8_t *A = b->d_arena;
-  if (nc) HIPCHECK(hipMemcpy(keys.data(), A + b->o_err, nc * 8, hipMemcpyDeviceToHost), err);
+  if (nc) HIPCHECK(hipMemcpy(keys.data(), A + (b->err_sel ? b->o_err2 : b->o_err), nc * 8, hipMemcpyDeviceToHost), err);
   if (np) {
     HIPCHECK(hipMemcpy(vbase.data(), A + b->o_vbase, np * 8, hipMemcpyDeviceToHost), err);
     HIPCHECK(hipMemcpy(nn.data(), A + b->o_nn, np * 4, hipMemcpyDeviceToHost), err);
@@ -2605,16 +2641,7 @@ int pqgpu_ctx_create(int device, pqgpu_ctx **out, pqgpu_error *err) {
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-  // PQ_DELTA_STREAM_PRIO=1 (probe): the DELTA stream (cfg2: the level kernels beside the values
-  // launch) at the device's highest stream priority, so its workgroups are dispatched first
-  const char *dsp = getenv("PQ_DELTA_STREAM_PRIO");
-  if (e == hipSuccess && dsp && atoi(dsp) != 0) {
-    int lo = 0, hi = 0;
-    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->delta, hipStreamNonBlocking, hi);
-  } else if (e == hipSuccess) {
-    e = hipStreamCreateWithFlags(&c->delta, hipStreamNonBlocking);
-  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->delta, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);

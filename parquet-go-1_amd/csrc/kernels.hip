@@ -1537,13 +1537,9 @@ DEV uint32_t sg_run_wave(uint32_t *vb, const uint32_t *stage, uint32_t sa, uint6
   return ones;
 }
 
-#ifndef PQ_SEG_PRIO
-#define PQ_SEG_PRIO 0  // k_levels_seg's wave priority (probe: beside the values launch)
-#endif
 __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages) {
   const BatchDev b = global_view(b_in);
   __shared__ LevelSegLDS L;
-  if (PQ_SEG_PRIO) __builtin_amdgcn_s_setprio(PQ_SEG_PRIO);
   const uint32_t pi = pages[blockIdx.x], lane = lane_id();
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];

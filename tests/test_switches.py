@@ -21,7 +21,7 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_NEST_FUSED=0/1  nested arrays by k_nest_count + k_nest_emit, or by k_nest_tile
 - PQ_SCAN_SLOTS=0    byte-array slot tables by their own k_dict_slots launch instead of k_scan_slots
 - PQ_LV_SPLIT=0      nested batches' repetition-stream level kernels on the batch stream, not beside
-- PQ_NEST_PCOUNT=0   k_nest_tile counts the nested pages (k_bases waits for it) instead of k_nest_pcount
+- PQ_NEST_PCOUNT=1   the nested pages' counts by k_nest_pcount, k_nest_tile beside the values path
 """
 import pytest
 
@@ -56,7 +56,7 @@ SWITCHES = {
     "nest_fused": {"PQ_NEST_FUSED": "1"},
     "slots_own_launch": {"PQ_SCAN_SLOTS": "0"},
     "lv_no_split": {"PQ_LV_SPLIT": "0"},
-    "nest_no_pcount": {"PQ_NEST_PCOUNT": "0"},
+    "nest_pcount": {"PQ_NEST_PCOUNT": "1"},
 }
 
 
