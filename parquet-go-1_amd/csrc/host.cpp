@@ -582,14 +582,19 @@ struct pqgpu_batch {
   uint64_t l_level_bw1 = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0, l_pc = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
-  // Chunk error keys, two buffers (o_err, o_err2) at the two ends of the 0xff region. A decode in the
-  // DELTA-major schedule takes the buffer reset during the decode before it and resets the other one
-  // (with the rest of the per-decode state) on the level stream, beside its values launch: no reset
-  // in front of the critical path. err_sel: the buffer the last decode reported into (sync reads it);
-  // err_ready[k]: buffer k's reset is enqueued and it has not been used since.
-  uint64_t o_err2 = 0;
+  // Chunk error keys. DELTA-major decodes (cfg2) run their two streams without a join per decode:
+  // the values launch on the batch stream reports into o_err / o_err2 (alternately: the launch resets
+  // the next decode's buffer itself, err_next), the level stream into o_err_ds (reset with the rest of
+  // the per-decode state on that stream). So consecutive decodes put nothing but the values launches
+  // on the batch stream -- no reset, no cross-stream wait in front of the critical path; the level
+  // stream is joined when anything else needs the batch (join_deferred). sync takes the smaller key
+  // of the batch stream's buffer and the level stream's. err_sel: the batch-stream buffer the last
+  // decode reported into; err_ready[k]: buffer k's reset is enqueued and it has not been used since.
+  uint64_t o_err2 = 0, o_err_ds = 0;
   uint32_t err_sel = 0;
   bool err_ready[2] = {false, false};
+  bool ds_pending = false;  // the level stream's work of a DELTA-major decode is not joined yet
+  bool ds_synced = false;   // the level stream has waited for the batch stream since the last upload
   uint32_t n_delta_items = 0;
   uint64_t o_dbg = 0;
   bool debug_stamps = getenv("PQ_DEBUG_STAMPS") && atoi(getenv("PQ_DEBUG_STAMPS")) != 0;
@@ -1161,7 +1166,9 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
 // ---------------------------------------------------------------------------
 // Upload: arena layout, descriptors, work lists
 // ---------------------------------------------------------------------------
+static hipError_t join_deferred(pqgpu_batch *b, hipStream_t s);
 static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
+  if (b->ctx) HIPCHECK(join_deferred(b, s), err);  // (the level stream may still read the stage)
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
   b->items.clear();
   b->level_pages.clear();
@@ -1537,13 +1544,16 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     b->base_chunks.clear();
   }
-  // Region set to 0xff before every decode: chunk error keys, dictionary tile table and descriptors.
+  // Region set to 0xff before every decode: chunk error keys (the batch stream's two buffers first,
+  // the level stream's last), dictionary tile table and descriptors.
   b->o_err = take((uint64_t)nc * 8);
   b->f_begin = b->o_err;
+  b->o_err2 = take((uint64_t)nc * 8);
   b->o_tile_first = take(b->tile_total * 4);
   b->o_tile_desc = take(b->tile_total * 32);  // (filled too: a descriptor k_scan_runs did not write reads invalid)
-  b->o_err2 = take((uint64_t)nc * 8);
+  b->o_err_ds = take((uint64_t)nc * 8);
   b->f_end = a;
+  b->ds_synced = false;
   b->err_sel = 0;
   b->err_ready[0] = b->err_ready[1] = false;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
@@ -2064,6 +2074,13 @@ static hipError_t timed(pqgpu_batch *b, int slot, hipStream_t s, uint64_t n, F f
   return e;
 }
 
+// The level stream's work of DELTA-major decodes that no join has covered yet: s waits for it.
+static hipError_t join_deferred(pqgpu_batch *b, hipStream_t s) {
+  if (!b->ds_pending) return hipSuccess;
+  b->ds_pending = false;
+  return hipStreamWaitEvent(s, b->ev_delta_join, 0);
+}
+
 static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (!b->uploaded) {
     int e = build_and_upload(b, s, err);
@@ -2090,6 +2107,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // the error keys of this decode (see err_sel): the DELTA-major schedule resets the state on its
   // level stream (below) and reports into the buffer its predecessor reset; the others reset all on s
   uint32_t eu = 0;
+  // deferred joins only on the context's own stream: a caller's stream must hold the whole decode
+  const bool defer = delta_major && s == b->ctx->stream;
+  BatchDev dl = d;  // the level stream's view in a DELTA-major decode (its own error keys)
   if (delta_major) {
     eu = b->err_sel ^ 1u;
     if (!b->err_ready[eu]) {  // (the first such decode): this buffer alone, in front
@@ -2097,9 +2117,14 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(launch_reset(nullptr, 0, A + o, align_up((uint64_t)nc * 8, 16), s), err);
     }
     d.chunk_err = (unsigned long long *)(A + (eu ? b->o_err2 : b->o_err));
+    d.err_next = (unsigned long long *)(A + (eu ? b->o_err : b->o_err2));  // reset by k_values_delta
+    dl.chunk_err = (unsigned long long *)(A + b->o_err_ds);
+    b->err_ready[eu ^ 1u] = true;
   } else {
+    HIPCHECK(join_deferred(b, s), err);
     HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
     b->err_ready[1] = true;  // (o_err2 is inside the region)
+    b->ds_synced = false;
   }
   b->err_sel = eu;
   b->err_ready[eu] = false;
@@ -2254,22 +2279,24 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     // the level kernels and k_bases go to the DELTA stream beside it. No stream waits on the
     // critical path but the final join of the (long finished) level stream: cfg2 lost ~20 us per
     // step between k_reset and k_values_delta and ~13 us after it to cross-stream waits.
-    if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
-    HIPCHECK(hipEventRecord(b->ev_fork, s), err);
-    HIPCHECK(hipStreamWaitEvent(ds, b->ev_fork, 0), err);
-    {  // the per-decode state, and the other key buffer for the next decode, on the level stream:
-       // [o_err, o_tile_desc end) or [o_tile_first, o_err2 end) -- never the buffer in use
-      const uint64_t f0 = eu ? b->o_err : b->o_tile_first, f1 = eu ? b->o_err2 : b->f_end;
-      HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + f0, f1 - f0, ds), err);
-      b->err_ready[eu ^ 1u] = true;
+    // The level stream reads only uploaded pages and writes only its own state: it waits for the
+    // batch stream once after an upload (or a decode of another schedule), not per decode
+    if (!b->ds_synced || !defer) {
+      if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
+      HIPCHECK(hipEventRecord(b->ev_fork, s), err);
+      HIPCHECK(hipStreamWaitEvent(ds, b->ev_fork, 0), err);
+      b->ds_synced = true;
     }
-    HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(d, l, ds); }), err);
-    HIPCHECK(timed(b, 15, ds, l.n_lf_list, [&] { return launch_level_fill(d, l, ds); }), err);
-    HIPCHECK(timed(b, 3, ds, l.n_base_chunks, [&] { return launch_bases(d, l, ds); }), err);
+    // the per-decode state and the level stream's keys: [o_tile_first, o_err_ds end) of the 0xff region
+    HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->o_tile_first, b->f_end - b->o_tile_first, ds), err);
+    HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(dl, l, ds); }), err);
+    HIPCHECK(timed(b, 15, ds, l.n_lf_list, [&] { return launch_level_fill(dl, l, ds); }), err);
+    HIPCHECK(timed(b, 3, ds, l.n_base_chunks, [&] { return launch_bases(dl, l, ds); }), err);
     HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);
     HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
     HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s); }), err);
-    HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
+    if (defer) b->ds_pending = true;  // joined by the next operation that needs it (join_deferred)
+    else HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else if (b->spec) {
     // Speculative mode: the values path (dictionary pages, run tables, values) runs on the
     // side stream concurrently with the level decode; k_bases then checks the header counts
@@ -2417,6 +2444,7 @@ static void decode_key(uint64_t key, int chunk, pqgpu_error *e) {
 
 static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   clear_err(err);
+  HIPCHECK(join_deferred(b, s), err);
   HIPCHECK(hipStreamSynchronize(s), err);
   if (!b->decoded) return PQ_OK;
   if (b->spec) {
@@ -2434,7 +2462,12 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   std::vector<uint64_t> keys(nc), vbase(np), rbase(np);
   std::vector<uint32_t> nn(np), rec(np);
   uint8_t *A = b->d_arena;
-  if (nc) HIPCHECK(hipMemcpy(keys.data(), A + (b->err_sel ? b->o_err2 : b->o_err), nc * 8, hipMemcpyDeviceToHost), err);
+  if (nc) {
+    HIPCHECK(hipMemcpy(keys.data(), A + (b->err_sel ? b->o_err2 : b->o_err), nc * 8, hipMemcpyDeviceToHost), err);
+    std::vector<uint64_t> kd(nc);  // the level stream's keys (0xff.. unless a DELTA-major decode reported)
+    HIPCHECK(hipMemcpy(kd.data(), A + b->o_err_ds, nc * 8, hipMemcpyDeviceToHost), err);
+    for (uint32_t c = 0; c < nc; c++) keys[c] = std::min(keys[c], kd[c]);
+  }
   if (np) {
     HIPCHECK(hipMemcpy(vbase.data(), A + b->o_vbase, np * 8, hipMemcpyDeviceToHost), err);
     HIPCHECK(hipMemcpy(nn.data(), A + b->o_nn, np * 4, hipMemcpyDeviceToHost), err);
@@ -2773,6 +2806,7 @@ void pqgpu_batch_destroy(pqgpu_batch *b) {
   (void)hipStreamSynchronize(b->ctx->side);
   (void)hipStreamSynchronize(b->ctx->copy);
   (void)hipStreamSynchronize(b->ctx->delta);  // an error return inside decode_impl can leave forked work here
+  (void)hipStreamSynchronize(b->ctx->aux);
   free_payloads(b);
   if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
@@ -2798,9 +2832,11 @@ int pqgpu_batch_reset(pqgpu_batch *b) {
     (void)hipStreamSynchronize(b->ctx->side);  // forked work of a decode that returned early
     (void)hipStreamSynchronize(b->ctx->copy);
     (void)hipStreamSynchronize(b->ctx->delta);
+    (void)hipStreamSynchronize(b->ctx->aux);
     if (b->last_stream) (void)hipStreamSynchronize(b->last_stream);  // an H2D copy may still read the stage
     free_payloads(b);
   }
+  b->ds_pending = false;
   b->chunks.clear();
   b->pages.clear();
   b->ba_delta.clear();
@@ -3366,6 +3402,7 @@ int pqgpu_copy(pqgpu_ctx *ctx, void *dst, const void *src, size_t bytes, pqgpu_e
 int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset) {
   if (!b->ctx || !b->d_arena) return PQ_ERR_ARG;
   (void)hipSetDevice(b->ctx->device);
+  (void)join_deferred(b, b->ctx->stream);
   (void)hipStreamSynchronize(b->ctx->stream);
   if (hipMemcpy(out64, b->d_arena + b->o_dbg, 64 * 8, hipMemcpyDeviceToHost) != hipSuccess) return PQ_ERR_HIP;
   if (reset) (void)hipMemset(b->d_arena + b->o_dbg, 0, 64 * 8);
@@ -3378,6 +3415,7 @@ int pqgpu_batch_stats_get(const pqgpu_batch *b, pqgpu_batch_stats *out) {
 }
 
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable) {
+  if (b->ctx) (void)join_deferred(b, b->ctx->stream);
   if (b->ctx) (void)hipStreamSynchronize(b->ctx->stream);
   b->timer.resolve();
   b->timer.enabled = enable != 0;

@@ -12,6 +12,8 @@ struct BatchDev {
   const PageDesc *pages;
   const ChunkDesc *chunks;
   unsigned long long *chunk_err;  // [nchunks] first-error key (atomicMin), init ~0
+  unsigned long long *err_next;   // DELTA-major decodes: the key buffer of the next decode, which
+                                  // k_values_delta's first workgroup resets (else null)
   uint32_t *page_nn;              // [npages] decoded non-null count (written by k_levels)
   uint32_t *page_nn_v;            // [npages] non-null count the values kernels use: a copy of
                                   // page_nn (serial mode, k_bases) or the page header's count

@@ -3874,6 +3874,8 @@ union DeltaLDS {
 #endif
 DEV void values_delta(BatchDev b_in, const WorkItem *items, DeltaLDS &lds) {
   const BatchDev b = global_view(b_in);
+  if (blockIdx.x == 0 && b.err_next)  // (DELTA-major decodes: the next decode's keys, on this stream)
+    for (uint32_t c = threadIdx.x; c < b.nchunks; c += blockDim.x) gp(b.err_next)[c] = ~0ull;
   const WorkItem wi = items[blockIdx.x];
   const PageDesc &pd = b.pages[wi.page];
   const ChunkDesc &cd = b.chunks[pd.chunk];

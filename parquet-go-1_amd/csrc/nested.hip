@@ -796,8 +796,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
-  // diagnostic build: k_nest_count's stamps 0-3 (expansion), then 0-4 of the emission
+  // diagnostic build (tools/diag_nest.py): slots 24-31 -- 0 run staging, 1 group marks, 2 expansion,
+  // 3 page counts, 4 flag masks and counts, 5 look-back (wave 0) and its barrier, 6 slot validity;
+  // slots 32-39, the emission as k_nest_emit's
   PQ_STAMPS(st, b.dbg);
+  PQ_STAMPS(se, b.dbg);
   st.begin();
   uint64_t lw[2][4];
   uint32_t eqd[4], end_d = 0;
@@ -824,6 +827,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     if (lane == 0) { L.part[0][j][wv] = a2; L.part[1][j][wv] = b2; }
   }
   wg_barrier();  // part and vb complete
+  st.lap(4);
   if (wv == 0) {
     uint64_t agg[C], pre[C];
     uint32_t h0[C];
@@ -857,6 +861,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       if (lane == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
     }
   }
+  st.lap(5);
   // slot validity (definition level == max_def) of the definition stream's covered values
   if (vtile) {
     const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
@@ -869,7 +874,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     }
   }
   wg_barrier();  // base complete; the counting LDS is free for the emission
+  st.lap(5);
+  st.flush(24);
   if (L.bad) return;  // workgroup-uniform
+  se.begin();
   uint64_t base0[C], base1[C];
 #pragma unroll
   for (uint32_t j = 0; j < C; j++) {
@@ -885,9 +893,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       vm[j] = (vmm[j] >> (16 * h)) & 0xffffu;
     }
     auto gmask = [&](uint32_t gi) -> uint32_t { return (L.gmk[gi][tid] >> (16 * h)) & 0xffffu; };
-    nest_emit_half<R>(b, cd, x, tid, h, f, vm, h ? base1 : base0, gown, gmask, L.u.e, st);
+    nest_emit_half<R>(b, cd, x, tid, h, f, vm, h ? base1 : base0, gown, gmask, L.u.e, se);
   }
-  st.flush(32);
+  se.flush(32);
 }
 
 // Struct validity of the OPTIONAL groups of a leaf with max_rep == 0: entries are the leaf's slots,

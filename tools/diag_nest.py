@@ -1,6 +1,7 @@
-"""Diagnostic: per-phase cycles of k_nest_count and k_nest_emit on cfg4 (diag build, PQ_DEBUG_STAMPS=1).
-Slots 24-31 (k_nest_count) and 32-39 (k_nest_emit) are shared with the DELTA walk and the paired
-dictionary tiles, which cfg4 does not run."""
+"""Diagnostic: per-phase cycles of the nested kernels on cfg4 (diag build, PQ_DEBUG_STAMPS=1): k_nest_tile
+by default (slots 24-31: its counting half; 32-39: its emission), k_nest_count / k_nest_emit with
+PQ_NEST_FUSED=0. The slots are shared with the DELTA walk and the paired dictionary tiles, which cfg4
+does not run."""
 import os
 import sys
 import time
@@ -28,10 +29,13 @@ dt = time.perf_counter() - t0
 d = b.debug_counters()
 print(f"decode {dt*1e3:.3f} ms (cfg4, one decode with stamps)")
 tot = sum(int(d[24 + k]) for k in range(8))
-for k, n in enumerate(["run_stage", "group_marks", "expansion", "page_counts", "packed", "counters", "validity", "-"]):
+fused = os.environ.get("PQ_NEST_FUSED", "1") != "0"
+names = (["run_stage", "group_marks", "expansion", "page_counts", "masks", "lookback", "validity", "-"] if fused else
+         ["run_stage", "group_marks", "expansion", "page_counts", "packed", "counters", "validity", "-"])
+for k, n in enumerate(names):
     v = int(d[24 + k])
-    print(f"nest_count {n:12s} {v:>16d} cycles (wave sums) {v / max(tot, 1):6.3f}")
+    print(f"{'nest_tile ' if fused else 'nest_count'} {n:12s} {v:>16d} cycles (wave sums) {v / max(tot, 1):6.3f}")
 tot = sum(int(d[32 + k]) for k in range(8))
 for k, n in enumerate(["levels_flags", "entry_index", "offsets", "validity", "groups", "-", "-", "-"]):
     v = int(d[32 + k])
-    print(f"nest_emit  {n:12s} {v:>16d} cycles (wave sums) {v / max(tot, 1):6.3f}")
+    print(f"{'  (emit)  ' if fused else 'nest_emit '} {n:12s} {v:>16d} cycles (wave sums) {v / max(tot, 1):6.3f}")
