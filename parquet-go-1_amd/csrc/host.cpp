@@ -487,7 +487,11 @@ struct pqgpu_batch {
   std::vector<uint4> nest_tiles;  // nested fill tiles: {global fill tile, page, tile of the page, chunk}
   std::vector<uint32_t> grp_tiles;  // chunk of every k_group_flat tile (max_rep == 0 leaves with struct bitmaps)
   uint64_t l_grp_tiles = 0;
-  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0;
+  uint64_t o_nest_cnt = 0, o_nest_base = 0, o_nest_tot = 0, l_nest_tiles = 0, l_nest_chunks = 0, l_nest_order = 0;
+  // k_nest_tile's block order within each list-level group: the chunks' tiles interleaved (block
+  // -> tile position), so that a tile's predecessor in its chunk was dispatched a chunk count of
+  // blocks earlier and has usually published by the time the tile looks back
+  std::vector<uint32_t> nest_order;
   uint64_t o_nest_done = 0;
   uint32_t n_nest_empty = 0;  // nested chunks without fill tiles (first in nest_chunks)
   uint32_t nest_first[PQGPU_MAX_NEST + 2] = {};
@@ -1439,6 +1443,19 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
   }
   b->nest_first[PQGPU_MAX_NEST + 1] = (uint32_t)b->nest_tiles.size();
+  b->nest_order.clear();
+  for (uint32_t r = 1; r <= PQGPU_MAX_NEST; r++) {
+    std::vector<uint32_t> cs;
+    uint32_t most = 0;
+    for (uint32_t c : b->nest_chunks)
+      if (b->chunks[c].nest == r && b->chunks[c].nest_ntiles) {
+        cs.push_back(c);
+        most = std::max(most, b->chunks[c].nest_ntiles);
+      }
+    for (uint32_t k = 0; k < most; k++)
+      for (uint32_t c : cs)
+        if (k < b->chunks[c].nest_ntiles) b->nest_order.push_back(b->chunks[c].nest_tile0 + k);
+  }
   // chunks with tiles are scanned by their last k_nest_count tile; the others by k_nest_scan
   std::stable_partition(b->nest_chunks.begin(), b->nest_chunks.end(), [&](uint32_t c) { return b->chunks[c].nest_ntiles == 0; });
   b->n_nest_empty = 0;
@@ -1729,6 +1746,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_rec = take(b->rec_pages.size() * 4);
   b->l_pc = take(b->pc_pages.size() * 4);
   b->l_nest_tiles = take(b->nest_tiles.size() * 16);
+  b->l_nest_order = take(b->nest_order.size() * 4);
   b->l_nest_chunks = take(b->nest_chunks.size() * 4);
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
   b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 4);  // every entry written by k_nest_count
@@ -1928,6 +1946,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->l_rec, b->rec_pages.data(), b->rec_pages.size() * 4), err);
   HIPCHECK(up(b->l_pc, b->pc_pages.data(), b->pc_pages.size() * 4), err);
   HIPCHECK(up(b->l_nest_tiles, b->nest_tiles.data(), b->nest_tiles.size() * 16), err);
+  HIPCHECK(up(b->l_nest_order, b->nest_order.data(), b->nest_order.size() * 4), err);
   HIPCHECK(up(b->l_nest_chunks, b->nest_chunks.data(), b->nest_chunks.size() * 4), err);
   HIPCHECK(up(b->l_grp_tiles, b->grp_tiles.data(), b->grp_tiles.size() * 4), err);
   HIPCHECK(up(b->o_dblk_base, b->dblk_base.data(), np * 8), err);
@@ -1950,7 +1969,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
 
 static BatchDev batch_dev(pqgpu_batch *b) {
   uint8_t *A = b->d_arena;
-  BatchDev d;
+  BatchDev d{};  // (every field not set below is null: err_next, dbg, ...)
   d.pages = (const PageDesc *)(A + b->o_pages);
   d.chunks = (const ChunkDesc *)(A + b->o_chunks);
   d.chunk_err = (unsigned long long *)(A + b->o_err);
@@ -2043,6 +2062,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.pc_pages = (const uint32_t *)(A + b->l_pc);
   l.n_pc_pages = (uint32_t)b->pc_pages.size();
   l.nest_desc = (const uint4 *)(A + b->l_nest_tiles);
+  l.nest_order = (const uint32_t *)(A + b->l_nest_order);
   l.n_nest_tiles = (uint32_t)b->nest_tiles.size();
   for (uint32_t r = 0; r < PQGPU_MAX_NEST + 2; r++) l.nest_first[r] = b->nest_first[r];
   l.nest_chunks = (const uint32_t *)(A + b->l_nest_chunks);

@@ -96,6 +96,8 @@ struct LaunchLists {
   const uint4 *nest_desc; uint32_t n_nest_tiles;         // fill tiles of the nested chunks (k_nest_count / k_nest_emit):
                                                          // {global fill tile, page, tile of the page, chunk}
   uint32_t nest_first[10];        // tiles of chunks with R list levels: [nest_first[R], nest_first[R + 1])
+  const uint32_t *nest_order;     // k_nest_tile: block nest_first[R] + i of group R takes tile position
+                                  // nest_order[nest_first[R] + i] (the group's chunks interleaved)
   const uint32_t *nest_chunks; uint32_t n_nest_chunks, n_nest_empty;  // nested chunks, those without tiles first
   const uint32_t *grp_tiles; uint32_t n_grp_tiles;       // chunk of every k_group_flat tile
   const uint32_t *delta_pages; uint32_t n_delta_pages;   // tiled DELTA pages (header walk, block scan)

@@ -538,7 +538,7 @@ DEV void nest_put_bits(uint32_t *bm, uint64_t off, const uint32_t *row, uint32_t
 // per-counter array is indexed by compile-time constants and stays in registers).
 template <uint32_t R>
 struct NestEmitLDS {
-  uint32_t ent[4][kNestWaveSlots];  // per-wave entry rows
+  uint32_t ent[4][kNestWaveSlots + 4];  // per-wave entry rows (shifted to the destination's 16-B phase)
   uint32_t wtot[2][R + 1][4];
   uint32_t brow[4][kNestWaveSlots / 32 + 1];
 };
@@ -582,7 +582,11 @@ DEV void nest_emit_half(const BatchDev &b, const ChunkDesc &cd, const NestFill &
     const uint32_t lv = j < R ? j : 0;  // j == R: record offsets
     if (j == R && !rec) break;
     if (PQ_ABLATE(b, 16)) break;  // diagnostic bit 16: no offset stores
-    uint32_t m = f[lv], k = P[lv];
+    int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
+    // the row holds entry e at row[a + e], a = dst's dword phase in its 16-B piece, so that the body
+    // leaves as aligned 16-B LDS reads and stores (head and tail entries one by one)
+    const uint32_t a = (uint32_t)((uintptr_t)dst >> 2) & 3u;
+    uint32_t m = f[lv], k = a + P[lv];
     const uint32_t cb = (uint32_t)(run[lv + 1] + P[lv + 1]);  // children before this lane's slots
     while (m) {
       const uint32_t i = __builtin_ctz(m);
@@ -590,8 +594,12 @@ DEV void nest_emit_half(const BatchDev &b, const ChunkDesc &cd, const NestFill &
       row[k++] = j < R ? cb + (uint32_t)__popc(f[lv + 1] & ((1u << i) - 1u)) : (uint32_t)(s + i);
     }
     wave_lds_sync();
-    int32_t *dst = j < R ? gp_u64<int32_t>(cd.lvl_offsets[j]) + run[j] : rec + run[0];
-    for (uint32_t e = lane; e < T[lv]; e += 64) dst[e] = (int32_t)row[e];
+    const uint32_t tn = T[lv], head = min(tn, (4u - a) & 3u), nb = (tn - head) >> 2, t0 = head + 4 * nb;
+    if (lane < head) dst[lane] = (int32_t)row[a + lane];
+    const uint4 *r4 = reinterpret_cast<const uint4 *>(row + a + head);  // (a + head is 0 or 4)
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst + head);
+    for (uint32_t q = lane; q < nb; q += 64) d4[q] = r4[q];
+    if (lane < tn - t0) dst[t0 + lane] = (int32_t)row[a + t0 + lane];
     wave_lds_sync();
   }
   st.lap(2);
@@ -706,7 +714,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
 // only for tiles of its chunk with lower block indices (dispatched before it).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kNsStride = 16;  // u64 per tile: one 128-B line (no two tiles' atomics share a line)
-constexpr uint32_t kNsWin = 16;     // predecessors read per look-back round trip
+#ifndef PQ_NS_WIN
+#define PQ_NS_WIN 16
+#endif
+constexpr uint32_t kNsWin = PQ_NS_WIN;  // predecessors read per look-back round trip (one per lane)
 constexpr uint64_t kNsAgg = 1ull << 62, kNsIncl = 2ull << 62, kNsMask = (1ull << 62) - 1;
 constexpr uint32_t kNsMaxPolls = 1u << 22;  // look-back polls before giving up (seconds: a bound, not a wait)
 
@@ -788,11 +799,11 @@ template <uint32_t R>
 #define PQ_NEST_TILE_WPE1 5
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
-                                                                                                                                     uint32_t counted) {
+                                                                                                                                     uint32_t counted, const uint32_t *order) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestTileLDS<R> L;
-  const uint32_t pos = first + blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const uint32_t pos = gp(order)[first + blockIdx.x], tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const NestFill x = nest_fill(b, gp(tiles)[pos]);
   const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
@@ -874,7 +885,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     }
   }
   wg_barrier();  // base complete; the counting LDS is free for the emission
-  st.lap(5);
+  st.lap(6);
   st.flush(24);
   if (L.bad) return;  // workgroup-uniform
   se.begin();
@@ -1002,7 +1013,7 @@ static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s
 template <uint32_t R>
 static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], counted);
+  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], counted, l.nest_order);
 }
 hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted) {
   if (!l.n_nest_tiles) return hipSuccess;
