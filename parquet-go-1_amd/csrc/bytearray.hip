@@ -405,12 +405,15 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 #ifndef PQ_BA_P0
 #define PQ_BA_P0 1
 #endif
+#ifndef PQ_BA_G
+#define PQ_BA_G 2  // pass B: rounds whose slot pieces are loaded together
+#endif
 template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool PA = false, class EL, bool P0 = false>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,
                    uint32_t lo, uint32_t hi, bool is_dict, bool have, DictTile &tl, EL &L, Stamps &st,
                    const uint4 *lslots = nullptr) {
   // SV: uint4 per slot (at most)
-  constexpr uint32_t G = 2;              // rounds per load group
+  constexpr uint32_t G = PQ_BA_G;        // rounds per load group
   const uint32_t s4 = cd.slot_shift - 4; // SLOT: uint4 per slot = 1 << s4
   constexpr uint32_t R = kRounds;
   const uint64_t vb = b.page_vbase[p];

@@ -721,8 +721,11 @@ constexpr uint32_t kNsWin = PQ_NS_WIN;  // predecessors read per look-back round
 constexpr uint64_t kNsAgg = 1ull << 62, kNsIncl = 2ull << 62, kNsMask = (1ull << 62) - 1;
 constexpr uint32_t kNsMaxPolls = 1u << 22;  // look-back polls before giving up (seconds: a bound, not a wait)
 
+#ifndef PQ_NS_SLEEP
+#define PQ_NS_SLEEP 2  // s_sleep between the polls of a predecessor that has not published
+#endif
 template <uint32_t C>
-DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
+DEV uint32_t nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
   uint64_t *st = b.nest_state;
   const uint32_t lane = lane_id(), j0 = pos - cd.nest_tile0;
   auto publish = [&](uint64_t flag, const uint64_t (&v)[C]) {
@@ -737,7 +740,7 @@ DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, con
   for (uint32_t q = 0; q < C; q++) pre[q] = 0;
   if (j0 == 0) {
     publish(kNsIncl, agg);
-    return;
+    return 0;
   }
   publish(kNsAgg, agg);
   int64_t k = (int64_t)pos - 1;  // the nearest tile not yet added
@@ -746,7 +749,7 @@ DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, con
     if (++polls > kNsMaxPolls) {  // never (a predecessor that does not publish): prefixes past any
 #pragma unroll                   // chunk's slots make the caller write nothing and report it
       for (uint32_t q = 0; q < C; q++) pre[q] = kNsMask;
-      return;
+      return polls;
     }
     const int64_t my = k - (int64_t)lane;
     const bool win = lane < kNsWin, valid = win && my >= (int64_t)cd.nest_tile0;
@@ -771,12 +774,13 @@ DEV void nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, con
     for (uint32_t q = 0; q < C; q++) pre[q] += wave_sum64(lane < upto ? (s[q] & kNsMask) : 0);
     if (stop < h) break;  // reached an inclusive prefix (or the chunk's first tile)
     k -= upto;
-    if (h < 64) __builtin_amdgcn_s_sleep(2);
+    if (h < 64 && PQ_NS_SLEEP) __builtin_amdgcn_s_sleep(PQ_NS_SLEEP);
   }
   uint64_t inc[C];
 #pragma unroll
   for (uint32_t q = 0; q < C; q++) inc[q] = pre[q] + agg[q];
   publish(kNsIncl, inc);
+  return polls;
 }
 
 template <uint32_t R>
@@ -847,7 +851,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       h0[j] = L.part[0][j][0] + L.part[0][j][1] + L.part[0][j][2] + L.part[0][j][3];
       agg[j] = h0[j] + L.part[1][j][0] + L.part[1][j][1] + L.part[1][j][2] + L.part[1][j][3];
     }
-    nest_lookback<C>(b, cd, pos, agg, pre);
+    const uint32_t polls = nest_lookback<C>(b, cd, pos, agg, pre);
+    st.add(7, polls);  // (diagnostic build: look-back round trips)
     bool over = false;  // a counter's entries are at most the chunk's slots (the arrays' capacity)
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {

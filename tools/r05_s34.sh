@@ -11,3 +11,11 @@ tools/gpu_steps.sh \
   "200 s34_diag_nest python -u tools/diag_nest.py" \
   "200 s34_tl4 tools/timeline.sh cfg4" \
   "200 s34_cfg2 $B --config cfg2"
+# (appended) k_ba_emit pass B with 4 / 8 rounds' slot pieces loaded together (4 waves per SIMD: the
+# same two 8-wave workgroups per CU) against the default 2, cfg3
+L=parquet-go-1_amd/lib
+tools/gpu_steps.sh \
+  "200 s34_cfg3 $B --config cfg3" \
+  "200 s34_cfg3_bag4 env PQGPU_LIB=$L/libpqgpu_bag4.so $B --config cfg3" \
+  "200 s34_cfg3_bag8 env PQGPU_LIB=$L/libpqgpu_bag8.so $B --config cfg3" \
+  "200 s34_cfg3_b $B --config cfg3"
