@@ -724,25 +724,27 @@ constexpr uint32_t kNsMaxPolls = 1u << 22;  // look-back polls before giving up 
 #ifndef PQ_NS_SLEEP
 #define PQ_NS_SLEEP 2  // s_sleep between the polls of a predecessor that has not published
 #endif
+// A tile's counter words (wave 0): its aggregates, or, for the chunk's first tile, its inclusive
+// prefixes (lane q < C writes word q; selects, no dynamic register index).
 template <uint32_t C>
-DEV uint32_t nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
-  uint64_t *st = b.nest_state;
-  const uint32_t lane = lane_id(), j0 = pos - cd.nest_tile0;
-  auto publish = [&](uint64_t flag, const uint64_t (&v)[C]) {
-    uint64_t w = 0;
+DEV void nest_publish(const BatchDev &b, uint32_t pos, uint64_t flag, const uint64_t (&v)[C]) {
+  const uint32_t lane = lane_id();
+  uint64_t w = 0;
 #pragma unroll
-    for (uint32_t q = 0; q < C; q++)
-      if (lane == q) w = flag | v[q];  // (selects: no dynamic register index)
-    if (lane < C)
-      __hip_atomic_exchange(&st[(uint64_t)pos * kNsStride + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
+  for (uint32_t q = 0; q < C; q++)
+    if (lane == q) w = flag | v[q];
+  if (lane < C)
+    __hip_atomic_exchange(&b.nest_state[(uint64_t)pos * kNsStride + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The tile's exclusive prefixes `pre` (wave 0), its aggregates already published (nest_publish), then
+// its inclusive prefixes published. Returns the look-back's round trips.
+template <uint32_t C>
+DEV uint32_t nest_resolve(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, const uint64_t (&agg)[C], uint64_t (&pre)[C]) {
+  uint64_t *st = b.nest_state;
+  const uint32_t lane = lane_id();
 #pragma unroll
   for (uint32_t q = 0; q < C; q++) pre[q] = 0;
-  if (j0 == 0) {
-    publish(kNsIncl, agg);
-    return 0;
-  }
-  publish(kNsAgg, agg);
+  if (pos == cd.nest_tile0) return 0;  // (published its inclusive prefixes already)
   int64_t k = (int64_t)pos - 1;  // the nearest tile not yet added
   uint32_t polls = 0;
   for (;;) {
@@ -779,10 +781,14 @@ DEV uint32_t nest_lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t pos,
   uint64_t inc[C];
 #pragma unroll
   for (uint32_t q = 0; q < C; q++) inc[q] = pre[q] + agg[q];
-  publish(kNsIncl, inc);
+  nest_publish<C>(b, pos, kNsIncl, inc);
   return polls;
 }
 
+#ifndef PQ_NEST_TILES
+#define PQ_NEST_TILES 2  // tiles per k_nest_tile workgroup
+#endif
+constexpr uint32_t kNestTiles = PQ_NEST_TILES;
 template <uint32_t R>
 struct NestTileLDS {
   union {
@@ -794,29 +800,22 @@ struct NestTileLDS {
   } u;
   uint32_t part[2][R + 1][4];
   uint32_t gmk[PQGPU_MAX_NEST][256];  // the owned groups' validity masks (the levels are not kept)
-  uint64_t base[R + 1];  // the tile's first entry of each counter (the look-back's prefix)
-  uint32_t half0[R + 1]; // the first half's entries of each counter
-  uint32_t bad;          // the prefixes exceed the chunk's slots (never: no output is written then)
+  uint32_t h0[kNestTiles][R + 1];     // per tile: the first half's entries of each counter
+  uint32_t h1[kNestTiles][R + 1];     // the second half's
+  uint64_t base[R + 1];               // the tile being emitted: its first entry of each counter
+  uint32_t bad;                       // its prefixes exceed the chunk's slots (never: it writes nothing)
 };
+// One tile's counting half (k_nest_count's work, without the flag masks leaving registers): the
+// levels expanded, u8 levels / slot validity / page counts written, the masks fm / vmm, the owned
+// groups' masks in L.gmk, the per-half counts in L.h0[q] / L.h1[q], and the tile's aggregates
+// published (wave 0).
 template <uint32_t R>
-#ifndef PQ_NEST_TILE_WPE1
-#define PQ_NEST_TILE_WPE1 5
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
-                                                                                                                                     uint32_t counted, const uint32_t *order) {
+DEV void nest_tile_count(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, bool counted, NestTileLDS<R> &L,
+                         uint32_t (&fm)[R + 1], uint32_t (&vmm)[R + 1], Stamps &st) {
   constexpr uint32_t C = R + 1;
-  const BatchDev b = global_view(b_in);
-  __shared__ NestTileLDS<R> L;
-  const uint32_t pos = gp(order)[first + blockIdx.x], tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const NestFill x = nest_fill(b, gp(tiles)[pos]);
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const PageDesc &pd = b.pages[x.pi];
   const ChunkDesc &cd = b.chunks[x.chunk];
-  // diagnostic build (tools/diag_nest.py): slots 24-31 -- 0 run staging, 1 group marks, 2 expansion,
-  // 3 page counts, 4 flag masks and counts, 5 look-back (wave 0) and its barrier, 6 slot validity;
-  // slots 32-39, the emission as k_nest_emit's
-  PQ_STAMPS(st, b.dbg);
-  PQ_STAMPS(se, b.dbg);
-  st.begin();
   uint64_t lw[2][4];
   uint32_t eqd[4], end_d = 0;
   nest_expand(b, pd, cd, x, L.u.a.st, tid, lw, eqd, end_d, st, !counted);  // (counted: k_nest_pcount's)
@@ -828,12 +827,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   }
   const bool swar = cd.max_def < 128;
   const uint32_t inm = nest_cover_mask(b, pd, cd, x, tid);
-  const uint32_t gown = nest_groups_owned(cd);
-  for (uint32_t gm = gown; gm; gm &= gm - 1) {
+  for (uint32_t gm = nest_groups_owned(cd); gm; gm &= gm - 1) {
     const uint32_t gi = (uint32_t)__builtin_ctz(gm);
     L.gmk[gi][tid] = nest_mask<R>(cd, lw, swar, 2, 0, gi);
   }
-  uint32_t fm[C], vmm[C];
 #pragma unroll
   for (uint32_t j = 0; j < C; j++) {
     fm[j] = nest_mask<R>(cd, lw, swar, 0, j, 0) & inm;
@@ -843,21 +840,51 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   }
   wg_barrier();  // part and vb complete
   st.lap(4);
+  // slot validity (definition level == max_def) of the definition stream's covered values
+  if (vtile) {
+    const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
+    const int64_t w0 = x.t0 + 32 * (int64_t)w;
+    if (w0 + 32 > (int64_t)x.lo && w0 < (int64_t)end_d) {
+      const uint32_t v = L.u.a.vb[w];
+      uint32_t *dst = vbits + ((x.sbase + (uint64_t)w0) >> 5);
+      if (w0 >= (int64_t)x.lo && w0 + 32 <= (int64_t)end_d) *dst = v;  // the tile owns the whole word
+      else if (v) atomicOr(dst, v);                                     // shared with a neighbouring page
+    }
+  }
   if (wv == 0) {
-    uint64_t agg[C], pre[C];
-    uint32_t h0[C];
+    uint64_t agg[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
-      h0[j] = L.part[0][j][0] + L.part[0][j][1] + L.part[0][j][2] + L.part[0][j][3];
-      agg[j] = h0[j] + L.part[1][j][0] + L.part[1][j][1] + L.part[1][j][2] + L.part[1][j][3];
+      const uint32_t a0 = L.part[0][j][0] + L.part[0][j][1] + L.part[0][j][2] + L.part[0][j][3];
+      const uint32_t a1 = L.part[1][j][0] + L.part[1][j][1] + L.part[1][j][2] + L.part[1][j][3];
+      agg[j] = a0 + a1;
+      if (lane == j) { L.h0[q][j] = a0; L.h1[q][j] = a1; }
     }
-    const uint32_t polls = nest_lookback<C>(b, cd, pos, agg, pre);
-    st.add(7, polls);  // (diagnostic build: look-back round trips)
+    nest_publish<C>(b, pos, pos == cd.nest_tile0 ? kNsIncl : kNsAgg, agg);
+  }
+  st.lap(6);
+}
+// One tile's second half: its bases by the look-back (wave 0), the chunk's totals and closing
+// entries from its last tile, then the outputs (nest_emit_half). The caller synchronises after it.
+template <uint32_t R>
+DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, NestTileLDS<R> &L,
+                        const uint32_t (&fm)[R + 1], const uint32_t (&vmm)[R + 1], Stamps &st, Stamps &se) {
+  constexpr uint32_t C = R + 1;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const PageDesc &pd = b.pages[x.pi];
+  const ChunkDesc &cd = b.chunks[x.chunk];
+  st.lap(7);
+  if (wv == 0) {
+    uint64_t agg[C], pre[C];
+#pragma unroll
+    for (uint32_t j = 0; j < C; j++) agg[j] = (uint64_t)L.h0[q][j] + L.h1[q][j];
+    const uint32_t polls = nest_resolve<C>(b, cd, pos, agg, pre);
+    st.add(3, polls);  // (diagnostic build: look-back round trips, in place of the page counts' slot)
     bool over = false;  // a counter's entries are at most the chunk's slots (the arrays' capacity)
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
       over |= pre[j] > cd.num_slots || pre[j] + agg[j] > cd.num_slots;
-      if (lane == j) { L.base[j] = pre[j]; L.half0[j] = h0[j]; }
+      if (lane == j) L.base[j] = pre[j];
     }
     if (lane == 0) {
       L.bad = over;
@@ -877,29 +904,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
       if (lane == 0 && rec) rec[tot[0]] = (int32_t)cd.num_slots;
     }
   }
-  st.lap(5);
-  // slot validity (definition level == max_def) of the definition stream's covered values
-  if (vtile) {
-    const uint32_t w = tid;  // kLfTile / 32 = 256 words: one per thread
-    const int64_t w0 = x.t0 + 32 * (int64_t)w;
-    if (w0 + 32 > (int64_t)x.lo && w0 < (int64_t)end_d) {
-      const uint32_t v = L.u.a.vb[w];
-      uint32_t *dst = vbits + ((x.sbase + (uint64_t)w0) >> 5);
-      if (w0 >= (int64_t)x.lo && w0 + 32 <= (int64_t)end_d) *dst = v;  // the tile owns the whole word
-      else if (v) atomicOr(dst, v);                                     // shared with a neighbouring page
-    }
-  }
   wg_barrier();  // base complete; the counting LDS is free for the emission
-  st.lap(6);
-  st.flush(24);
+  st.lap(5);
   if (L.bad) return;  // workgroup-uniform
   se.begin();
   uint64_t base0[C], base1[C];
 #pragma unroll
   for (uint32_t j = 0; j < C; j++) {
     base0[j] = L.base[j];
-    base1[j] = base0[j] + L.half0[j];
+    base1[j] = base0[j] + L.h0[q][j];
   }
+  const uint32_t gown = nest_groups_owned(cd);
 #pragma unroll 1
   for (uint32_t h = 0; h < 2; h++) {
     uint32_t f[C], vm[C];
@@ -911,6 +926,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     auto gmask = [&](uint32_t gi) -> uint32_t { return (L.gmk[gi][tid] >> (16 * h)) & 0xffffu; };
     nest_emit_half<R>(b, cd, x, tid, h, f, vm, h ? base1 : base0, gown, gmask, L.u.e, se);
   }
+  se.lap(5);
+}
+
+// k_nest_tile<R>: kNestTiles tiles per workgroup (block-order positions from `order`): every tile's
+// counting half first, publishing its aggregates, then each tile's look-back and outputs -- the
+// look-back of the first tile waits while the second one counts. A tile whose chunk has group bitmaps
+// of its own (their masks live in one LDS set) is emitted right after its count.
+template <uint32_t R>
+#ifndef PQ_NEST_TILE_WPE1
+#define PQ_NEST_TILE_WPE1 (PQ_NEST_TILES > 1 ? 4 : 5)  // R = 1: 125 / 96 VGPRs
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
+                                                                                                                                     uint32_t n, uint32_t counted, const uint32_t *order) {
+  constexpr uint32_t C = R + 1;
+  const BatchDev b = global_view(b_in);
+  __shared__ NestTileLDS<R> L;
+  // diagnostic build (tools/diag_nest.py): slots 24-31 -- 0 run staging, 1 group marks, 2 expansion,
+  // 3 look-back round trips (count), 4 flag masks and counts, 5 look-back (wave 0) and its barrier,
+  // 6 slot validity and the aggregates, 7 between the counts and the look-back; slots 32-39, the
+  // emission as k_nest_emit's
+  PQ_STAMPS(st, b.dbg);
+  PQ_STAMPS(se, b.dbg);
+  st.begin();
+  static_assert(kNestTiles == 1 || kNestTiles == 2, "one or two tiles per workgroup");
+  uint32_t fm0[C], vmm0[C], fm1[C], vmm1[C];  // (two named sets: an indexed pair would go to scratch)
+  uint32_t pend = 0;  // tiles counted, not yet emitted
+  auto count = [&](uint32_t q, uint32_t (&fm)[C], uint32_t (&vmm)[C]) {
+    const uint32_t k = blockIdx.x * kNestTiles + q;
+    if (k >= n) return;  // workgroup-uniform
+    const uint32_t pos = gp(order)[first + k];
+    const NestFill x = nest_fill(b, gp(tiles)[pos]);
+    nest_tile_count<R>(b, x, pos, q, counted != 0, L, fm, vmm, st);
+    if (nest_groups_owned(b.chunks[x.chunk])) {  // (one set of group masks in LDS)
+      nest_tile_emit<R>(b, x, pos, q, L, fm, vmm, st, se);
+      wg_barrier();
+    } else {
+      pend |= 1u << q;
+    }
+  };
+  auto emit = [&](uint32_t q, const uint32_t (&fm)[C], const uint32_t (&vmm)[C]) {
+    if (!((pend >> q) & 1u)) return;
+    const uint32_t pos = gp(order)[first + blockIdx.x * kNestTiles + q];
+    const NestFill x = nest_fill(b, gp(tiles)[pos]);
+    nest_tile_emit<R>(b, x, pos, q, L, fm, vmm, st, se);
+    wg_barrier();  // (the next tile's bases and rows reuse the LDS)
+  };
+  count(0, fm0, vmm0);
+  if (kNestTiles > 1) count(1, fm1, vmm1);
+  emit(0, fm0, vmm0);
+  if (kNestTiles > 1) emit(1, fm1, vmm1);
+  st.flush(24);
   se.flush(32);
 }
 
@@ -1018,7 +1084,8 @@ static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s
 template <uint32_t R>
 static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], counted, l.nest_order);
+  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3((n + kNestTiles - 1) / kNestTiles), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], n,
+                            counted, l.nest_order);
 }
 hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted) {
   if (!l.n_nest_tiles) return hipSuccess;

@@ -30,7 +30,7 @@ d = b.debug_counters()
 print(f"decode {dt*1e3:.3f} ms (cfg4, one decode with stamps)")
 tot = sum(int(d[24 + k]) for k in range(8))
 fused = os.environ.get("PQ_NEST_FUSED", "1") != "0"
-names = (["run_stage", "group_marks", "expansion", "page_counts", "masks", "lookback", "validity", "polls(count)"] if fused else
+names = (["run_stage", "group_marks", "expansion", "polls(count)", "masks", "lookback+barrier", "validity+publish", "to_lookback"] if fused else
          ["run_stage", "group_marks", "expansion", "page_counts", "packed", "counters", "validity", "-"])
 for k, n in enumerate(names):
     v = int(d[24 + k])
