@@ -786,7 +786,7 @@ DEV uint32_t nest_resolve(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, 
 }
 
 #ifndef PQ_NEST_TILES
-#define PQ_NEST_TILES 2  // tiles per k_nest_tile workgroup
+#define PQ_NEST_TILES 1  // tiles per k_nest_tile workgroup (2: cfg4 k_nest_tile 0.63 -> 0.73 ms, profiles/r05_s36_probe_nest_pairs.txt)
 #endif
 constexpr uint32_t kNestTiles = PQ_NEST_TILES;
 template <uint32_t R>
