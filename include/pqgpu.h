@@ -359,7 +359,7 @@ int pqgpu_batch_debug_counters(pqgpu_batch *b, uint64_t *out64, int reset);
 int pqgpu_batch_kernel_timing(pqgpu_batch *b, int enable);
 int pqgpu_batch_kernel_time(pqgpu_batch *b, double *avg_ms, int64_t *launches, char *name, size_t name_len);
 /* The same for every timed launch slot (0 <= slot < PQGPU_TIMER_SLOTS); PQ_ERR_ARG past the end. */
-#define PQGPU_TIMER_SLOTS 24
+#define PQGPU_TIMER_SLOTS 25
 int pqgpu_batch_kernel_slot(pqgpu_batch *b, int slot, double *avg_ms, int64_t *launches, char *name,
                             size_t name_len);
 /* Algorithmic bytes (sections read + outputs written, counted once) of one launch

@@ -386,7 +386,7 @@ static const char *kTimerNames[PQGPU_TIMER_SLOTS] = {
     "k_levels", "k_values_delta", "k_scan_runs", "k_bases", "k_ba_sums", "k_ba_scan",
     "k_ba_emit", "k_records", "k_values_dict", "k_values", "k_delta_prep", "k_snappy", "k_dict_slots",
     "k_nest_count", "k_nest_emit", "k_level_fill", "k_nest_scan", "k_pba", "k_ba_delta", "k_dba_gather",
-    "k_values_copy", "k_group_flat", "k_nest_tile", "k_nest_pcount"};
+    "k_values_copy", "k_group_flat", "k_nest_tile", "k_nest_pcount", "k_nest_tcount"};
 
 // The staged page bytes of a batch: grows geometrically without zero-filling, and in a batch
 // with a device context lives in pinned host memory, so upload's H2D copy reads it directly
@@ -528,6 +528,10 @@ struct pqgpu_batch {
   // 0.38 -> 1.1 ms, profiles/r05_s30_probe_cfg4_sched.txt), so k_nest_tile counts them by default.
   bool level_split = !getenv("PQ_LV_SPLIT") || atoi(getenv("PQ_LV_SPLIT")) != 0;
   bool nest_pcount = getenv("PQ_NEST_PCOUNT") && atoi(getenv("PQ_NEST_PCOUNT")) != 0;
+  // Batches whose nested chunks all have one list level: every tile's counts from the run tables
+  // (k_nest_tcount) and a per-chunk scan before k_nest_tile, which then takes its bases from them
+  // instead of looking back over the chunk's earlier tiles; PQ_NEST_TCOUNT=0: the look-back
+  bool nest_tcount = !getenv("PQ_NEST_TCOUNT") || atoi(getenv("PQ_NEST_TCOUNT")) != 0;
   // (cfg4: 1.59 -> 1.47 ms, profiles/r05_s29_probe_cfg4_fused.txt)
   bool nest_fused = !getenv("PQ_NEST_FUSED") || atoi(getenv("PQ_NEST_FUSED")) != 0;
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and
@@ -2219,6 +2223,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
         e = timed(b, 22, b->ctx->aux, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, b->ctx->aux, true); });
       if (e == hipSuccess) e = hipEventRecord(b->ev_aux_join, b->ctx->aux);
       aux_out = e == hipSuccess;
+      return e;
+    }
+    if (b->nest_fused && b->nest_tcount && l.nest_first[2] == l.nest_first[PQGPU_MAX_NEST + 1]) {  // (all R = 1)
+      hipError_t e = timed(b, 24, st, l.n_nest_tiles, [&] { return launch_nest_tcount(d, l, st); });
+      if (e == hipSuccess) e = timed(b, 22, st, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, st, false, true); });
       return e;
     }
     if (b->nest_fused) return timed(b, 22, st, l.n_nest_tiles, [&] { return launch_nest_tile(d, l, st, false); });

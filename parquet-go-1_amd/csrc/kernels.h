@@ -129,7 +129,10 @@ hipError_t launch_nest_count(const BatchDev &b, const LaunchLists &l, hipStream_
 hipError_t launch_nest_scan(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_nest_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // the two passes in one (count, look-back over the chunk's earlier tiles, emit): k_nest_tile
-hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted);
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted, bool based = false);
+// the one-list-level tiles' counts from the run tables and every nested chunk's scan (k_nest_tcount,
+// k_nest_scan): k_nest_tile then takes its bases from them instead of looking back
+hipError_t launch_nest_tcount(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 // the nested pages' record and non-null counts from the level run tables (k_nest_pcount)
 hipError_t launch_nest_pcount(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 constexpr uint32_t kGrpTileHost = 8192;  // nested.hip kGrpTile: slots per k_group_flat workgroup

@@ -810,8 +810,8 @@ struct NestTileLDS {
 // groups' masks in L.gmk, the per-half counts in L.h0[q] / L.h1[q], and the tile's aggregates
 // published (wave 0).
 template <uint32_t R>
-DEV void nest_tile_count(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, bool counted, NestTileLDS<R> &L,
-                         uint32_t (&fm)[R + 1], uint32_t (&vmm)[R + 1], Stamps &st) {
+DEV void nest_tile_count(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, bool counted, bool based,
+                         NestTileLDS<R> &L, uint32_t (&fm)[R + 1], uint32_t (&vmm)[R + 1], Stamps &st) {
   constexpr uint32_t C = R + 1;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const PageDesc &pd = b.pages[x.pi];
@@ -860,14 +860,14 @@ DEV void nest_tile_count(const BatchDev &b, const NestFill &x, uint32_t pos, uin
       agg[j] = a0 + a1;
       if (lane == j) { L.h0[q][j] = a0; L.h1[q][j] = a1; }
     }
-    nest_publish<C>(b, pos, pos == cd.nest_tile0 ? kNsIncl : kNsAgg, agg);
+    if (!based) nest_publish<C>(b, pos, pos == cd.nest_tile0 ? kNsIncl : kNsAgg, agg);
   }
   st.lap(6);
 }
 // One tile's second half: its bases by the look-back (wave 0), the chunk's totals and closing
 // entries from its last tile, then the outputs (nest_emit_half). The caller synchronises after it.
 template <uint32_t R>
-DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, NestTileLDS<R> &L,
+DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint32_t q, bool based, NestTileLDS<R> &L,
                         const uint32_t (&fm)[R + 1], const uint32_t (&vmm)[R + 1], Stamps &st, Stamps &se) {
   constexpr uint32_t C = R + 1;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
@@ -878,9 +878,18 @@ DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint
     uint64_t agg[C], pre[C];
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) agg[j] = (uint64_t)L.h0[q][j] + L.h1[q][j];
-    const uint32_t polls = nest_resolve<C>(b, cd, pos, agg, pre);
-    st.add(3, polls);  // (diagnostic build: look-back round trips, in place of the page counts' slot)
     bool over = false;  // a counter's entries are at most the chunk's slots (the arrays' capacity)
+    if (based) {  // k_nest_tcount + k_nest_scan: the bases are known, and the counts must be this tile's
+#pragma unroll
+      for (uint32_t j = 0; j < C; j++) {
+        pre[j] = b.nest_base[(2 * (uint64_t)pos) * kNestCnt + j];
+        over |= b.nest_cnt[(2 * (uint64_t)pos) * kNestCnt + j] != L.h0[q][j] ||
+                b.nest_cnt[(2 * (uint64_t)pos + 1) * kNestCnt + j] != L.h1[q][j];
+      }
+    } else {
+      const uint32_t polls = nest_resolve<C>(b, cd, pos, agg, pre);
+      st.add(3, polls);  // (diagnostic build: look-back round trips, in place of the page counts' slot)
+    }
 #pragma unroll
     for (uint32_t j = 0; j < C; j++) {
       over |= pre[j] > cd.num_slots || pre[j] + agg[j] > cd.num_slots;
@@ -890,7 +899,7 @@ DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint
       L.bad = over;
       if (over) report(b, x.chunk, 1, pd.page_in_chunk, ST_VALUES, 0, PQ_ERR_UNSUPPORTED);  // internal error
     }
-    if (pos - cd.nest_tile0 == cd.nest_ntiles - 1 && !over) {  // the chunk's last tile: totals, closing entries
+    if (!based && pos - cd.nest_tile0 == cd.nest_ntiles - 1 && !over) {  // the chunk's last tile: totals, closing entries
       uint64_t tot[C];
 #pragma unroll
       for (uint32_t j = 0; j < C; j++) {
@@ -929,6 +938,91 @@ DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint
   se.lap(5);
 }
 
+// Fields >= D among the bw-bit fields of x (zero past its last field): the even fields, then the odd
+// ones moved onto the even positions, each with a field's width of zero bits above it, so that
+// field + (2^bw - D) carries into that gap exactly when field >= D. fm / ad / cb: every even position
+// below 56 / bw fields -- the field mask, the addend and the carry bits.
+struct FieldsGe {
+  uint64_t fm, ad, cb;
+  uint32_t bw;
+  DEV FieldsGe(uint32_t w, uint32_t D) : fm(0), ad(0), cb(0), bw(w) {
+    const uint32_t k = 56 / w;
+    for (uint32_t i = 0; i < k; i += 2) {
+      fm |= ((1ull << w) - 1ull) << (i * w);
+      ad |= (uint64_t)((1u << w) - D) << (i * w);
+      cb |= 1ull << (i * w + w);
+    }
+  }
+  DEV uint32_t operator()(uint64_t x) const {
+    return (uint32_t)__popcll(((x & fm) + ad) & cb) + (uint32_t)__popcll((((x >> bw) & fm) + ad) & cb);
+  }
+};
+
+// k_nest_tcount (chunks with one list level): each nested tile's counts per 4,096-slot half straight
+// from the level run tables -- counter 0, the list starts (repetition level 0), from the repetition
+// stream; counter 1, the element slots (definition level >= list_def[0]), from the definition
+// stream; both over the slots both streams cover, as k_nest_tile's masks count them. RLE runs count
+// whole, bit-packed runs 64 bits at a time (fields_ge). One wave per tile, a run per lane and step.
+// k_nest_scan then turns the counts into every half's bases, so k_nest_tile looks back on nothing.
+__global__ void __launch_bounds__(256) k_nest_tcount(BatchDev b_in, const uint4 *tiles, uint32_t first, uint32_t n) {
+  const BatchDev b = global_view(b_in);
+  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (w >= n) return;  // wave-uniform
+  const uint32_t pos = first + w;
+  const NestFill x = nest_fill(b, gp(tiles)[pos]);
+  const PageDesc &pd = b.pages[x.pi];
+  const ChunkDesc &cd = b.chunks[x.chunk];
+  const uint32_t cov_r = b.lv_meta[4 * x.pi + 1], cov_d = cd.max_def ? b.lv_meta[4 * x.pi + 3] : pd.num_slots;
+  const uint32_t endc = min(x.hi, min(cov_r, cov_d));
+  const int64_t hmid = x.t0 + (int64_t)kNestHalf;  // the halves: [lo, mid) and [mid, endc)
+  const uint32_t mid = (uint32_t)min(max(hmid, (int64_t)x.lo), (int64_t)max(endc, x.lo));
+  uint32_t cnt[2][2] = {{0, 0}, {0, 0}};  // [counter][half]
+  if (x.lo < endc) {
+#pragma unroll
+    for (uint32_t s2 = 0; s2 < 2; s2++) {  // stream 0: repetition (counter 0), 1: definition (counter 1)
+      const uint32_t nr = b.lv_meta[4 * x.pi + 2 * s2];
+      if (!nr) continue;
+      const uint2 *runs = b.lv_runs + b.lv_run_base[2 * x.pi + s2];
+      const uint32_t r0 = b.lv_tile_run[2 * (uint64_t)x.t + s2];
+      const uint8_t *src = gp_u64<const uint8_t>(pd.data) + (s2 ? pd.def_off : pd.rep_off);
+      const uint32_t slen = s2 ? pd.def_len : pd.rep_len;
+      const uint32_t bw = s2 ? (uint32_t)cd.def_bw : (uint32_t)cd.rep_bw;
+      const uint32_t D = s2 ? (uint32_t)cd.list_def[0] : 1u;  // rep: count the fields below 1
+      const uint32_t k = 56 / bw;
+      const FieldsGe ge(bw, D);
+      for (uint32_t r = r0 + lane; r < nr; r += 64) {
+        const uint2 run = runs[r];
+        const uint32_t x0 = max(run.x, x.lo), x1 = min(r + 1 < nr ? runs[r + 1].x : endc, endc);
+        if (run.x >= endc) break;  // (lanes past the tile: their runs start later still)
+        if (x0 >= x1) continue;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+          const uint32_t a = h ? max(x0, mid) : x0, e = h ? x1 : min(x1, mid);
+          if (a >= e) continue;
+          uint32_t c = 0;
+          if (!(run.y >> 31)) {  // RLE
+            c = run.y >= D ? e - a : 0u;
+          } else {
+            uint64_t bo = (uint64_t)(run.y & 0x7fffffffu) * 8 + (uint64_t)(a - run.x) * bw;
+            for (uint32_t v = a; v < e; v += k, bo += (uint64_t)k * bw) {
+              const uint32_t m = min(k, e - v);
+              c += ge(bits64c(src, slen, bo, m * bw));
+            }
+          }
+          cnt[s2][h] += s2 ? c : (e - a) - c;  // rep: the fields below 1 (list starts)
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 2; j++)
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t t = (uint32_t)wave_sum64(cnt[j][h]);
+      if (lane == 0) b.nest_cnt[(2 * (uint64_t)pos + h) * kNestCnt + j] = t;
+    }
+}
+
 // k_nest_tile<R>: kNestTiles tiles per workgroup (block-order positions from `order`): every tile's
 // counting half first, publishing its aggregates, then each tile's look-back and outputs -- the
 // look-back of the first tile waits while the second one counts. A tile whose chunk has group bitmaps
@@ -938,7 +1032,7 @@ template <uint32_t R>
 #define PQ_NEST_TILE_WPE1 (PQ_NEST_TILES > 1 ? 4 : 5)  // R = 1: 125 / 96 VGPRs
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
-                                                                                                                                     uint32_t n, uint32_t counted, const uint32_t *order) {
+                                                                                                                                     uint32_t n, uint32_t counted, const uint32_t *order, uint32_t based) {
   constexpr uint32_t C = R + 1;
   const BatchDev b = global_view(b_in);
   __shared__ NestTileLDS<R> L;
@@ -957,9 +1051,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     if (k >= n) return;  // workgroup-uniform
     const uint32_t pos = gp(order)[first + k];
     const NestFill x = nest_fill(b, gp(tiles)[pos]);
-    nest_tile_count<R>(b, x, pos, q, counted != 0, L, fm, vmm, st);
+    nest_tile_count<R>(b, x, pos, q, counted != 0, based != 0, L, fm, vmm, st);
     if (nest_groups_owned(b.chunks[x.chunk])) {  // (one set of group masks in LDS)
-      nest_tile_emit<R>(b, x, pos, q, L, fm, vmm, st, se);
+      nest_tile_emit<R>(b, x, pos, q, based != 0, L, fm, vmm, st, se);
       wg_barrier();
     } else {
       pend |= 1u << q;
@@ -969,7 +1063,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
     if (!((pend >> q) & 1u)) return;
     const uint32_t pos = gp(order)[first + blockIdx.x * kNestTiles + q];
     const NestFill x = nest_fill(b, gp(tiles)[pos]);
-    nest_tile_emit<R>(b, x, pos, q, L, fm, vmm, st, se);
+    nest_tile_emit<R>(b, x, pos, q, based != 0, L, fm, vmm, st, se);
     wg_barrier();  // (the next tile's bases and rows reuse the LDS)
   };
   count(0, fm0, vmm0);
@@ -1082,24 +1176,33 @@ static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s
   if (n) hipLaunchKernelGGL(k_nest_emit<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R]);
 }
 template <uint32_t R>
-static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted) {
+static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted, uint32_t based) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
   if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3((n + kNestTiles - 1) / kNestTiles), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], n,
-                            counted, l.nest_order);
+                            counted, l.nest_order, based);
 }
-hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted) {
+// (based: every tile's bases from k_nest_tcount + k_nest_scan, chunks with one list level only)
+hipError_t launch_nest_tile(const BatchDev &b, const LaunchLists &l, hipStream_t s, bool counted, bool based) {
   if (!l.n_nest_tiles) return hipSuccess;
   // tiles are grouped by list levels (host.cpp): one instantiation per group; a chunk's tiles are
   // contiguous and in slot order within one launch (the look-back's predecessors)
   const uint32_t c = counted ? 1u : 0u;
-  launch_tile_r<1>(b, l, s, c);
-  launch_tile_r<2>(b, l, s, c);
-  launch_tile_r<3>(b, l, s, c);
-  launch_tile_r<4>(b, l, s, c);
-  launch_tile_r<5>(b, l, s, c);
-  launch_tile_r<6>(b, l, s, c);
-  launch_tile_r<7>(b, l, s, c);
-  launch_tile_r<8>(b, l, s, c);
+  launch_tile_r<1>(b, l, s, c, based ? 1u : 0u);
+  launch_tile_r<2>(b, l, s, c, 0u);
+  launch_tile_r<3>(b, l, s, c, 0u);
+  launch_tile_r<4>(b, l, s, c, 0u);
+  launch_tile_r<5>(b, l, s, c, 0u);
+  launch_tile_r<6>(b, l, s, c, 0u);
+  launch_tile_r<7>(b, l, s, c, 0u);
+  launch_tile_r<8>(b, l, s, c, 0u);
+  return hipGetLastError();
+}
+// the R = 1 tiles' counts (k_nest_tcount), then every nested chunk's scan (k_nest_scan: bases, totals
+// and closing entries; chunks without tiles too)
+hipError_t launch_nest_tcount(const BatchDev &b, const LaunchLists &l, hipStream_t s) {
+  const uint32_t n = l.nest_first[2] - l.nest_first[1];
+  if (n) hipLaunchKernelGGL(k_nest_tcount, dim3((n + 3) / 4), dim3(256), 0, s, b, l.nest_desc, l.nest_first[1], n);
+  if (l.n_nest_chunks) hipLaunchKernelGGL(k_nest_scan, dim3(l.n_nest_chunks), dim3(256), 0, s, b, l.nest_chunks);
   return hipGetLastError();
 }
 hipError_t launch_nest_pcount(const BatchDev &b, const LaunchLists &l, hipStream_t s) {

@@ -119,7 +119,7 @@ class PipelineStats(ctypes.Structure):
 
 
 _LIB = None
-TIMER_SLOTS = 24  # PQGPU_TIMER_SLOTS
+TIMER_SLOTS = 25  # PQGPU_TIMER_SLOTS
 ABI_VERSION = 8  # PQGPU_ABI_VERSION in include/pqgpu.h (struct layouts above)
 _EXPORTS = [
     "pqgpu_abi_version", "pqgpu_status_string", "pqgpu_ctx_create", "pqgpu_ctx_destroy", "pqgpu_file_open",
