@@ -528,10 +528,12 @@ struct pqgpu_batch {
   // 0.38 -> 1.1 ms, profiles/r05_s30_probe_cfg4_sched.txt), so k_nest_tile counts them by default.
   bool level_split = !getenv("PQ_LV_SPLIT") || atoi(getenv("PQ_LV_SPLIT")) != 0;
   bool nest_pcount = getenv("PQ_NEST_PCOUNT") && atoi(getenv("PQ_NEST_PCOUNT")) != 0;
-  // Batches whose nested chunks all have one list level: every tile's counts from the run tables
-  // (k_nest_tcount) and a per-chunk scan before k_nest_tile, which then takes its bases from them
-  // instead of looking back over the chunk's earlier tiles; PQ_NEST_TCOUNT=0: the look-back
-  bool nest_tcount = !getenv("PQ_NEST_TCOUNT") || atoi(getenv("PQ_NEST_TCOUNT")) != 0;
+  // PQ_NEST_TCOUNT=1 (batches whose nested chunks all have one list level): every tile's counts from
+  // the run tables (k_nest_tcount) and a per-chunk scan before k_nest_tile, which then takes its bases
+  // from them instead of looking back over the chunk's earlier tiles. Off: k_nest_tile without the
+  // look-back is only 0.63 -> 0.60 ms, and the counts cost 0.13 ms (cfg4 1.37 -> 1.47 ms,
+  // profiles/r05_s38_probe_nest_tcount.txt): the look-back's waits overlap other workgroups' work.
+  bool nest_tcount = getenv("PQ_NEST_TCOUNT") && atoi(getenv("PQ_NEST_TCOUNT")) != 0;
   // (cfg4: 1.59 -> 1.47 ms, profiles/r05_s29_probe_cfg4_fused.txt)
   bool nest_fused = !getenv("PQ_NEST_FUSED") || atoi(getenv("PQ_NEST_FUSED")) != 0;
   // PLAIN / BOOLEAN copies inside k_values (on the side stream, beside the level kernels and

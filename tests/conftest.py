@@ -26,12 +26,12 @@ def gpu_ctx():
     return pqgpu.Context(0)
 
 
-@pytest.fixture(params=["fused", "fused_lookback", "two_pass"])
+@pytest.fixture(params=["fused", "fused_tcount", "two_pass"])
 def nest_mode(request, monkeypatch):
-    """Nested arrays by k_nest_tile (one pass; the default takes one-list-level chunks' bases from
-    k_nest_tcount + k_nest_scan, deeper ones by a decoupled look-back), by k_nest_tile looking back
-    everywhere (PQ_NEST_TCOUNT=0), and by k_nest_count + k_nest_emit (PQ_NEST_FUSED=0): all three
-    must give the reference's arrays."""
+    """Nested arrays by k_nest_tile (one pass with a decoupled look-back: the default), by k_nest_tile
+    with one-list-level chunks' bases from k_nest_tcount + k_nest_scan (PQ_NEST_TCOUNT=1; its tiles
+    report any count that differs from their own), and by k_nest_count + k_nest_emit
+    (PQ_NEST_FUSED=0): all three must give the reference's arrays."""
     monkeypatch.setenv("PQ_NEST_FUSED", "0" if request.param == "two_pass" else "1")
-    monkeypatch.setenv("PQ_NEST_TCOUNT", "0" if request.param == "fused_lookback" else "1")
+    monkeypatch.setenv("PQ_NEST_TCOUNT", "1" if request.param == "fused_tcount" else "0")
     return request.param

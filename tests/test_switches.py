@@ -22,7 +22,7 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_SCAN_SLOTS=0    byte-array slot tables by their own k_dict_slots launch instead of k_scan_slots
 - PQ_LV_SPLIT=0      nested batches' repetition-stream level kernels on the batch stream, not beside
 - PQ_NEST_PCOUNT=1   the nested pages' counts by k_nest_pcount, k_nest_tile beside the values path
-- PQ_NEST_TCOUNT=0   k_nest_tile's bases by its look-back instead of k_nest_tcount + k_nest_scan
+- PQ_NEST_TCOUNT=1   k_nest_tile's bases from k_nest_tcount + k_nest_scan instead of its look-back
 """
 import pytest
 
@@ -58,7 +58,7 @@ SWITCHES = {
     "slots_own_launch": {"PQ_SCAN_SLOTS": "0"},
     "lv_no_split": {"PQ_LV_SPLIT": "0"},
     "nest_pcount": {"PQ_NEST_PCOUNT": "1"},
-    "nest_lookback": {"PQ_NEST_TCOUNT": "0"},
+    "nest_tcount": {"PQ_NEST_TCOUNT": "1"},
 }
 
 
