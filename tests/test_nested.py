@@ -230,3 +230,105 @@ def test_deep_file_levels():
     assert md == 6 and len(ld) == 2
     assert int(np.max(r.def_levels)) == 6 and int(np.max(r.rep_levels)) == 2
     assert len(r.def_levels) > 8192 * 4  # several fill tiles per chunk
+
+
+def _b2b_file(bad_page=None):
+    """LIST<INT32> (optional list, optional elements: maxR 1, maxD 3) and a MAP-style dictionary
+    BYTE_ARRAY key leaf (maxR 1, maxD 2), written as V1 pages without statistics, so the batch takes
+    the serial schedule (cfg4's); the level streams are single bit-packed runs.
+    bad_page: that data page of the list leaf gets a definition stream starting with an empty RLE run
+    (hybrid_decoder.go:159-161)."""
+    import os
+    import struct
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
+    import rawpq
+    rng = np.random.default_rng(23)
+    vocab = sorted({bytes(rng.integers(97, 123, int(rng.integers(1, 24)), dtype=np.uint8)) for _ in range(300)})
+    n_rec, per_page = 12_000, 1_500
+    lpages, kpages, lslots, kslots = [], [rawpq.dict_page_ref("BYTE_ARRAY", vocab)], 0, 0
+    for p0 in range(0, n_rec, per_page):
+        lr, ld, lv, kr, kd, ki = [], [], [], [], [], []
+        for _ in range(per_page):
+            u = rng.random()
+            if u < 0.08:
+                lr.append(0), ld.append(0)
+            elif u < 0.15:
+                lr.append(0), ld.append(1)
+            else:
+                for j in range(int(rng.integers(1, 7))):
+                    lr.append(0 if j == 0 else 1)
+                    if rng.random() < 0.1:
+                        ld.append(2)
+                    else:
+                        ld.append(3)
+                        lv.append(int(rng.integers(-(1 << 31), 1 << 31)))
+            u = rng.random()
+            if u < 0.05:
+                kr.append(0), kd.append(0)
+            elif u < 0.1:
+                kr.append(0), kd.append(1)
+            else:
+                for j in range(int(rng.integers(1, 5))):
+                    kr.append(0 if j == 0 else 1), kd.append(2), ki.append(int(rng.integers(0, len(vocab))))
+        page = len(lpages)
+        if page == bad_page:  # rep stream as usual, the def stream: varint 0 (an empty RLE run), value byte
+            body = rawpq.levels_v1_ref(lr, 1) + struct.pack("<I", 2) + b"\x00\x03" + rawpq.plain_encode("INT32", lv)
+            dph = [(1, rawpq.I32, len(lr)), (2, rawpq.I32, rawpq.ENC["PLAIN"]), (3, rawpq.I32, rawpq.ENC["RLE"]),
+                   (4, rawpq.I32, rawpq.ENC["RLE"])]
+            lpages.append(rawpq._page(0, body, 5, dph))
+        else:
+            lpages.append(rawpq.data_page_v1_ref(len(lr), "PLAIN", rawpq.plain_encode("INT32", lv), def_levels=ld,
+                                                 max_def=3, rep_levels=lr, max_rep=1))
+        kpages.append(rawpq.data_page_v1_ref(len(kr), "RLE_DICTIONARY", rawpq.dict_values_section(ki, len(vocab)),
+                                             def_levels=kd, max_def=2, rep_levels=kr, max_rep=1))
+        lslots += len(lr)
+        kslots += len(kr)
+    schema = [[(4, rawpq.BIN, "schema"), (5, rawpq.I32, 2)],
+              rawpq.schema_group("l", "OPTIONAL", 1), rawpq.schema_group("list", "REPEATED", 1),
+              rawpq.schema_leaf("element", "INT32", "OPTIONAL"),
+              rawpq.schema_group("m", "OPTIONAL", 1), rawpq.schema_group("key_value", "REPEATED", 1),
+              rawpq.schema_leaf("key", "BYTE_ARRAY", "REQUIRED")]
+    return rawpq.write_file_schema(schema, [("l.list.element", "INT32"), ("m.key_value.key", "BYTE_ARRAY")],
+                                   [(n_rec, [(lpages, lslots, False), (kpages, kslots, True)])])
+
+
+def test_b2b_file_shape():
+    """The back-to-back fixtures decode in the oracle as intended: the good file whole, the bad one
+    with the reference's empty-RLE-run error on the list leaf's page 2 and the map leaf intact."""
+    good = pqtest.oracle_decode(_b2b_file())
+    assert all(not isinstance(r, O.OracleError) for _, _, r in good)
+    assert all(int(np.max(r.rep_levels)) == 1 for _, _, r in good)
+    bad = pqtest.oracle_decode(_b2b_file(bad_page=2))
+    assert isinstance(bad[0][2], O.OracleError) and bad[0][2].code == 3 and bad[0][2].page == 2
+    assert not isinstance(bad[1][2], O.OracleError)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad_page", [None, 2])
+def test_gpu_back_to_back_decodes(gpu_ctx, nest_mode, bad_page):
+    """Three decodes queued back to back, then one sync (the benchmark's pattern), then decode + sync
+    pairs: every chunk equals the oracle (levels, values, nested arrays) after each, and a level
+    error is reported with the reference's code and page every time."""
+    import pqgpu
+    data = _b2b_file(bad_page)
+    orc = pqtest.oracle_decode(data)
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = [b.add_file_chunk(f, 0, c)[0] for c in range(2)]
+    for rounds in (3, 1, 1):
+        for _ in range(rounds):
+            b.decode()
+        e = b.sync()
+        for (rg, col, o), cid in zip(orc, ids):
+            if isinstance(o, O.OracleError):
+                assert e is not None and (e.code, e.page) == (o.code, o.page), (e, o)
+                continue
+            r = b.result(cid)
+            pqtest.assert_chunk_equal(r, o, f"back-to-back col{col}")
+            lnd, ld, md = _levels_of(data, col)
+            want_levels, want_elem = nested_ref(o.rep_levels, o.def_levels, md, lnd, ld)
+            _check_nested(r.nested, r.element_validity, want_levels, want_elem, f"back-to-back col{col}")
+        if bad_page is None:
+            assert e is None, e
+    b.close()
