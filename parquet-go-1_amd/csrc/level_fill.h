@@ -35,6 +35,27 @@ DEV void lf_group_from(const RT &R, uint32_t m, uint32_t j, const uint8_t *src, 
     if (!(r.y >> 31)) {  // RLE
       pk = 0x0101010101010101ull * (uint64_t)(r.y & 0xffu);
       e = r.y == cmp ? 0xffu : 0u;
+    } else if (bw == 1) {  // bit-packed, 1-bit levels: nibble -> bytes by one multiply (SWAR; cfg4
+      // k_nest_tile 0.632 -> 0.607 ms with the 2-bit case below, profiles/r05_s46_probe_lf_swar.txt)
+      // (x * 0x204081 places bit k of a nibble at 8k and its other copies at 7k'..: no two overlap)
+      const uint32_t x = (uint32_t)bits64c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v - r.x), cnt);
+      const uint32_t lo = ((x & 0xfu) * 0x00204081u) & 0x01010101u, hi = (((x >> 4) & 0xfu) * 0x00204081u) & 0x01010101u;
+      pk = ((uint64_t)hi << 32) | lo;
+      e = cmp == 1 ? x : cmp == 0 ? ~x : 0u;
+    } else if (bw == 2) {  // bit-packed, 2-bit levels: fields -> bytes by two shift-or steps
+      const uint32_t x = (uint32_t)bits64c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v - r.x) * 2, cnt * 2);
+      uint32_t lo = x & 0xffu, hi = (x >> 8) & 0xffu;
+      lo = (lo | (lo << 12)) & 0x000f000fu;
+      hi = (hi | (hi << 12)) & 0x000f000fu;
+      lo = (lo | (lo << 6)) & 0x03030303u;
+      hi = (hi | (hi << 6)) & 0x03030303u;
+      pk = ((uint64_t)hi << 32) | lo;
+      // fields equal to cmp: zero 2-bit fields of x ^ cmp..., their low bits compressed to one bit each
+      const uint32_t t = x ^ (cmp * 0x5555u);
+      uint32_t z = ~(t | (t >> 1)) & 0x5555u;
+      z = (z | (z >> 1)) & 0x3333u;
+      z = (z | (z >> 2)) & 0x0f0fu;
+      e = cmp < 4 ? (z | (z >> 4)) & 0xffu : 0u;  // (no 2-bit field equals a larger cmp)
     } else if (bw <= 7) {  // bit-packed: one read for the segment
       const uint64_t x = bits64c(src, n, (uint64_t)(r.y & 0x7fffffffu) * 8 + (uint64_t)(v - r.x) * bw, cnt * bw);
       pk = 0;
