@@ -1363,6 +1363,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.col.max_rep > 0 && !hc.nest) b->rec_pages.push_back(p);  // nested chunks: k_nest_emit
       if (hc.nest && pd.num_slots) b->pc_pages.push_back(p);
       const uint32_t ns_p = pd.num_slots;
+      const uint32_t plain_tile_b = getenv("PQ_PLAIN_TILE_B") ? (uint32_t)atoi(getenv("PQ_PLAIN_TILE_B")) : 0u;  // (probe)
       auto tiles = [&](uint8_t kind, uint32_t tile) {
         for (uint32_t v0 = 0; v0 < ns_p; v0 += tile) b->items.push_back(WorkItem{p, v0, std::min(v0 + tile, ns_p), kind, {0, 0, 0}});
       };
@@ -1377,7 +1378,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       }
       const bool snappy_values = (pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values;
       switch (pd.vkind) {
-        case VK_PLAIN_FIXED: case VK_PLAIN_INT96: if (!snappy_values) tiles(WI_PLAIN, kPlainTile); break;
+        case VK_PLAIN_FIXED: case VK_PLAIN_INT96:
+          if (!snappy_values) tiles(WI_PLAIN, plain_tile_b ? std::max<uint32_t>(1, plain_tile_b / std::max(1, hc.value_width)) : kPlainTile);
+          break;
         case VK_PLAIN_BOOL: tiles(WI_BOOL, kPlainTile); break;
         case VK_DICT: case VK_RLE_BOOL: {
           if (pd.dict_bw > 0 && ns_p > 0) {
@@ -1757,10 +1760,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->l_grp_tiles = take(b->grp_tiles.size() * 4);
   b->o_nest_cnt = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 4);  // every entry written by k_nest_count
   b->o_nest_base = take((uint64_t)b->nest_tiles.size() * 2 * kNestCnt * 8);
-  for (uint32_t c : b->nest_chunks) {  // the slots' flag masks (written by k_nest_count)
+  for (uint32_t c : b->nest_chunks) {  // the slots' flag masks (written by k_nest_count; two-pass mode only)
     HostChunk &hc = b->chunks[c];
     hc.nest_nmask = 2 * (hc.nest + 1) + hc.ngroups;
-    hc.o_nest_mask = take((uint64_t)hc.nest_ntiles * hc.nest_nmask * 1024);
+    hc.o_nest_mask = b->nest_fused ? 0 : take((uint64_t)hc.nest_ntiles * hc.nest_nmask * 1024);
   }
   b->o_nest_tot = take((uint64_t)nc * kNestCnt * 8);
   b->arena_size = a;
@@ -1873,7 +1876,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.nest_tile0 = hc.nest_tile0;
     cd.nest_ntiles = hc.nest_ntiles;
     cd.nest_nmask = hc.nest ? hc.nest_nmask : 0u;
-    cd.nest_masks = hc.nest ? dp(hc.o_nest_mask) : 0;
+    cd.nest_masks = hc.nest && hc.o_nest_mask ? dp(hc.o_nest_mask) : 0;
     for (uint32_t k = 0; k < PQGPU_MAX_NEST; k++) {
       cd.list_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_def[k] : 0);
       cd.list_null_def[k] = (uint8_t)(k < hc.nest ? hc.col.list_null_def[k] : 0);
@@ -2126,7 +2129,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   const bool any_delta = b->n_delta_items || l.n_delta_pages;
   const bool any_nest = l.n_nest_chunks || l.n_nest_tiles || l.n_grp_tiles;
   // Speculative mode whose values path is the DELTA launch alone (with its fused copies; cfg2): see below
-  const bool delta_major = b->n_groups == 0 && b->spec && any_delta && !any_nest && !b->one_stream &&
+  // (n_delta_items > 0: k_values_delta launches and resets the other key buffer, see err_ready)
+  const bool delta_major = b->n_groups == 0 && b->spec && b->n_delta_items > 0 && !any_nest && !b->one_stream &&
                            b->copy_mode == 0 && !b->levels_first && !l.n_scan_pages && !b->n_dict_items &&
                            l.n_items == b->n_delta_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
                            b->ba_chunks.empty() && !l.n_rec_pages && !side;
@@ -3360,11 +3364,19 @@ int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t 
     same = h == 0;
   }
   if (same) {
-    // link ib to ia itself: ia's own result resolves its levels [0, La) (those it shares further down
-    // its chain come from there, chunk_result recurses), while the chain's root may hold fewer of
-    // them. The chain is walked only to keep the links acyclic: when ia already follows ib, the
-    // arrays are equal and nothing is linked, so chunk_result's walk along share_from ends.
-    int32_t at = ia;
+    // link ib to the nearest chunk of ia's chain that resolves levels [0, La) and groups [0, Ga) itself:
+    // a chunk that shares at least that many from its own link hands out its link's arrays, so ib
+    // can point past it (leaves linked in order, a -> b, b -> c, ..., then all point at a and
+    // chunk_result's recursion stays as deep as the number of distinct sharing depths, <= 8).
+    // Then walk the rest of the chain to keep the links acyclic: when it already reaches ib, the
+    // arrays are equal and nothing is linked.
+    int32_t to = ia;
+    for (int32_t hops = 0; hops <= (int32_t)b->chunks.size(); hops++) {
+      const HostChunk &ht = b->chunks[(size_t)to];
+      if (ht.share_from < 0 || ht.share_from == ib || (int32_t)ht.share_lists < La || (int32_t)ht.share_groups < Ga) break;
+      to = ht.share_from;
+    }
+    int32_t at = to;
     for (int32_t hops = 0; at >= 0 && hops <= (int32_t)b->chunks.size(); hops++) {
       if (at == ib) {
         if (equal) *equal = 1;
@@ -3372,7 +3384,7 @@ int pqgpu_batch_share_ancestors(pqgpu_batch *b, int32_t ia, int32_t ib, int32_t 
       }
       at = b->chunks[(size_t)at].share_from;
     }
-    hb.share_from = ia;
+    hb.share_from = to;
     hb.share_lists = (uint32_t)La;
     hb.share_groups = (uint32_t)Ga;
     if (equal) *equal = 1;

@@ -1537,10 +1537,8 @@ DEV uint32_t sg_run_wave(uint32_t *vb, const uint32_t *stage, uint32_t sa, uint6
   return ones;
 }
 
-__global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages) {
-  const BatchDev b = global_view(b_in);
-  __shared__ LevelSegLDS L;
-  const uint32_t pi = pages[blockIdx.x], lane = lane_id();
+DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
+  const uint32_t lane = lane_id();
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t ns = pd.num_slots;
@@ -1775,6 +1773,17 @@ __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t
     }
   }
   stp.flush(16);
+}
+
+// One wavefront walks pages k, k + gridDim.x, ... of the list: a grid smaller than the page count
+// keeps fewer level waves resident beside the values launch (DELTA-major schedule), each for longer.
+__global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages, uint32_t npages) {
+  const BatchDev b = global_view(b_in);
+  __shared__ LevelSegLDS L;
+  for (uint32_t k = blockIdx.x; k < npages; k += gridDim.x) {
+    wave_lds_sync();  // (the previous page's stage reads are done)
+    levels_seg_page(b, L, pages[k]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -4625,7 +4634,9 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s,
       hipLaunchKernelGGL(k_levels_bw1w, dim3(l.n_level_pages_bw1), dim3(64), 0, s, b, l.level_pages_bw1);
     } else {
       const uint32_t nseg = l.n_level_pages_seg, nrest = l.n_level_pages_bw1 - nseg;
-      if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(nseg), dim3(64), 0, s, b, l.level_pages_bw1);
+      const char *sg = getenv("PQ_SEG_GRID");  // (probe) wavefronts of k_levels_seg; 0: one per page
+      const uint32_t want = sg && atoi(sg) > 0 ? (uint32_t)atoi(sg) : nseg, grid = want < nseg ? want : nseg;
+      if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(grid), dim3(64), 0, s, b, l.level_pages_bw1, nseg);
       if (nrest) hipLaunchKernelGGL(k_levels_bw1, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages_bw1 + nseg);
     }
   }

@@ -735,6 +735,20 @@ DEV void nest_publish(const BatchDev &b, uint32_t pos, uint64_t flag, const uint
 #pragma unroll
   for (uint32_t q = 0; q < C; q++)
     if (lane == q) w = flag | v[q];
+#ifdef PQ_DIAG_STAMPS
+  // diagnostic build, PQ_ABLATE bit 26 (tests/test_nested.py::test_gpu_lookback_torn_publish): the
+  // words go out one by one in reverse order, ~27 us apart, so a successor that polls meanwhile
+  // finds this tile half-way between its aggregates and its inclusive prefixes (the state the
+  // look-back must read again, nest_resolve) — certain, not a rare interleaving
+  if (PQ_ABLATE(b, 26)) {
+    for (int32_t q = (int32_t)C - 1; q >= 0; q--) {
+      if (lane == (uint32_t)q)
+        __hip_atomic_exchange(&b.nest_state[(uint64_t)pos * kNsStride + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < 8; i++) __builtin_amdgcn_s_sleep(127);
+    }
+    return;
+  }
+#endif
   if (lane < C)
     __hip_atomic_exchange(&b.nest_state[(uint64_t)pos * kNsStride + lane], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -769,7 +783,17 @@ DEV uint32_t nest_resolve(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, 
     }
     // a predecessor's C words become visible one by one: one caught between its aggregates and its
     // inclusive prefixes (some of each) is read again, like one not yet published
-    const bool rdy = set && !(any_agg && any_inc), inc = rdy && !any_agg;
+    bool rdy = set && !(any_agg && any_inc);
+    const bool inc = rdy && !any_agg;
+#ifdef PQ_DIAG_STAMPS
+    if (PQ_ABLATE(b, 26)) {  // torn-state injection (nest_publish): wait for the predecessors'
+      // inclusive prefixes instead of taking their aggregates (for up to 2^16 polls), so the reader
+      // is polling while they go out word by word
+      if (b.dbg && lane == 0 && __ballot(win && set && any_agg && any_inc))
+        atomicAdd(&b.dbg[20], 1ull);  // torn predecessors seen, read again (slot 20: no stamp uses it)
+      if (polls < (1u << 16)) rdy = inc;
+    }
+#endif
     const uint64_t incl = __ballot(win && inc), hole = __ballot(win && !rdy);
     const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
     const uint32_t h = hole ? (uint32_t)__builtin_ctzll(hole) : 64u;
@@ -900,6 +924,9 @@ DEV void nest_tile_emit(const BatchDev &b, const NestFill &x, uint32_t pos, uint
     if (lane == 0) {
       L.bad = over;
       if (over) report(b, x.chunk, 1, pd.page_in_chunk, ST_VALUES, 0, PQ_ERR_UNSUPPORTED);  // internal error
+#ifdef PQ_DIAG_STAMPS
+      if (over && PQ_ABLATE(b, 26) && b.dbg) atomicAdd(&b.dbg[20], 1ull << 40);  // the guard fired (high bits)
+#endif
     }
     if (!based && pos - cd.nest_tile0 == cd.nest_ntiles - 1 && !over) {  // the chunk's last tile: totals, closing entries
       uint64_t tot[C];

@@ -87,7 +87,7 @@ struct PageDesc {        // 104 B
   uint32_t dict_tile0;   // VK_DICT / VK_RLE_BOOL with a run scan: the page's first entry of the tile tables
 };
 
-struct ChunkDesc {       // 192 B
+struct ChunkDesc {       // 480 B (static_assert below; copied to the device as is)
   int32_t type, type_length, max_def, max_rep;
   int32_t def_bw, rep_bw, value_width, flags;
   uint32_t first_page, num_pages;
@@ -132,7 +132,9 @@ struct ChunkDesc {       // 192 B
   uint8_t group_def[8], group_depth[8];
   uint64_t group_validity[8];
   uint64_t nest_masks;            // device u32 [nest_ntiles][nest_nmask][256]: a thread's 32 slots per mask
+                                  // (two-pass nested mode only; 0 with k_nest_tile)
 };
+static_assert(sizeof(ChunkDesc) == 480, "ChunkDesc layout: host and device share it byte for byte");
 
 // Chunk flags
 enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8,

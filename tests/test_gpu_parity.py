@@ -191,3 +191,51 @@ def test_repeated_decode_with_failed_byte_array_chunk(gpu_ctx, route, monkeypatc
         assert e is not None and (e.code, e.page) == (orc[0][2].code, orc[0][2].page)
         pqtest.assert_chunk_equal(b.result(ids[1]), orc[1][2], "good chunk")
     b.close()
+
+
+def _cfg2_delta_corrupt(page=2):
+    """cfg2_v2_small with the first miniblock width of column a's DELTA page `page` set to 70 (> 64:
+    the reference's init() rejects it, deltabp_decoder.go:101-105)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
+    import pqinspect
+    buf = bytearray(pqtest.load("cfg2_v2_small"))
+    ph, j = list(pqinspect.pages(bytes(buf), 0, 0))[page]
+    assert ph[1] == 3 and ph[8][4] == 5  # DATA_PAGE_V2, DELTA_BINARY_PACKED
+    p = j + ph[8][6] + ph[8][5]  # past the rep and def sections
+    for _ in range(5):  # block size, miniblocks, count, first value, min delta
+        _, p = pqinspect.uvar(buf, p)
+    buf[p] = 70
+    return bytes(buf)
+
+
+@pytest.mark.parametrize("which", ["good", "delta_error", "level_error"])
+def test_back_to_back_delta_major(gpu_ctx, which):
+    """The DELTA-major schedule (host.cpp decode_impl: speculative V2 OPTIONAL DELTA + PLAIN, cfg2's
+    shape) rotates two error-key buffers between consecutive decodes and defers the level stream's
+    join. Three decodes queued back to back, then one sync (the benchmark's pattern), then decode +
+    sync pairs: every chunk equals the oracle each time, and an error in a DELTA page or in a
+    definition-level stream is reported with the reference's (code, page) every time."""
+    data = {"good": lambda: pqtest.load("cfg2_v2_small"), "delta_error": _cfg2_delta_corrupt,
+            "level_error": lambda: pqtest.load("bad_def_empty_run")}[which]()
+    orc = pqtest.oracle_decode(data)
+    bad = [(rg, col, r) for rg, col, r in orc if isinstance(r, O.OracleError)]
+    assert bool(bad) == (which != "good"), bad
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = {(rg, col): b.add_file_chunk(f, rg, col)[0] for rg in range(f.num_row_groups) for col in range(f.num_columns)}
+    for rounds in (3, 1, 1, 2, 1):
+        for _ in range(rounds):
+            b.decode()
+        e = b.sync()
+        assert (e is None) == (not bad), e
+        for rg, col, r in orc:
+            g = b.status(ids[(rg, col)])
+            where = f"{which} x{rounds} rg{rg} col{col}"
+            if isinstance(r, O.OracleError):
+                assert g is not None and (g.code, g.page) == (r.code, r.page), (where, g, r)
+            else:
+                assert g is None, (where, g)
+                pqtest.assert_chunk_equal(b.result(ids[(rg, col)]), r, where)
+    b.close()

@@ -332,3 +332,61 @@ def test_gpu_back_to_back_decodes(gpu_ctx, nest_mode, bad_page):
         if bad_page is None:
             assert e is None, e
     b.close()
+
+
+TORN_SCRIPT = r"""
+import sys
+sys.path[:0] = sys.argv[1:4]
+import numpy as np
+import pqgpu, pqtest, py_oracle as O
+import test_nested as T
+ctx = pqgpu.Context(0)
+torn = over = 0
+for name, data in (("cfg4_small", pqtest.load("cfg4_small")), ("cfg4_v2", pqtest.load("cfg4_v2")),
+                   ("deep1", T._deep_file("1.0")), ("deep2", T._deep_file("2.0"))):
+    of = O.File(data)
+    f, b, ids = T._gpu_nested_all(ctx, data)
+    b.debug_counters(reset=True)
+    for _ in range(2):  # the benchmark's pattern: decodes back to back, then one sync
+        b.decode()
+    assert b.sync() is None, name
+    c = b.debug_counters(reset=True)
+    torn += int(c[20]) & ((1 << 40) - 1)  # (nested.hip: slot 20, the guard's count in bits 40 and up)
+    over += int(c[20]) >> 40
+    for (rg, col), cid in ids.items():
+        r = b.result(cid)
+        o = of.read_chunk(rg, col)
+        pqtest.assert_chunk_equal(r, o, f"torn {name} rg{rg} col{col}")
+        lnd, ld, md = T._levels_of(data, col)
+        want_levels, want_elem = T.nested_ref(o.rep_levels, o.def_levels, md, lnd, ld)
+        T._check_nested(r.nested, r.element_validity, want_levels, want_elem, f"torn {name} rg{rg} col{col}")
+    b.close()
+print("TORN", torn, "OVER", over)
+"""
+
+
+@pytest.mark.gpu
+def test_gpu_lookback_torn_publish():
+    """k_nest_tile's look-back with the torn state made certain (diagnostic library, PQ_ABLATE bit 26:
+    every tile publishes its counter words one at a time, in reverse order, ~27 us apart, nested.hip
+    nest_publish). A successor then finds predecessors whose words are partly aggregates and partly
+    inclusive prefixes (counted in debug slot 20) and must read them again rather than sum them: every
+    nested array equals the oracle's on cfg4_small, cfg4_v2 and the two-list-level documents, and the
+    prefix guard (a prefix past the chunk's slots; slot 20's high bits) never fires."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "parquet-go-1_amd", "lib", "libpqgpu_diag.so")
+    assert os.path.exists(diag), "make -C parquet-go-1_amd diag"
+    env = dict(os.environ, PQGPU_LIB=diag, PQ_ABLATE=str(1 << 26), PQ_DEBUG_STAMPS="1", PQ_NEST_FUSED="1",
+               PQ_NEST_TCOUNT="0")
+    tests = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", TORN_SCRIPT, tests, os.path.join(root, "parquet-go-1_amd"),
+                        os.path.join(root, "oracle")], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("TORN")][-1].split()
+    torn, over = int(line[1]), int(line[3])
+    print(f"torn predecessors re-read: {torn}, guard fired: {over}")
+    assert torn > 0, "the injection produced no torn state: the test would prove nothing"
+    assert over == 0
