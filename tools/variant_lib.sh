@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build lib/libpqgpu_<name>.so: kernels.hip (and bytearray.hip) compiled with extra -D flags,
-# linked with the other objects of the default build (for tools/r03_libs.sh; experiments only).
+# linked with the other objects of the default build (A/B runs of kernel variants in one session; experiments only).
 set -e
 name=$1; shift
 cd "$(dirname "$0")/../parquet-go-1_amd"
