@@ -1408,46 +1408,67 @@ __global__ void __launch_bounds__(64) k_levels_bw1w(BatchDev b_in, const uint32_
 // page, by verified speculation over stream segments (no workgroup barrier, no list ranking).
 //
 // The run-header chain is serial: run k+1 starts where run k ends. The stream (staged in LDS) is
-// cut into 64 segments [lo_i, hi_i), one per lane. Lane i starts kSgMargin bytes before its
+// cut into 64 segments [lo_i, hi_i), one per lane. Lane i starts kSg1Margin bytes before its
 // segment at an arbitrary byte and walks run headers speculatively (a header that is not a
-// well-formed run, or one that would jump more than kSgCap bytes, moves it one byte on); a chain
-// started anywhere joins the true chain within a few runs (measured on pyarrow's def-level
-// streams: 99.5 % within 128 bytes, 99.997 % within 256, once jumps are capped — garbage varints
-// otherwise jump kilobytes and never rejoin). Its first position at or past lo_i is its ENTRY;
-// from there it walks exactly (every fast run is taken, whatever its length) up to the first
-// position at or past hi_i, its EXIT, counting the values of the runs it passed.
+// well-formed run, or one that would jump more than kSg1Cap bytes, moves it one byte on); a chain
+// started anywhere joins the true chain within a few runs. Measured offline on pyarrow's def-level
+// streams (tools/sim_level_join.py): with hops capped at 16 bytes 99.6 % of the lanes of a 10 %-null
+// stream are on the true chain before their segment starts, from 48 bytes ahead (round 5's 72-byte
+// cap needed 128 bytes for 98.8 %: a garbage walker that takes long bit-packed "runs" out of payload
+// bytes rarely lands back on the chain, one that steps byte by byte does). Its first position at or
+// past lo_i is its ENTRY; from there it walks exactly (every fast run is taken, whatever its length)
+// up to the first position at or past hi_i, its EXIT, counting the values of the runs it passed.
 // Verification is exact: lane 0 starts at stream position 0; lane i's chain IS the true chain from
 // its entry on iff entry_i == exit_(i-1) and lane i-1 is verified (chains are deterministic
 // functions of a position). The first lane that fails (or stopped at a header the fast decoder does
-// not take: a varint over 4 bytes, a run cut by EOF, an error) is re-walked from its predecessor's
+// not take: a varint over 2 bytes, a run cut by EOF, an error) is re-walked from its predecessor's
 // exit with the reference's full header semantics (decode_hdr), uniformly by the wave; then the
 // next one, in lane order. A long run that jumps over whole segments leaves them empty.
 // Then a wave scan of the lanes' value counts gives every run its first value index, and each lane
-// walks its verified range again and writes its values' validity bits straight to the chunk bitmap
-// (pre-zeroed every decode): a lane's values are one contiguous bit range, assembled in a 64-bit
-// register accumulator; words inside the range are plain stores, the range's first and last words
-// (shared with the neighbouring lanes or pages) atomic ORs; null runs only move the cursor. Runs of
-// more than kSgLong values go to the whole wave. Runs past the one that reaches num_values are never
-// read; an error is the page's only if the reference's next() meets it before num_values (same
+// walks its verified range again and writes its values' validity bits into the page's bitmap image
+// in LDS: a lane's values are one contiguous bit range, assembled in a 64-bit register accumulator;
+// words inside the range are plain LDS stores, the range's first and last words (shared with the
+// neighbouring lanes) LDS atomic ORs; null runs only move the cursor. Runs of more than kSgLong values
+// go to the whole wave. The image is then stored to the chunk bitmap with coalesced stores (atomic OR
+// only for the page's two edge words, which the neighbouring pages share; slots past the image's
+// kSg1Words words go to the chunk bitmap directly). Runs past the one that reaches num_values are
+// never read; an error is the page's only if the reference's next() meets it before num_values (same
 // class, same value position as decodePackedArray), and a failing page writes nothing.
+// Round 6: the hop reads 4 bytes and decodes 1- and 2-byte varints only (the longer ones stop the
+// lane for the exact re-walk, or take the general decoder on a verified range), the speculative hops
+// are capped at 16 bytes, and the bitmap is assembled in LDS: round 5's loop spent ~23 K issued
+// instructions per page beside the DELTA launch, and its scattered per-lane global stores moved 1.6x
+// the bitmap's bytes.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSgStage = kSgStageHost;  // LDS stage; pages whose stream does not fit take k_levels_bw1
 constexpr uint32_t kSgSlack = 128;    // zero bytes after the stage (reads of lanes past their range)
-constexpr uint32_t kSgMargin = 128;   // bytes a lane walks speculatively before its segment
-constexpr uint32_t kSgCap = 72;       // a speculative hop longer than this is not taken
+constexpr uint32_t kSgMargin = 128;   // k_levels_segw: bytes a lane walks speculatively before its segment
+constexpr uint32_t kSgCap = 72;       // k_levels_segw: a speculative hop longer than this is not taken
+constexpr uint32_t kSg1Margin = 48;   // k_levels_seg: the same two for bit width 1 streams
+constexpr uint32_t kSg1Cap = 16;
 constexpr uint32_t kSgLong = 1024;    // runs of more values (not null runs) expand with the whole wave
 constexpr uint32_t kSgQueue = 64;
+constexpr uint32_t kSg1Words = 2056;  // bitmap image: page bits [slot_base & ~31, + 32 * kSg1Words)
+constexpr uint32_t kSg1Image = 2124;  // image words with one pad word per 32 (sg1_sw), a multiple of 4
 enum : uint32_t { SG_OK = 0, SG_STOP = 1, SG_ERR = 2, SG_TRUNC = 3 };
 struct LevelSegLDS {
   uint32_t stage[(kSgStage + kSgSlack) / 4];  // stream bytes from the 16-B aligned address below s
-  uint32_t qg[kSgQueue], qc[kSgQueue], qv[kSgQueue], nq;  // long runs: first value, count, bp | payload / 1
+  uint32_t bm[kSg1Image];                     // the page's bitmap image (word w at sg1_sw(w))
+  uint32_t qg[kSgQueue], qc[kSgQueue], qv[kSgQueue], nq;  // long runs: first bit, count, bp | payload / 1
 };
+// Image word w at w + w / 32: the lanes' current words are ~32 words apart (1,024 values each), which
+// would put every lane of a store on one bank.
+DEV uint32_t sg1_sw(uint32_t w) { return w + (w >> 5); }
 
 // Bytes [p, p + 8) of the staged stream (stage byte o = stream byte o - sa; zero past the stream).
 DEV uint64_t sg_bytes8(const uint32_t *stage, uint32_t o) {
   const uint32_t a = o >> 2, sh = o & 3;
   const uint32_t w0 = stage[a], w1 = stage[a + 1], w2 = stage[a + 2];
   return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+DEV uint32_t sg_bytes4(const uint32_t *stage, uint32_t o) {
+  const uint32_t a = o >> 2;
+  return __builtin_amdgcn_alignbyte(stage[a + 1], stage[a], o & 3);
 }
 
 // The fast form of the header whose 8 bytes are x, at stream position p (bit width 1): a varint of
@@ -1472,30 +1493,43 @@ DEV SgHop sg_decode(uint64_t x, uint32_t p, uint32_t n) {
   r.L = L;
   return r;
 }
+// The same for varints of 1 or 2 bytes (runs of fewer than 8,192 values or groups) from the 4 bytes
+// x at p: the hop of k_levels_seg's walks. adv == 0: not taken here (sg_decode / decode_hdr).
+// Branch-free (bitwise flags, selects): it is the body of the walk loops.
+DEV SgHop sg_fast(uint32_t x, uint32_t p, uint32_t n) {
+  const uint32_t two = (x >> 7) & 1u;  // a second varint byte
+  const uint32_t h = (x & 0x7fu) | ((x >> 1) & (0x3f80u & (0u - two)));
+  const uint32_t L = 1u + two;
+  const uint32_t cnt = h >> 1, bp = h & 1u;
+  const uint32_t adv = L + (bp ? cnt : 1u);
+  const uint32_t v = __builtin_amdgcn_ubfe(x, 8u + 8u * two, 8u);  // RLE value byte
+  const uint32_t ok = (((x >> 15) & two) ^ 1u) & (uint32_t)(cnt != 0) & (uint32_t)(p + adv <= n) &
+                      (bp | (uint32_t)(v <= 1u));
+  SgHop r;
+  r.adv = ok ? adv : 0u;
+  r.nv = bp ? cnt << 3 : cnt;
+  r.bp = bp;
+  r.val = bp ? p + L : v;
+  r.L = L;
+  return r;
+}
 
-// A lane's validity bits, in value order, into the chunk bitmap `vb` (pre-zeroed): bits gather in
-// a 64-bit accumulator; a finished word is stored plainly unless it is the first word of a range
-// (shared with whoever wrote the bits before it: atomic OR); the last, unfinished word is OR-ed.
-struct SgOut {
-  uint32_t *vb;
+// A lane's validity bits, in value order, into the page's bitmap image (LDS, pre-zeroed; words past
+// the image: the chunk bitmap, pre-zeroed every decode): bits gather in a 64-bit accumulator and
+// every finished or last word is OR-ed in (the first and last words of a lane's range are shared
+// with the neighbouring lanes; on the zeroed image an OR is the store for the others).
+struct SgBits {
+  uint32_t *bm;  // LDS image
+  uint32_t *vb;  // chunk bitmap from the image's word 0
   uint64_t acc;
-  uint32_t W, o;  // word of the accumulator's bit 0, bits in use
-  bool first;
-  uint32_t ones;
+  uint32_t w, o, ones;  // word of the accumulator's bit 0, bits in use, ones written
   bool nostore;  // diagnostic build: PQ_ABLATE bit 20 (no bitmap stores)
-  DEV void start(uint64_t g) { W = (uint32_t)(g >> 5); o = (uint32_t)(g & 31); acc = 0; first = true; }
+  DEV void start(uint32_t g) { w = g >> 5; o = g & 31; acc = 0; }
   DEV void put(uint32_t x) {
-    if (!nostore) {
-      if (first) { if (x) atomicOr(&vb[W], x); }
-      else vb[W] = x;
+    if (x && !nostore) {
+      if (w < kSg1Words) atomicOr(&bm[sg1_sw(w)], x);
+      else atomicOr(&vb[w], x);
     }
-    first = false;
-  }
-  DEV void app(uint32_t x, uint32_t k) {  // k <= 32 bits (x has no bits above k)
-    ones += __popc(x);
-    acc |= (uint64_t)x << o;
-    o += k;
-    if (o >= 32) { put((uint32_t)acc); acc >>= 32; W++; o -= 32; }
   }
   DEV void step(uint32_t x, uint32_t k) {  // k values, bits x (x == 0 whenever k > 32)
     ones += __popc(x);
@@ -1504,35 +1538,36 @@ struct SgOut {
     if (t >= 32) {  // (t >= 64 only for nulls: acc >> 32 is then 0 and the words between stay zero)
       put((uint32_t)acc);
       acc >>= 32;
-      W += t >> 5;
+      w += t >> 5;
     }
     o = t & 31;
   }
   DEV void end() {  // the range's last word, shared with whoever writes the bits after it
-    if (o && acc && !nostore) atomicOr(&vb[W], (uint32_t)acc);
+    if (o) put((uint32_t)acc);
     o = 0;
   }
 };
 
-// One long run (values [g, g + c) of the chunk bitmap) by the whole wave: output word w takes run
-// bits [32 w - g, +32); words inside the run are plain stores, the two edge words atomic ORs.
-// Returns this lane's count of ones.
-DEV uint32_t sg_run_wave(uint32_t *vb, const uint32_t *stage, uint32_t sa, uint64_t g, uint32_t c, bool bp,
-                         uint32_t pay) {
+// One long run (image bits [g, g + c)) by the whole wave: image word w takes run bits [32 w - g, +32),
+// OR-ed in (the edge words are shared). Returns this lane's ones.
+DEV uint32_t sg1_run_wave(LevelSegLDS &L, uint32_t *vb, uint32_t sa, uint32_t g, uint32_t c, bool bp,
+                          uint32_t pay) {
   const uint32_t lane = lane_id();
-  const uint64_t w0 = g >> 5, w1 = (g + c - 1) >> 5;
+  const uint32_t w0 = g >> 5, w1 = (g + c - 1) >> 5;
   uint32_t ones = 0;
-  for (uint64_t w = w0 + lane; w <= w1; w += 64) {
-    const int64_t r = (int64_t)(w * 32) - (int64_t)g;  // run bit at the word's bit 0 (negative: first word)
-    const uint32_t lo = r < 0 ? (uint32_t)(-r) : 0u;    // word bits before the run
-    const uint64_t rb = r > 0 ? (uint64_t)r : 0u;       // the word's first run bit
-    const uint32_t nb = (uint32_t)min<uint64_t>(32 - lo, (uint64_t)c - rb);
-    uint32_t x = bp ? (uint32_t)(sg_bytes8(stage, pay + sa + (uint32_t)(rb >> 3)) >> (rb & 7)) : ~0u;
+  for (uint32_t w = w0 + lane; w <= w1; w += 64) {
+    const int32_t r = (int32_t)(w * 32) - (int32_t)g;  // run bit at the word's bit 0 (negative: first word)
+    const uint32_t lo = r < 0 ? (uint32_t)(-r) : 0u;   // word bits before the run
+    const uint32_t rb = r > 0 ? (uint32_t)r : 0u;      // the word's first run bit
+    const uint32_t nb = min(32u - lo, c - rb);
+    uint32_t x = bp ? (uint32_t)(sg_bytes8(L.stage, pay + sa + (rb >> 3)) >> (rb & 7)) : ~0u;
     x &= nb == 32 ? ~0u : ((1u << nb) - 1u);
     x <<= lo;
     ones += __popc(x);
-    if (lo || nb + lo < 32) { if (x) atomicOr(&vb[w], x); }
-    else vb[w] = x;
+    if (x) {
+      if (w < kSg1Words) atomicOr(&L.bm[sg1_sw(w)], x);
+      else atomicOr(&vb[w], x);
+    }
   }
   return ones;
 }
@@ -1542,14 +1577,15 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
   const PageDesc pd = b.pages[pi];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t ns = pd.num_slots;
-  uint32_t *vbits = gp_u64<uint32_t>(cd.validity);
+  const uint32_t o0 = (uint32_t)(pd.slot_base & 31u);                        // image bit of the page's slot 0
+  uint32_t *vbw = gp_u64<uint32_t>(cd.validity) + (uint32_t)(pd.slot_base >> 5);  // chunk word of image word 0
   const uint8_t *s = gp_u64<const uint8_t>(pd.data) + pd.def_off;
   const uint32_t n = pd.def_len;  // n + 24 <= kSgStage (host)
-  // diagnostic build: 0 stage, 1 A, 2 B, 3 C+D; 5 B iterations, 6 A steps, 7 D steps
+  // diagnostic build: 0 stage, 1 A, 2 B, 3 C+D, 4 image store; 5 B iterations, 6 A steps, 7 D steps
   PQ_STAMPS(stp, b.dbg);
   stp.begin();
   // ---- stage: the stream from the 16-B aligned address at or below s, zero at and past its end
-  // (a short final group zero-fills; lanes past their range read zeros)
+  // (a short final group zero-fills; lanes past their range read zeros); the image zeroed
   const uint32_t sa = (uint32_t)((uintptr_t)s & 15u);
   {
     const uint4 *g = (const uint4 *)(s - sa);
@@ -1572,6 +1608,8 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
       }
       *(uint4 *)&L.stage[4 * k] = x;
     }
+    const uint32_t nimg = min(sg1_sw(min((o0 + ns + 31) >> 5, kSg1Words)) + 1, kSg1Image);
+    for (uint32_t k = lane; 4 * k < nimg; k += 64) *(uint4 *)&L.bm[4 * k] = make_uint4(0u, 0u, 0u, 0u);
     if (lane == 0) L.nq = 0;
   }
   uint32_t err_pos = 0, err = 0, ones = 0;
@@ -1584,38 +1622,30 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
     if (ns) err = PQ_ERR_INVALID;  // "reader is not initialized"
   } else if (ns) {
     // ---- A. speculative walks: segment [lo, hi) of lane i (branch-free body: every lane runs the
-    // same instructions; a lane past its range only reads)
+    // same instructions; a lane past its range only reads). A lane that starts at stream position 0
+    // is on the chain from the start: its hops are not capped and a header it cannot take stops it.
     const uint32_t S = max((n + 63) / 64, 16u);
     const uint32_t lo = lane * S, hi = lo + S;
     const uint32_t lim = lo < n ? min(hi, n) : 0u;
-    uint32_t p = (lane == 0 || lo <= kSgMargin || lo >= n) ? 0u : lo - kSgMargin;
+    uint32_t p = (lane == 0 || lo <= kSg1Margin || lo >= n) ? 0u : lo - kSg1Margin;
+    const uint32_t from0 = (uint32_t)(p == 0);
     uint32_t entry = lo < n ? (p >= lo ? p : ~0u) : n, cnt = 0, st = SG_OK;
     for (;;) {
       const bool act = st == SG_OK && p < lim;
       if (!__ballot(act)) break;
       stp.count(6);
-      // up to two hops per 8-byte read: the second header is decoded from the same bytes when the
-      // first run took at most 3 of them (5 left: a 4-byte varint and an RLE value byte)
-      const uint64_t x = sg_bytes8(L.stage, p + sa);
-      const SgHop h = sg_decode(x, p, n);
-      const bool spec = p < lo;
-      const bool take = h.adv != 0 && (!spec || h.adv <= kSgCap);
-      const uint32_t np = take ? p + h.adv : p + 1u;  // (a stop does not move: st ends the walk)
-      const SgHop h2 = sg_decode(x >> (8 * min(h.adv, 3u)), np, n);
-      const bool spec2 = np < lo;
-      const bool take2 = take && h.adv <= 3 && np < lim && h2.adv != 0 && (!spec2 || h2.adv <= kSgCap);
-      const uint32_t np2 = take2 ? np + h2.adv : np;
-      if (act && !spec) {
-        cnt += take ? h.nv : 0u;
-        st = take ? SG_OK : SG_STOP;
-      }
-      if (act && take2 && !spec2) cnt += h2.nv;
-      if (act && spec && np >= lo) entry = np;
-      if (act && take2 && spec2 && np2 >= lo) entry = np2;
-      if (act && (take || spec)) p = np2;
+      const SgHop h = sg_fast(sg_bytes4(L.stage, p + sa), p, n);
+      const uint32_t spec = (uint32_t)(p < lo), exact = (spec ^ 1u) | from0, a = (uint32_t)act;
+      const uint32_t take = (uint32_t)(h.adv != 0) & (exact | (uint32_t)(h.adv <= kSg1Cap));
+      const uint32_t np = take ? p + h.adv : p + 1u;
+      const uint32_t stop = a & exact & (take ^ 1u);  // (a stop does not move: st ends the walk)
+      cnt += (a & (spec ^ 1u) & take) ? h.nv : 0u;
+      entry = (a & spec & (uint32_t)(np >= lo)) ? np : entry;
+      p = (a & (stop ^ 1u)) ? np : p;
+      st = stop ? SG_STOP : st;
     }
     uint32_t exit = lo < n ? p : n;
-    if (lo < n && entry == ~0u) entry = p;  // (cannot stay unset: the loop runs until p >= lo)
+    if (lo < n && entry == ~0u) entry = p;  // (a lane from 0 that stopped before its segment: fails B)
     stp.lap(1);
     // ---- B. verification in lane order; the first failing lane is re-walked exactly from its
     // predecessor's (verified) exit, uniformly by the wave
@@ -1686,59 +1716,61 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
         err = PQ_ERR_EOF;
       }
     }
-    // ---- D. every verified lane writes its values' validity bits (a failing page writes nothing).
-    // One uniform step per iteration: a lane whose run is spent takes the next header, then every
-    // lane appends up to 32 values of its run (a null run all at once: the cursor moves), so the
-    // wave runs one short path instead of the union of a per-run-kind branch chain (round 4's loop
-    // spent ~4,700 cycles per step in it: 74 % of the kernel, tools/diag.py seg_CD).
+    // ---- D. every verified lane writes its values' validity bits into the image (a failing page
+    // writes nothing). One uniform step per iteration: a lane whose run is spent takes the next
+    // header, then every lane appends up to 32 values of its run (a null run all at once: the
+    // cursor moves), so the wave runs one short path instead of a per-run-kind branch chain.
     if (!err && !PQ_ABLATE(b, 21)) {  // (diagnostic: bit 21 skips D)
       uint32_t P = entry, v = base;
       const bool mine = cnt > 0 && base < need;
       const uint32_t vend = min(base + cnt, need);
-      SgOut out;
-      out.vb = vbits;
+      SgBits out;
+      out.bm = L.bm;
+      out.vb = vbw;
       out.ones = 0;
       out.nostore = PQ_ABLATE(b, 20);
-      out.start(pd.slot_base + base);
-      uint32_t rem = 0, rpay = 0;  // the current run: values left, next payload bit (stage bits)
-      bool rbits = false, rone = false;  // bit-packed / RLE of ones (else RLE of nulls)
+      out.start(o0 + base);
+      uint32_t rem = 0, rpay = 0, kind = 0;  // the current run: values left, next payload byte (stage),
+                                             // 0 nulls / 1 ones / 2 bit-packed
       for (;;) {
         const bool act = mine && (rem || (P < exit && v < vend));
         if (!__ballot(act)) break;
         stp.count(7);
         if (act && !rem) {
-          SgHop h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
-          if (!h.adv) {  // a run decode_hdr took in B (the only kind left on a verified range)
-            const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
-            h.adv = eh.adv;
-            h.nv = eh.nvals;
-            h.bp = eh.bp;
-            h.val = eh.value;
+          SgHop h = sg_fast(sg_bytes4(L.stage, P + sa), P, n);
+          if (!h.adv) {  // a longer varint, or a run decode_hdr took in B
+            h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
+            if (!h.adv) {
+              const Hdr eh = decode_hdr(s4, 0u - sa4, s, P, n, 1, 1);
+              h.adv = eh.adv;
+              h.nv = eh.nvals;
+              h.bp = eh.bp;
+              h.val = eh.value;
+            }
           }
           rem = min(h.nv, vend - v);
-          rbits = h.bp != 0;
-          rone = !h.bp && h.val;
-          rpay = 8 * (h.val + sa);
+          kind = h.bp ? 2u : (h.val ? 1u : 0u);
+          rpay = h.val + sa;
           P += h.adv;
-          if (rem > kSgLong && (rbits || rone)) {  // long: the whole wave (the accumulator restarts after it)
+          if (rem > kSgLong && kind) {  // long: the whole wave (the accumulator restarts after it)
             const uint32_t q = atomicAdd(&L.nq, 1u);
             if (q < kSgQueue) {
               out.end();
-              L.qg[q] = v;
+              L.qg[q] = o0 + v;
               L.qc[q] = rem;
-              L.qv[q] = rbits ? 0x80000000u | h.val : 1u;
+              L.qv[q] = kind == 2 ? 0x80000000u | h.val : 1u;
               v += rem;
-              out.start(pd.slot_base + v);
+              out.start(o0 + v);
               rem = 0;
             }
           }
         }
         if (act && rem) {
-          const uint32_t k = (rbits || rone) ? min(rem, 32u) : rem;
+          const uint32_t k = kind ? min(rem, 32u) : rem;
           const uint32_t m = k >= 32 ? ~0u : ((1u << k) - 1u);
-          const uint32_t x = rbits ? (uint32_t)(sg_bytes8(L.stage, rpay >> 3) >> (rpay & 7)) & m : rone ? m : 0u;
+          const uint32_t x = kind == 2 ? sg_bytes4(L.stage, rpay) & m : (kind ? m : 0u);
           out.step(x, k);
-          rpay += k;
+          rpay += 4;
           rem -= k;
           v += k;
         }
@@ -1749,7 +1781,7 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
         uint32_t c = min(min(eh.okvals, eh.nvals), need - v), pay = eh.value;
         for (uint32_t q = 0; q < c; q += 32, pay += 4) {
           const uint32_t k = min(32u, c - q);
-          out.app((uint32_t)sg_bytes8(L.stage, pay + sa) & (k == 32 ? ~0u : ((1u << k) - 1u)), k);
+          out.step(sg_bytes4(L.stage, pay + sa) & (k == 32 ? ~0u : ((1u << k) - 1u)), k);
         }
       }
       if (mine) out.end();
@@ -1758,10 +1790,24 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
       const uint32_t nq = min(L.nq, kSgQueue);
       for (uint32_t q = 0; q < nq; q++) {
         const uint32_t qv = L.qv[q];
-        ones += sg_run_wave(vbits, L.stage, sa, pd.slot_base + L.qg[q], L.qc[q], (qv >> 31) != 0, qv & 0x7fffffffu);
+        ones += sg1_run_wave(L, vbw, sa, L.qg[q], L.qc[q], (qv >> 31) != 0, qv & 0x7fffffffu);
       }
+      stp.lap(3);
+      // ---- the image to the chunk bitmap: coalesced word stores, atomic OR for the page's edge words
+      wave_lds_sync();
+      if (!PQ_ABLATE(b, 20)) {
+        const uint32_t nw = (o0 + ns + 31) >> 5, nl = min(nw, kSg1Words);
+        const bool edge_hi = ((o0 + ns) & 31u) != 0;
+        for (uint32_t w = lane; w < nl; w += 64) {
+          const uint32_t x = L.bm[sg1_sw(w)];
+          if ((w == 0 && o0) || (w == nw - 1 && edge_hi)) { if (x) atomicOr(&vbw[w], x); }
+          else vbw[w] = x;
+        }
+      }
+      stp.lap(4);
+    } else {
+      stp.lap(3);
     }
-    stp.lap(3);
   }
   const uint32_t cntv = (uint32_t)wave_sum64(ones);
   if (lane == 0) {
@@ -1777,11 +1823,15 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
 
 // One wavefront walks pages k, k + gridDim.x, ... of the list: a grid smaller than the page count
 // keeps fewer level waves resident beside the values launch (DELTA-major schedule), each for longer.
+// The LDS is dynamic (sizeof(LevelSegLDS) at launch): with a static size the compiler sizes the
+// register allocation to the occupancy the LDS allows (176 VGPRs for 64 used), and each of those
+// registers is one the DELTA launch beside it cannot have.
 __global__ void __launch_bounds__(64) k_levels_seg(BatchDev b_in, const uint32_t *pages, uint32_t npages) {
   const BatchDev b = global_view(b_in);
-  __shared__ LevelSegLDS L;
+  extern __shared__ uint4 sg_dyn_lds[];
+  LevelSegLDS &L = *reinterpret_cast<LevelSegLDS *>(sg_dyn_lds);
   for (uint32_t k = blockIdx.x; k < npages; k += gridDim.x) {
-    wave_lds_sync();  // (the previous page's stage reads are done)
+    wave_lds_sync();  // (the previous page's stage and image reads are done)
     levels_seg_page(b, L, pages[k]);
   }
 }
@@ -2616,17 +2666,22 @@ DEV uint32_t plain_err(uint64_t have, uint32_t w) { return (have % w) == 0 ? PQ_
 template <uint32_t U = 0>
 DEV void do_plain(const BatchDev &b, const WorkItem &wi, const PageDesc &pd, const ChunkDesc &cd, uint32_t nn) {
   const uint32_t w = (uint32_t)cd.value_width;
-  uint32_t v1 = min(wi.v1, nn);
-  if (wi.v0 >= v1) return;
+  const uint64_t vb = b.page_vbase[wi.page];
+  // the tiles' inner boundaries moved to 16-B aligned destination bytes (4- and 8-byte values): a
+  // boundary line written half by each of two workgroups costs a partial-line write each
+  const uint32_t a = w == 8 ? (uint32_t)(vb & 1u) : (w == 4 ? (uint32_t)((4u - (uint32_t)(vb & 3u)) & 3u) : 0u);
+  const uint32_t v0 = wi.v0 ? wi.v0 + a : 0u;
+  uint32_t v1 = min(wi.v1 + a, nn);
+  if (v0 >= v1) return;
   const uint64_t have = pd.val_len;
   uint64_t fit = have / w;  // values that fit
   uint32_t e1 = (uint32_t)min((uint64_t)v1, fit);
   if (e1 < v1 && threadIdx.x == 0) report(b, pd.chunk, 1, pd.page_in_chunk, ST_VALUES, (uint32_t)fit, plain_err(have, w));
-  if (e1 <= wi.v0) return;
-  const uint8_t *src = gp_u64<const uint8_t>(pd.data) + pd.val_off + (uint64_t)wi.v0 * w;
-  uint8_t *dst = gp_u64<uint8_t>(cd.values) + (b.page_vbase[wi.page] + wi.v0) * w;
-  if constexpr (U == 0) copy_bytes(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
-  else copy_bytes_u<U>(dst, src, (uint64_t)(e1 - wi.v0) * w, threadIdx.x, blockDim.x);
+  if (e1 <= v0) return;
+  const uint8_t *src = gp_u64<const uint8_t>(pd.data) + pd.val_off + (uint64_t)v0 * w;
+  uint8_t *dst = gp_u64<uint8_t>(cd.values) + (vb + v0) * w;
+  if constexpr (U == 0) copy_bytes(dst, src, (uint64_t)(e1 - v0) * w, threadIdx.x, blockDim.x);
+  else copy_bytes_u<U>(dst, src, (uint64_t)(e1 - v0) * w, threadIdx.x, blockDim.x);
 }
 
 // BOOLEAN PLAIN (type_boolean.go:46-69): bit i of byte i/8, LSB first, one byte read per 8 values.
@@ -3865,7 +3920,7 @@ __global__ void __launch_bounds__(256) k_values_copy(BatchDev b_in, const WorkIt
   const PageDesc &pd = b.pages[wi.page];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t nn = b.page_nn_v[wi.page];
-  if (wi.kind == WI_PLAIN) do_plain(b, wi, pd, cd, nn);
+  if (wi.kind == WI_PLAIN) do_plain<4>(b, wi, pd, cd, nn);  // (copy_shapes ubench: 4 pieces per lane, nt)
   else do_bool(b, wi, pd, cd, nn);
 }
 
@@ -4636,7 +4691,7 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s,
       const uint32_t nseg = l.n_level_pages_seg, nrest = l.n_level_pages_bw1 - nseg;
       const char *sg = getenv("PQ_SEG_GRID");  // (probe) wavefronts of k_levels_seg; 0: one per page
       const uint32_t want = sg && atoi(sg) > 0 ? (uint32_t)atoi(sg) : nseg, grid = want < nseg ? want : nseg;
-      if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(grid), dim3(64), 0, s, b, l.level_pages_bw1, nseg);
+      if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(grid), dim3(64), sizeof(LevelSegLDS), s, b, l.level_pages_bw1, nseg);
       if (nrest) hipLaunchKernelGGL(k_levels_bw1, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages_bw1 + nseg);
     }
   }

@@ -35,7 +35,7 @@ names = ["stage", "P1_links", "P2_doubling", "P3_ckp", "P4_walkers", "P5_P6", "t
 for k, n in enumerate(names):
     v = int(d[k])
     print(f"levels {n:12s} total {v:>14d}  per page(wave) {v / pages / 4:>12.1f}")
-for k, nm in enumerate(["seg_stage", "seg_A", "seg_B", "seg_CD", "seg_flush", "seg_B_iters", "seg_A_steps", "seg_D_steps"]):
+for k, nm in enumerate(["seg_stage", "seg_A", "seg_B", "seg_CD", "seg_store", "seg_B_iters", "seg_A_steps", "seg_D_steps"]):
     v = int(d[16 + k])
     print(f"levels {nm:12s} total {v:>14d}  per page(wave) {v / pages:>12.1f}")
 for k, nm in enumerate(["w_first", "w_fetch_issue", "w_walk", "w_bar1", "w_store", "w_bar2", "w_reloads#", "w_windows#"]):

@@ -1,7 +1,10 @@
 """Offline measurement behind k_levels_seg's speculative join: on cfg2's pyarrow
 definition-level streams (bit width 1), how far does a run-header walk started at an arbitrary byte
 go before it lands on a position of the true chain? A well-formed fast run moves the walk by its
-length if that is at most `cap` bytes, anything else by one byte. CPU only.
+length if that is at most `cap` bytes, anything else by one byte. Second table: k_levels_seg's lanes
+(64 segments per page, each lane's walk from `margin` bytes before its segment with hops capped at
+`cap` bytes): the share of lanes whose first position at or past their segment start is not the true
+chain's, i.e. that verification sends to the exact re-walk. CPU only.
 
   python tools/sim_level_join.py [pages] [stride]
 """
@@ -77,6 +80,28 @@ def main():
         d = np.array(dist)
         print(f"cap {cap}: {len(d)} starts; not joined within 64 / 128 / 256 bytes: "
               f"{(d > 64).mean():.4%} / {(d > 128).mean():.4%} / {(d > 256).mean():.4%}")
+    ss = streams()[:npages]
+    for margin, cap in ((128, 72), (48, 16), (48, 8), (64, 16), (32, 16)):
+        lanes = fails = hops = 0
+        for s in ss:
+            n, p, true = len(s), 0, []
+            while 0 <= p < n:
+                true.append(p)
+                p = hop(s, p, 1 << 30)
+            S = max((n + 63) // 64, 16)
+            for lane in range(1, 64):
+                lo = lane * S
+                if lo >= n:
+                    break
+                lanes += 1
+                p = 0 if lo <= margin else lo - margin
+                while p < lo:
+                    q = hop(s, p, cap)
+                    p = p + 1 if q < 0 else q
+                    hops += 1
+                fails += p != next((t for t in true if t >= lo), n)
+        print(f"margin {margin} cap {cap}: {lanes} lanes, {fails / lanes:.3%} fail verification, "
+              f"{hops / lanes:.1f} speculative hops per lane")
 
 
 if __name__ == "__main__":

@@ -9,6 +9,9 @@
 //   items_u4   the product copy (copy_bytes_u<4>) over cfg2-shaped work items, misaligned sources
 //   items_p4   a pipelined item copy (next round's loads before this round's stores), misaligned
 //   d2d        hipMemcpyAsync device to device
+//   items_ua*  the item copy with unaligned 16-B loads (global_load_dwordx4 at any byte address; no
+//              funnel shifts or lane shuffles), 16-B aligned stores; _nt: non-temporal; _d8: the
+//              destinations only 8-B aligned as well (unaligned 16-B stores)
 // Build: make -C tools/ubench copy_shapes; run: tools/ubench/copy_shapes
 #include <hip/hip_runtime.h>
 
@@ -156,6 +159,54 @@ __global__ void __launch_bounds__(256) k_items_p4(const Item *items) {
   copy_bytes_p4(gp(it.dst), gp(it.src), it.n, threadIdx.x, 256);
 }
 
+typedef uint32_t ua_v4u32 __attribute__((ext_vector_type(4), aligned(1)));
+template <bool NT>
+DEV uint4 ld_ua(const uint8_t *p) {
+  ua_v4u32 v;
+  if (NT) v = __builtin_nontemporal_load((const ua_v4u32 *)p);
+  else v = *(const ua_v4u32 *)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+DEV void st_ua(uint8_t *p, uint4 v) {
+  const ua_v4u32 x = {v.x, v.y, v.z, v.w};
+  if (NT) __builtin_nontemporal_store(x, (ua_v4u32 *)p);
+  else *(ua_v4u32 *)p = x;
+}
+// dst[0..n) = src[0..n): 16-B pieces of the destination from its first 16-B aligned byte (A16) or its
+// first byte (unaligned stores), four per lane per round, unaligned 16-B loads
+template <bool NT, bool A16>
+DEV void copy_ua(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
+  uint64_t head = A16 ? ((16 - ((uintptr_t)dst & 15)) & 15) : 0;
+  if (head > n) head = n;
+  if (tid < head) dst[tid] = src[tid];
+  const uint64_t pieces = (n - head) >> 4;
+  uint8_t *d = dst + head;
+  const uint8_t *sp = src + head;
+  const uint32_t lane = tid & 63u, wv = tid >> 6;
+  const uint64_t per = (uint64_t)nt * 4;
+  uint64_t r0 = 0;
+  for (; r0 + per <= pieces; r0 += per) {
+    const uint64_t i = r0 + (uint64_t)wv * 256 + lane;
+    uint4 a[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) a[u] = ld_ua<NT>(sp + 16 * (i + 64 * u));
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (A16) st_ua<NT>(d + 16 * (i + 64 * u), a[u]);
+      else st_ua<NT>(d + 16 * (i + 64 * u), a[u]);
+    }
+  }
+  for (uint64_t i = r0 + tid; i < pieces; i += nt) st_ua<NT>(d + 16 * i, ld_ua<NT>(sp + 16 * i));
+  const uint64_t tail = n - head - 16 * pieces;
+  if (tid < tail) d[16 * pieces + tid] = sp[16 * pieces + tid];
+}
+template <bool NT, bool A16>
+__global__ void __launch_bounds__(256) k_items_ua(const Item *items) {
+  const Item it = gp(items)[blockIdx.x];
+  copy_ua<NT, A16>(gp(it.dst), gp(it.src), it.n, threadIdx.x, 256);
+}
+
 int main() {
   const uint32_t pages = 1024, vals = 59000;  // cfg2's DOUBLE column: ~59,000 non-null values per page
   const uint64_t page_bytes = (uint64_t)vals * 8;
@@ -207,8 +258,8 @@ int main() {
   }
   timeit("d2d", [&] { CK(hipMemcpyAsync(dst, src, total, hipMemcpyDeviceToDevice, 0)); });
   Item *ditems;
-  CK(hipMalloc(&ditems, sizeof(Item) * pages * 64));
-  for (uint32_t per : {16384u, 32768u}) {
+  CK(hipMalloc(&ditems, sizeof(Item) * pages * 64));  // (>= 59,000 / 2,048 items per page)
+  for (uint32_t per : {2048u, 4096u, 16384u, 32768u}) {
     std::vector<Item> items;
     for (uint32_t p = 0; p < pages; p++) {
       const uint32_t off = 1024 + (p * 7 + 3) % 16;  // value sections at arbitrary byte alignment
@@ -225,6 +276,30 @@ int main() {
     timeit(nm, [&] { k_items_u4<<<ni, 256>>>(ditems); });
     snprintf(nm, sizeof nm, "items_p4_per%u", per);
     timeit(nm, [&] { k_items_p4<<<ni, 256>>>(ditems); });
+    snprintf(nm, sizeof nm, "items_ua_per%u", per);
+    timeit(nm, [&] { k_items_ua<false, true><<<ni, 256>>>(ditems); });
+    snprintf(nm, sizeof nm, "items_ua_nt_per%u", per);
+    timeit(nm, [&] { k_items_ua<true, true><<<ni, 256>>>(ditems); });
+  }
+  for (uint32_t per : {2048u, 16384u}) {  // destinations 8-B aligned only (as int64 / double outputs at odd bases)
+    std::vector<Item> items;
+    for (uint32_t p = 0; p < pages; p++) {
+      const uint32_t off = 1024 + (p * 7 + 3) % 16;
+      for (uint32_t v0 = 0; v0 < vals; v0 += per) {
+        const uint32_t v1 = std::min(vals, v0 + per);
+        items.push_back({src + p * page_stride + off + (uint64_t)v0 * 8, dst + 8 + (uint64_t)p * page_bytes + (uint64_t)v0 * 8,
+                         (uint64_t)(v1 - v0) * 8});
+      }
+    }
+    CK(hipMemcpy(ditems, items.data(), sizeof(Item) * items.size(), hipMemcpyHostToDevice));
+    const uint32_t ni = (uint32_t)items.size();
+    char nm[96];
+    snprintf(nm, sizeof nm, "items_u4_d8_per%u", per);
+    timeit(nm, [&] { k_items_u4<<<ni, 256>>>(ditems); });
+    snprintf(nm, sizeof nm, "items_ua_nt_d8_per%u", per);
+    timeit(nm, [&] { k_items_ua<true, false><<<ni, 256>>>(ditems); });
+    snprintf(nm, sizeof nm, "items_ua_nt_d8a16_per%u", per);
+    timeit(nm, [&] { k_items_ua<true, true><<<ni, 256>>>(ditems); });
   }
   return 0;
 }
