@@ -289,6 +289,14 @@ DEV void cp_st16(uint4 *p, uint4 v) {
   if (PQ_COPY_NT >= 1) __builtin_nontemporal_store(nt_v4u32{v.x, v.y, v.z, v.w}, (nt_v4u32 *)p);
   else *p = v;
 }
+// The same store at any 4-B aligned address (gfx950 splits an unaligned 16-B store in the memory
+// pipeline; tools/ubench/copy_shapes: 8-B aligned destinations copied at 5.9 TB/s this way against
+// 5.3 TB/s with aligned pieces behind dword head stores)
+typedef uint32_t nt_v4u32_a4 __attribute__((ext_vector_type(4), aligned(4)));
+DEV void cp_st16_ua(uint8_t *p, uint4 v) {
+  if (PQ_COPY_NT >= 1) __builtin_nontemporal_store(nt_v4u32_a4{v.x, v.y, v.z, v.w}, (nt_v4u32_a4 *)p);
+  else *(nt_v4u32_a4 *)p = nt_v4u32_a4{v.x, v.y, v.z, v.w};
+}
 template <uint32_t U>
 DEV void copy_bytes_u(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt) {
   if (n == 0) return;

@@ -236,6 +236,7 @@ struct HostChunk {
   uint32_t dict_len = 0, dict_count = 0;
   // device outputs (offsets into the arena)
   uint64_t o_values = 0, o_def = 0, o_rep = 0, o_valid = 0, o_offsets = 0, o_lists = 0, o_ba_index = 0;
+  bool valid_unzeroed = false;  // the validity bitmap is outside the per-decode zeroed region (k_levels_seg stores all of it)
   // nested (Arrow-style) output: list levels (0: none), per level offsets / validity, elements
   uint32_t nest = 0, nest_tile0 = 0, nest_ntiles = 0, nest_nmask = 0;
   uint64_t o_nest_mask = 0;
@@ -1220,11 +1221,27 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     return o;
   };
   int64_t in_bytes = 0;
-  // Region zeroed before every decode: all validity bitmaps, then per-page record/run counters.
+  // Region zeroed before every decode: the validity bitmaps, then per-page record/run counters.
+  // A flat OPTIONAL chunk whose every page goes to k_levels_seg and covers whole bitmap words (slot
+  // base and count multiples of 32, at most the kernel's LDS image) has every word of its bitmap
+  // stored by that kernel each decode (a page that fails writes nothing, and the chunk reports the
+  // error): its bitmap lies past the region (cfg2: 16 MB less zeroing per decode).
+  const bool lv_seg = !(getenv("PQ_LV_SEG") && atoi(getenv("PQ_LV_SEG")) == 0);
+  auto seg_whole_words = [&](const HostChunk &hc) {
+    if (!lv_seg || hc.err.code || hc.col.max_def != 1 || hc.col.max_rep != 0) return false;
+    for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+      const PageDesc &pd = b->pages[p];
+      if (!(pd.flags & PF_DEF) || (uint64_t)pd.def_len + 24 > kSgStageHost || pd.slot_base % 32 || pd.num_slots % 32 ||
+          pd.num_slots > kSgImageSlotsHost)
+        return false;
+    }
+    return true;
+  };
   b->z_begin = align_up(a, 256);
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
-    hc.o_valid = (!hc.err.code && hc.col.max_def > 0) ? take(((hc.num_slots + 31) / 32 + 2) * 4) : 0;
+    hc.valid_unzeroed = hc.col.max_def > 0 && seg_whole_words(hc);
+    hc.o_valid = (!hc.err.code && hc.col.max_def > 0 && !hc.valid_unzeroed) ? take(((hc.num_slots + 31) / 32 + 2) * 4) : 0;
     // nested output: list validity bitmaps and element validity (OR-ed by k_nest_emit)
     hc.nest = 0;
     if (!hc.err.code && hc.col.max_rep > 0 && hc.col.max_rep <= PQGPU_MAX_NEST) {
@@ -1279,6 +1296,10 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   }
   b->o_nest_state = take(n_nest_tiles * 128);  // one 128-B line per tile (nested.hip kNsStride)
   b->z_end = a;
+  for (uint32_t c = 0; c < nc; c++) {
+    HostChunk &hc = b->chunks[c];
+    if (hc.valid_unzeroed) hc.o_valid = take(((hc.num_slots + 31) / 32 + 2) * 4);
+  }
   for (uint32_t c = 0; c < nc; c++) {
     HostChunk &hc = b->chunks[c];
     if (hc.err.code) continue;
@@ -1379,7 +1400,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       const bool snappy_values = (pd.flags & PF_DEV_SNAPPY) && b->snappy[pd.data].to_values;
       switch (pd.vkind) {
         case VK_PLAIN_FIXED: case VK_PLAIN_INT96:
-          if (!snappy_values) tiles(WI_PLAIN, plain_tile_b ? std::max<uint32_t>(1, plain_tile_b / std::max(1, hc.value_width)) : kPlainTile);
+          if (!snappy_values) tiles(WI_PLAIN, std::max<uint32_t>(1, (plain_tile_b ? plain_tile_b : kPlainTileBytes) / std::max(1, hc.value_width)));
           break;
         case VK_PLAIN_BOOL: tiles(WI_BOOL, kPlainTile); break;
         case VK_DICT: case VK_RLE_BOOL: {
@@ -2044,6 +2065,7 @@ static LaunchLists launch_lists(pqgpu_batch *b) {
   l.level_pages_bw1 = (const uint32_t *)(A + b->l_level_bw1);
   l.n_level_pages_bw1 = (uint32_t)b->level_pages_bw1.size();
   l.n_level_pages_seg = b->n_level_seg;
+  l.seg_grid = 0;
   l.n_level_units_seg = b->n_level_units_seg;
   l.n_level_units_hyb = b->n_level_units_hyb;
   l.lv_tiles = (const uint32_t *)(A + b->l_lv_tiles);
@@ -2324,7 +2346,11 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     // the per-decode state and the level stream's keys: [o_tile_first, o_err_ds end) of the 0xff region
     HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->o_tile_first, b->f_end - b->o_tile_first, ds), err);
-    HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(dl, l, ds); }), err);
+    // k_levels_seg beside the values launch: at most ~4 level waves per CU resident (each walks two
+    // pages or more; cfg2's 2,048 pages: 1,024 waves, step 0.361 -> 0.346 ms; 768 or 1,536: slower)
+    LaunchLists lv = l;
+    lv.seg_grid = l.n_level_pages_seg > 1024 ? std::max<uint32_t>(1024, l.n_level_pages_seg / 2) : 0;
+    HIPCHECK(timed(b, 0, ds, l.n_level_pages + l.n_level_pages_bw1, [&] { return launch_levels(dl, lv, ds); }), err);
     HIPCHECK(timed(b, 15, ds, l.n_lf_list, [&] { return launch_level_fill(dl, l, ds); }), err);
     HIPCHECK(timed(b, 3, ds, l.n_base_chunks, [&] { return launch_bases(dl, l, ds); }), err);
     HIPCHECK(hipEventRecord(b->ev_delta_join, ds), err);

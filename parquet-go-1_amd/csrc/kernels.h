@@ -62,7 +62,12 @@ struct BatchDev {
 
 constexpr uint32_t kDictTile = 4096;   // values per dictionary tile (tile table granularity)
 constexpr uint32_t kNestCnt = 9;       // nested counters per page: lists of levels 1..8, then elements
-constexpr uint32_t kPlainTile = 16384; // values per PLAIN tile
+constexpr uint32_t kPlainTile = 16384; // values per BOOLEAN PLAIN tile
+// bytes per fixed-width PLAIN tile (a workgroup's copy): the copies come out of one round or two
+// of 16-B pieces per lane instead of a loop, and more of them fill the CUs beside the DELTA pages
+// (cfg2 k_values_delta alone 0.306 -> 0.287 ms against 128 KiB tiles; tools/ubench/copy_shapes:
+// 16 KiB items 6.3 TB/s, 128 KiB items 5.0 TB/s)
+constexpr uint32_t kPlainTileBytes = 32768;
 constexpr uint32_t kDictEarlyHost = 4096;  // kernels.hip kDictEarly: dictionaries staged with their tile
 constexpr uint32_t kDictGroupHost = 2;     // kernels.hip kDictGroup: tiles per WI_DICT2 item (at most)
 // The pages whose dictionary tiles may be grouped into WI_DICT2 items: host.cpp groups only these and
@@ -79,6 +84,7 @@ struct LaunchLists {
   const uint32_t *lf_list; uint32_t n_lf_list;           // fill tiles of the non-nested chunks (k_level_fill)
   const uint32_t *level_pages_bw1; uint32_t n_level_pages_bw1;  // flat OPTIONAL pages (max_def 1, no rep)
   uint32_t n_level_pages_seg;  // the first n of them go to k_levels_seg (def stream fits its LDS stage)
+  uint32_t seg_grid;           // k_levels_seg's wavefronts (0: one per page)
   uint32_t n_level_units_seg;  // the first n level_pages units go to k_levels_segw (stream fits its stage)
   uint32_t n_level_units_hyb;  // the next n (repetition streams) to k_levels_hyb, the rest to k_levels
   uint32_t n_ba_delta;                                   // BaDelta entries (one workgroup each)
@@ -109,6 +115,7 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s,
 hipError_t launch_level_fill(const BatchDev &b, const LaunchLists &l, hipStream_t s);  // generic level run tables
 constexpr uint32_t kLfTileHost = 8192;  // k_level_fill tile (kernels.hip kLfTile)
 constexpr uint32_t kSgStageHost = 10240;  // k_levels_seg's LDS stage (kernels.hip kSgStage)
+constexpr uint32_t kSgImageSlotsHost = 65536;  // slots of a 32-aligned page k_levels_seg's bitmap image holds whole
 constexpr uint32_t kSgwStageHost = 57344; // k_levels_segw's LDS stage (kernels.hip kSgwStage)
 hipError_t launch_bases(const BatchDev &b, const LaunchLists &l, hipStream_t s);
 hipError_t launch_scan_runs(const BatchDev &b, const LaunchLists &l, hipStream_t s);

@@ -1449,6 +1449,7 @@ constexpr uint32_t kSg1Cap = 16;
 constexpr uint32_t kSgLong = 1024;    // runs of more values (not null runs) expand with the whole wave
 constexpr uint32_t kSgQueue = 64;
 constexpr uint32_t kSg1Words = 2056;  // bitmap image: page bits [slot_base & ~31, + 32 * kSg1Words)
+static_assert(kSgImageSlotsHost / 32 <= kSg1Words, "host: pages the image holds whole (unzeroed bitmaps)");
 constexpr uint32_t kSg1Image = 2124;  // image words with one pad word per 32 (sg1_sw), a multiple of 4
 enum : uint32_t { SG_OK = 0, SG_STOP = 1, SG_ERR = 2, SG_TRUNC = 3 };
 struct LevelSegLDS {
@@ -3789,19 +3790,9 @@ DEV void do_delta_page(const BatchDev &b, const DeltaStream &ds, uint32_t nn, De
             uint4 *dst = (uint4 *)dst0;
 #pragma unroll
             for (uint32_t q = 0; q < 2; q++) cp_st16(&dst[q * 64 + lane], xw[xsw(q * 64 + lane)]);
-          } else {  // 4-B aligned output: 16-B aligned body pieces from dword LDS reads, dword head/tail
-            const uint32_t bytes = 2048, adj = (16u - (uint32_t)((uintptr_t)dst0 & 15)) & 15u;
-            const uint32_t nbody = (bytes - adj) >> 4, a4 = adj >> 2;
-            const uint32_t *xs = (const uint32_t *)xw;
-            auto xd = [&](uint32_t D) -> uint32_t { return xs[xsw(D >> 2) * 4 + (D & 3)]; };  // dword D
-            uint4 *body = (uint4 *)(dst0 + adj);
-            for (uint32_t j = lane; j < nbody; j += 64) {
-              const uint32_t o = a4 + 4 * j;
-              body[j] = make_uint4(xd(o), xd(o + 1), xd(o + 2), xd(o + 3));
-            }
-            const uint32_t nt = (bytes - adj - 16 * nbody) >> 2;
-            if (lane < a4) ((uint32_t *)dst0)[lane] = xd(lane);
-            if (lane < nt) ((uint32_t *)(dst0 + adj + 16 * nbody))[lane] = xd(a4 + 4 * nbody + lane);
+          } else {  // 4-B aligned output: the same pieces, unaligned 16-B stores
+#pragma unroll
+            for (uint32_t q = 0; q < 2; q++) cp_st16_ua(dst0 + 16u * (q * 64 + lane), xw[xsw(q * 64 + lane)]);
           }
           asm volatile("" ::: "memory");  // this half's LDS reads precede the next half's writes
         }
@@ -4690,7 +4681,8 @@ hipError_t launch_levels(const BatchDev &b, const LaunchLists &l, hipStream_t s,
     } else {
       const uint32_t nseg = l.n_level_pages_seg, nrest = l.n_level_pages_bw1 - nseg;
       const char *sg = getenv("PQ_SEG_GRID");  // (probe) wavefronts of k_levels_seg; 0: one per page
-      const uint32_t want = sg && atoi(sg) > 0 ? (uint32_t)atoi(sg) : nseg, grid = want < nseg ? want : nseg;
+      const uint32_t want = sg && atoi(sg) > 0 ? (uint32_t)atoi(sg) : (l.seg_grid ? l.seg_grid : nseg);
+      const uint32_t grid = want < nseg ? want : nseg;
       if (nseg) hipLaunchKernelGGL(k_levels_seg, dim3(grid), dim3(64), sizeof(LevelSegLDS), s, b, l.level_pages_bw1, nseg);
       if (nrest) hipLaunchKernelGGL(k_levels_bw1, dim3(nrest), dim3(kLvThreads), 0, s, b, l.level_pages_bw1 + nseg);
     }

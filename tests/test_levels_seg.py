@@ -185,12 +185,16 @@ def test_oracle_levels_streams(files):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["seg", "ranking"])
+@pytest.mark.parametrize("kernel", ["seg", "seg_grid1", "ranking"])
 def test_gpu_levels_streams(gpu_ctx, files, monkeypatch, kernel):
+    """seg_grid1: one k_levels_seg wavefront walks every page in turn (a wave's second and later pages
+    reuse its LDS stage and bitmap image)."""
     import pqgpu
     import test_gpu_parity as P
     if kernel == "ranking":
         monkeypatch.setenv("PQ_LV_SEG", "0")
+    if kernel == "seg_grid1":
+        monkeypatch.setenv("PQ_SEG_GRID", "1")
     for name, data in files.items():
         gpu = P._gpu_decode(gpu_ctx, data)
         for rg, col, r in pqtest.oracle_decode(data):

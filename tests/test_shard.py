@@ -138,7 +138,8 @@ def test_strong_two_ranks_decode_parity():
     env = dict(os.environ, PQ_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--config", "cfg5", "--strong", "--total-rgs", "5", "--rg-rows", "20000", "--verify", "--verify-every", "1"]
+           "--gpus", "2", "--config", "cfg5", "--strong", "--total-rgs", "5", "--rg-rows", "20000", "--verify",
+           "--verify-every", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])

@@ -23,6 +23,10 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_LV_SPLIT=0      nested batches' repetition-stream level kernels on the batch stream, not beside
 - PQ_NEST_PCOUNT=1   the nested pages' counts by k_nest_pcount, k_nest_tile beside the values path
 - PQ_NEST_TCOUNT=1   k_nest_tile's bases from k_nest_tcount + k_nest_scan instead of its look-back
+- PQ_SEG_GRID=1/2    k_levels_seg with one / two wavefronts walking every page in turn (the default
+                     DELTA-major schedule walks two pages per wave once a batch has over 1,024 pages)
+- PQ_PLAIN_TILE_B=16 PLAIN copy tiles of 16 bytes (2-4 values: every tile boundary moved to a 16-B
+                     aligned destination byte, most tiles without a full piece)
 """
 import pytest
 
@@ -58,6 +62,10 @@ SWITCHES = {
     "slots_own_launch": {"PQ_SCAN_SLOTS": "0"},
     "lv_no_split": {"PQ_LV_SPLIT": "0"},
     "nest_pcount": {"PQ_NEST_PCOUNT": "1"},
+    "seg_grid1": {"PQ_SEG_GRID": "1"},
+    "seg_grid2": {"PQ_SEG_GRID": "2"},
+    "plain_tile16": {"PQ_PLAIN_TILE_B": "16"},
+    "plain_tile16_unfused": {"PQ_PLAIN_TILE_B": "16", "PQ_COPY_FUSED": "0"},
     "nest_tcount": {"PQ_NEST_TCOUNT": "1"},
 }
 
