@@ -1226,7 +1226,8 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   // base and count multiples of 32, at most the kernel's LDS image) has every word of its bitmap
   // stored by that kernel each decode (a page that fails writes nothing, and the chunk reports the
   // error): its bitmap lies past the region (cfg2: 16 MB less zeroing per decode).
-  const bool lv_seg = !(getenv("PQ_LV_SEG") && atoi(getenv("PQ_LV_SEG")) == 0);
+  const bool lv_seg = !(getenv("PQ_LV_SEG") && atoi(getenv("PQ_LV_SEG")) == 0) &&
+                      !(getenv("PQ_LV_WAVE") && atoi(getenv("PQ_LV_WAVE")) == 1);  // (launch_levels' routing)
   auto seg_whole_words = [&](const HostChunk &hc) {
     if (!lv_seg || hc.err.code || hc.col.max_def != 1 || hc.col.max_rep != 0) return false;
     for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
