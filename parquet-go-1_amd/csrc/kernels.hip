@@ -1589,26 +1589,36 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
   // (a short final group zero-fills; lanes past their range read zeros); the image zeroed
   const uint32_t sa = (uint32_t)((uintptr_t)s & 15u);
   {
+    // the stream's 16-B blocks, four loads in flight per lane, then two zero blocks past its end
+    // (reads past the stream: an 8-byte header read or a funnel at most 12 bytes on)
     const uint4 *g = (const uint4 *)(s - sa);
     const uint32_t lim = n + sa;
-    const uint32_t nv = (lim + 15) / 16;
-    for (uint32_t k = lane; k < (kSgStage + kSgSlack) / 16; k += 64) {
-      uint4 x = make_uint4(0u, 0u, 0u, 0u);
-      if (k < nv) {
-        x = g[k];
-        const int32_t rel = (int32_t)(lim - 16 * k);
-        if (rel < 16) {
-          uint32_t q[4] = {x.x, x.y, x.z, x.w};
+    const uint32_t nv = (lim + 15) / 16, nz = min(nv + 2, (kSgStage + kSgSlack) / 16);
+    auto masked = [&](uint4 x, uint32_t k) {
+      const int32_t rel = (int32_t)(lim - 16 * k);
+      if (rel >= 16) return x;
+      uint32_t q[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int32_t r = rel - 4 * i;
-            q[i] = r >= 4 ? q[i] : (r <= 0 ? 0u : (q[i] & ((1u << (8 * r)) - 1u)));
-          }
-          x = make_uint4(q[0], q[1], q[2], q[3]);
-        }
+      for (int i = 0; i < 4; i++) {
+        const int32_t r = rel - 4 * i;
+        q[i] = r >= 4 ? q[i] : (r <= 0 ? 0u : (q[i] & ((1u << (8 * r)) - 1u)));
       }
-      *(uint4 *)&L.stage[4 * k] = x;
+      return make_uint4(q[0], q[1], q[2], q[3]);
+    };
+    for (uint32_t k0 = 0; k0 < nv; k0 += 256) {
+      uint4 x[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t k = k0 + 64 * u + lane;
+        x[u] = k < nv ? g[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t k = k0 + 64 * u + lane;
+        if (k < nv) *(uint4 *)&L.stage[4 * k] = masked(x[u], k);
+      }
     }
+    for (uint32_t k = nv + lane; k < nz; k += 64) *(uint4 *)&L.stage[4 * k] = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t nimg = min(sg1_sw(min((o0 + ns + 31) >> 5, kSg1Words)) + 1, kSg1Image);
     for (uint32_t k = lane; 4 * k < nimg; k += 64) *(uint4 *)&L.bm[4 * k] = make_uint4(0u, 0u, 0u, 0u);
     if (lane == 0) L.nq = 0;
@@ -1625,7 +1635,9 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
     // ---- A. speculative walks: segment [lo, hi) of lane i (branch-free body: every lane runs the
     // same instructions; a lane past its range only reads). A lane that starts at stream position 0
     // is on the chain from the start: its hops are not capped and a header it cannot take stops it.
-    const uint32_t S = max((n + 63) / 64, 16u);
+    // segment bytes: an odd number of dwords, so the lanes' reads (about a segment apart) fall in
+    // different LDS banks
+    const uint32_t S = 4 * ((max((n + 63) / 64, 16u) + 3) / 8 * 2 + 1);
     const uint32_t lo = lane * S, hi = lo + S;
     const uint32_t lim = lo < n ? min(hi, n) : 0u;
     uint32_t p = (lane == 0 || lo <= kSg1Margin || lo >= n) ? 0u : lo - kSg1Margin;
@@ -1733,12 +1745,16 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
       out.start(o0 + base);
       uint32_t rem = 0, rpay = 0, kind = 0;  // the current run: values left, next payload byte (stage),
                                              // 0 nulls / 1 ones / 2 bit-packed
+      // (software-pipelined: the bytes of the header after the current run are read in the step
+      // before the one that decodes them, together with the step's payload piece: one LDS
+      // latency per step instead of a header read, its decode, then the dependent payload read)
+      uint32_t hx = sg_bytes4(L.stage, P + sa);
       for (;;) {
         const bool act = mine && (rem || (P < exit && v < vend));
         if (!__ballot(act)) break;
         stp.count(7);
         if (act && !rem) {
-          SgHop h = sg_fast(sg_bytes4(L.stage, P + sa), P, n);
+          SgHop h = sg_fast(hx, P, n);
           if (!h.adv) {  // a longer varint, or a run decode_hdr took in B
             h = sg_decode(sg_bytes8(L.stage, P + sa), P, n);
             if (!h.adv) {
@@ -1766,10 +1782,12 @@ DEV void levels_seg_page(const BatchDev &b, LevelSegLDS &L, const uint32_t pi) {
             }
           }
         }
+        const uint32_t px = sg_bytes4(L.stage, rpay);
+        hx = sg_bytes4(L.stage, P + sa);
         if (act && rem) {
           const uint32_t k = kind ? min(rem, 32u) : rem;
           const uint32_t m = k >= 32 ? ~0u : ((1u << k) - 1u);
-          const uint32_t x = kind == 2 ? sg_bytes4(L.stage, rpay) & m : (kind ? m : 0u);
+          const uint32_t x = kind == 2 ? px & m : (kind ? m : 0u);
           out.step(x, k);
           rpay += 4;
           rem -= k;
