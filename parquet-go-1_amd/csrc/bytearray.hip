@@ -38,11 +38,17 @@ namespace pq {
 
 constexpr uint32_t kWaveBuf = 2048;               // payload bytes per wave round staged in LDS
 constexpr uint32_t kWaveVec = kWaveBuf / 16 + 2;  // uint4 of one wave's LDS buffer
-constexpr uint32_t kLbWin = 16;     // look-back window (predecessors read per round trip)
+#ifndef PQ_BA_LBWIN
+#define PQ_BA_LBWIN 16
+#endif
+constexpr uint32_t kLbWin = PQ_BA_LBWIN;  // look-back window (predecessors read per round trip)
 constexpr uint32_t kStStride = 16;  // u64 per look-back state word: one per 128-B line (no two
                                     // tiles' atomics serialise on a line)
 constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStMask = (1ull << 62) - 1;
-constexpr uint32_t kHelpSpins = 24;               // look-back polls of a silent predecessor before computing its sum
+#ifndef PQ_BA_HELP
+#define PQ_BA_HELP 24
+#endif
+constexpr uint32_t kHelpSpins = PQ_BA_HELP;       // look-back polls of a silent predecessor before computing its sum
 constexpr uint32_t kEmitWaves = 8;                // waves of a k_ba_emit workgroup
 constexpr uint32_t kRounds = kBaTile / (64 * kEmitWaves);  // 64-value rounds per wave
 
