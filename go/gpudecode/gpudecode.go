@@ -332,6 +332,13 @@ func (b *Batch) Sync() error {
 	return toErr(C.pqgpu_batch_sync(b.b, nil, &e), &e)
 }
 
+// Wait blocks until the queued decodes have finished on the device; unlike
+// Sync it collects no errors (results and Status need Sync).
+func (b *Batch) Wait() error {
+	var e C.pqgpu_error
+	return toErr(C.pqgpu_batch_wait(b.b, nil, &e), &e)
+}
+
 // Status is the error of chunk id alone (nil when it decoded).
 func (b *Batch) Status(id int32) error {
 	var e C.pqgpu_error

@@ -305,6 +305,11 @@ int pqgpu_batch_decode(pqgpu_batch *b, void *stream, pqgpu_error *err);
 /* Wait for the batch and return the first error in (chunk, page, stage)
  * order — the error the reference's readValues would have returned. */
 int pqgpu_batch_sync(pqgpu_batch *b, void *stream, pqgpu_error *err);
+/* Wait for the batch's decodes to finish on the device, without collecting
+ * their errors or counts (pqgpu_batch_sync does both; results and status are
+ * valid only after it). A timing boundary: the decode work is done when it
+ * returns. A hipError_t failure is returned as PQ_ERR_HIP. */
+int pqgpu_batch_wait(pqgpu_batch *b, void *stream, pqgpu_error *err);
 
 int pqgpu_batch_num_chunks(const pqgpu_batch *b);
 /* Per-chunk status after sync (the error of that chunk alone). */

@@ -517,6 +517,9 @@ struct pqgpu_batch {
   // PQ_ONE_STREAM=1 (profiling): every launch on the batch stream, so each kernel is timed alone
   bool one_stream = getenv("PQ_ONE_STREAM") && atoi(getenv("PQ_ONE_STREAM")) != 0;
   bool levels_first = getenv("PQ_LEVELS_FIRST") && atoi(getenv("PQ_LEVELS_FIRST")) != 0;
+  // PQ_DICT_ONLY=0: dictionary-only batches take the generic speculative schedule (a reset launch
+  // in front of every decode) instead of the two-launch one (decode_impl)
+  bool dict_only_off = getenv("PQ_DICT_ONLY") && atoi(getenv("PQ_DICT_ONLY")) == 0;
   // Nested arrays in one pass (k_nest_tile: counts, a decoupled look-back over the chunk's earlier
   // tiles, then the outputs) instead of k_nest_count + k_nest_emit; PQ_NEST_FUSED=0: the two passes
   // The byte-array dictionaries' slot tables built by the run scan's launch (k_scan_slots) instead
@@ -2157,13 +2160,35 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
                            b->copy_mode == 0 && !b->levels_first && !l.n_scan_pages && !b->n_dict_items &&
                            l.n_items == b->n_delta_items && !pl.n_pages && !l.n_ba_delta && !l.n_copy_items &&
                            b->ba_chunks.empty() && !l.n_rec_pages && !side;
+  // Dictionary-only schedule (flat REQUIRED dictionary / boolean-RLE columns, value bases known at
+  // upload; cfg1): the run scan and the dictionary tiles, two launches on the batch stream and
+  // nothing else per decode. k_scan_runs resets its pages' tile tables itself, the dictionary launch
+  // resets the next decode's error keys (err_next, as k_values_delta does in the DELTA-major
+  // schedule); the other per-decode state is written by no kernel of this schedule, so the first
+  // decode's reset holds for the later ones.
+  const bool lvl_any0 = l.n_level_pages + l.n_level_pages_bw1 + l.n_lv_tiles > 0;
+  const bool dict_only = b->n_groups == 0 && (b->spec || b->bases_known) && b->snappy.empty() && !any_delta && !any_nest && !lvl_any0 &&
+                         b->n_dict_items > 0 && l.n_items == b->n_dict_items && l.n_scan_pages > 0 &&
+                         !l.n_copy_items && !pl.n_pages && !l.n_ba_delta && b->ba_chunks.empty() && !l.n_rec_pages &&
+                         !l.n_base_chunks && !l.n_lf_list && b->copy_mode == 0 && !b->levels_first && !side &&
+                         !b->dict_only_off;
   // the error keys of this decode (see err_sel): the DELTA-major schedule resets the state on its
   // level stream (below) and reports into the buffer its predecessor reset; the others reset all on s
   uint32_t eu = 0;
   // deferred joins only on the context's own stream: a caller's stream must hold the whole decode
   const bool defer = delta_major && s == b->ctx->stream;
   BatchDev dl = d;  // the level stream's view in a DELTA-major decode (its own error keys)
-  if (delta_major) {
+  if (dict_only) {
+    HIPCHECK(join_deferred(b, s), err);
+    eu = b->err_sel ^ 1u;
+    if (!b->err_ready[eu]) {  // the first decode after an upload: the whole per-decode state, once
+      HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
+      b->ds_synced = false;
+    }
+    d.chunk_err = (unsigned long long *)(A + (eu ? b->o_err2 : b->o_err));
+    d.err_next = (unsigned long long *)(A + (eu ? b->o_err : b->o_err2));  // reset by the dictionary launch
+    b->err_ready[eu ^ 1u] = true;
+  } else if (delta_major) {
     eu = b->err_sel ^ 1u;
     if (!b->err_ready[eu]) {  // (the first such decode): this buffer alone, in front
       const uint64_t o = eu ? b->o_err2 : b->o_err;
@@ -2373,7 +2398,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     const bool lv_then_val = b->copy_mode == 4, val_then_lv = b->copy_mode == 5;
     if (lv_then_val || val_then_lv) HIPCHECK(fork_copies(s), err);
     if (lv_then_val) HIPCHECK(levels(s), err);
-    HIPCHECK(hipEventRecord(b->ev_fork, s), err);
+    // (only when a stream waits for it: an event record on the batch stream costs ~6 us of idle GPU
+    // in front of the next launch, cfg1 / cfg3 kernel traces)
+    if (v != s || any_delta) HIPCHECK(hipEventRecord(b->ev_fork, s), err);
     if (b->levels_first)  // experiment (PQ_LEVELS_FIRST=1): the level kernels are dispatched first
       HIPCHECK(levels(s), err);
     if (v != s) HIPCHECK(hipStreamWaitEvent(v, b->ev_fork, 0), err);
@@ -2411,7 +2438,8 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
     if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
-    HIPCHECK(hipEventRecord(b->ev_fork, s), err);  // after k_bases: the value bases are known
+    if (any_delta && !b->split_values)  // (only when the DELTA stream waits for it)
+      HIPCHECK(hipEventRecord(b->ev_fork, s), err);  // after k_bases: the value bases are known
     if (b->split_values) {  // PQ_SPLIT_VALUES=1: DELTA and the other work items one after the other (profiling)
       HIPCHECK(timed(b, 10, s, l.n_delta_pages, [&] { return launch_delta_prep(d, l, s); }), err);
       HIPCHECK(timed(b, 1, s, l1.n_items, [&] { return launch_values_delta(d, l1.items, l1.n_items, s); }), err);
@@ -3176,6 +3204,16 @@ int pqgpu_batch_decode(pqgpu_batch *b, void *stream, pqgpu_error *err) {
   NEED_CTX(b, err);
   HIPCHECK(hipSetDevice(b->ctx->device), err);
   return decode_impl(b, pick_stream(b, stream), err);
+}
+
+int pqgpu_batch_wait(pqgpu_batch *b, void *stream, pqgpu_error *err) {
+  clear_err(err);
+  if (!b->ctx) return PQ_OK;  // plan-only: nothing runs on a device
+  HIPCHECK(hipSetDevice(b->ctx->device), err);
+  const hipStream_t s = pick_stream(b, stream);
+  HIPCHECK(join_deferred(b, s), err);
+  HIPCHECK(hipStreamSynchronize(s), err);
+  return PQ_OK;
 }
 
 int pqgpu_batch_sync(pqgpu_batch *b, void *stream, pqgpu_error *err) {

@@ -149,6 +149,7 @@ struct ScanLDS {
   uint32_t ctl_pos, ctl_done, ctl_stop;
 };
 
+constexpr uint32_t kPreGroups = 8;  // groups of 64 runs the stride prelude checks per step
 // PRE: the stride prelude from global memory first (a stream that is one run shape throughout is
 // then walked without staging it); without it every step of the walk reads the LDS window.
 template <class Sink, bool PRE = true, int SB = 56>  // SB: first diagnostic counter slot
@@ -201,10 +202,17 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
   // that differs, the stream end, an error) stops the prelude; the windowed walk below takes over
   // at that position with the reference's exact semantics.
   if (PRE && wv == 0) {
+    // Each step decodes the header at pos (the run shape), then reads the 8 header bytes of the
+    // kPreGroups x 64 runs from pos on at once (lane k of group j: run 64 j + k, had every run this
+    // shape) and keeps the longest prefix with that shape: those are exact chain nodes by induction,
+    // and the first run that differs is the true next node, whose bytes a lane already holds (no
+    // reload). A run that completes the values needed is taken whatever its length. One memory round
+    // trip per 512 runs: a dictionary page of 1,600 maximal literal runs (cfg4's map keys) took 25
+    // steps of two round trips each with one group.
     const uint8_t *sg = gp_u64<const uint8_t>((uint64_t)(uintptr_t)s);
+    uint64_t hx = pos < n ? ld64(sg + pos) : 0;  // bytes past the stream end are never used (checks below)
     while (done < need && pos < n) {
-      const uint64_t x0 = ld64(sg + pos);  // bytes past the stream end are never used (checks below)
-      const uint32_t u0 = sgpr((uint32_t)x0), u1 = sgpr((uint32_t)(x0 >> 32));
+      const uint32_t u0 = sgpr((uint32_t)hx), u1 = sgpr((uint32_t)(hx >> 32));
       const uint32_t tm = ~u0 & 0x80808080u;
       if (!tm) break;
       const uint32_t Lv = (uint32_t)(__builtin_ctz(tm) >> 3) + 1;
@@ -215,31 +223,59 @@ DEV uint32_t hyb_scan(ScanLDS &L, const uint8_t *s, uint32_t n, uint32_t bw, uin
       const uint32_t rv = (uint32_t)((((uint64_t)u1 << 32) | u0) >> (8 * Lv));
       const uint32_t val = isbp ? pos + Lv : (rs >= 4 ? rv : (rv & ((1u << (8 * rs)) - 1u)));
       const bool ok = cnt != 0 && (uint64_t)pos + adv <= n && (isbp || bw >= 32 || (val >> bw) == 0);
-      if (!(ok && adv >= 64)) break;
       const uint32_t nv = isbp ? cnt * 8 : cnt, rem = need - done;
-      const uint64_t Pk = (uint64_t)pos + (uint64_t)lane * adv;
-      bool same = lane == 0;
-      uint32_t vk = val;
-      if (lane > 0 && Pk + adv <= n) {
-        const uint64_t xk = ld64(sg + Pk);
-        const uint32_t a0 = (uint32_t)xk;
-        const uint32_t tk = ~a0 & 0x80808080u;
-        const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
-        const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
-        const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
-        const uint32_t rk = (uint32_t)(xk >> (8 * Lk));
-        vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
-        same = tk != 0 && Lk == Lv && hk == h && (isbp || bw >= 32 || (vk >> bw) == 0);
+      if (!(ok && (adv >= 64 || nv >= rem))) break;
+      const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);  // runs that cover rem
+      uint64_t xk[kPreGroups];
+      uint32_t vks[kPreGroups];
+#pragma unroll
+      for (uint32_t j = 0; j < kPreGroups; j++) {
+        const uint64_t Pk = (uint64_t)pos + (uint64_t)(64 * j + lane) * adv;
+        xk[j] = (64 * j + lane > 0 && 64 * j + lane < mneed && Pk < n) ? ld64(sg + Pk) : 0;
       }
-      const uint64_t nb = ~__ballot(same);
-      const uint32_t mneed = (uint32_t)(((uint64_t)rem + nv - 1) / nv);
-      const uint32_t m = min(nb ? (uint32_t)__builtin_ctzll(nb) : 64u, mneed);
-      const uint32_t first = done + lane * nv;
-      sink.window(lane < m, first, lane < m ? min(nv, need - first) : 0u, isbp != 0, vk, (uint32_t)Pk, nullptr, 0u);
-      st.add(5, m);
-      if (m == mneed) { done = need; break; }
-      done += m * nv;
-      pos += (uint32_t)(m * adv);
+      uint32_t F = 64 * kPreGroups;  // the first run (index from pos) without the shape
+#pragma unroll
+      for (uint32_t j = 0; j < kPreGroups; j++) {
+        const uint64_t Pk = (uint64_t)pos + (uint64_t)(64 * j + lane) * adv;
+        bool sm = j == 0 && lane == 0;
+        uint32_t vk = val;
+        if (!sm && Pk + adv <= n) {
+          const uint32_t a0 = (uint32_t)xk[j];
+          const uint32_t tk = ~a0 & 0x80808080u;
+          const uint32_t Lk = (uint32_t)(__builtin_ctz(tk | 0x80000000u) >> 3) + 1;
+          const uint32_t yk = (Lk >= 4 ? a0 : (a0 & ((1u << (8 * Lk)) - 1u))) & 0x7f7f7f7fu;
+          const uint32_t hk = (yk & 0x7fu) | ((yk >> 1) & 0x3f80u) | ((yk >> 2) & 0x1fc000u) | ((yk >> 3) & 0xfe00000u);
+          const uint32_t rk = (uint32_t)(xk[j] >> (8 * Lk));
+          vk = isbp ? (uint32_t)Pk + Lk : (rs >= 4 ? rk : (rk & ((1u << (8 * rs)) - 1u)));
+          sm = tk != 0 && Lk == Lv && hk == h && (isbp || bw >= 32 || (vk >> bw) == 0);
+        }
+        vks[j] = vk;
+        const uint64_t nb = ~__ballot(sm);
+        if (F == 64 * kPreGroups && nb) F = 64 * j + (uint32_t)__builtin_ctzll(nb);
+      }
+      const uint32_t M = min(F, mneed);  // runs of this step
+#pragma unroll
+      for (uint32_t j = 0; j < kPreGroups; j++) {
+        if (64 * j >= M) break;
+        const uint32_t g = 64 * j + lane;
+        const uint64_t Pk = (uint64_t)pos + (uint64_t)g * adv;
+        const uint32_t first = done + g * nv;  // < need for g < M
+        sink.window(g < M, first, g < M ? min(nv, need - first) : 0u, isbp != 0, vks[j], (uint32_t)Pk, nullptr, 0u);
+      }
+      st.add(5, M);
+      if (M == mneed) { done = need; break; }
+      done += M * nv;
+      pos += (uint32_t)(M * adv);
+      if (F < 64 * kPreGroups) {  // the run that differs: its bytes are in lane F mod 64 of group F / 64
+        if (pos >= n) break;
+        uint64_t x = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPreGroups; j++)
+          if (j == F / 64) x = xk[j];
+        hx = ((uint64_t)rdlane((uint32_t)(x >> 32), F & 63u) << 32) | rdlane((uint32_t)x, F & 63u);
+      } else {
+        hx = ld64(sg + pos);
+      }
     }
   }
   if (PRE) {
@@ -2619,6 +2655,13 @@ DEV void scan_runs_page(const BatchDev &b, uint32_t pi, ScanLDS &lds) {
   const uint32_t nn = b.page_nn_v[pi];
   RunSink rs{b.runs + b.run_base[pi], b.tile_first + b.tile_base[pi], 0u, 0u, 0u, 0u};
   uint32_t done = 0;
+  if (threadIdx.x < 64 && nn && pd.dict_bw > 0) {
+    // the page's tile table reads ~0 where no run starts a tile (the dictionary-only schedule has no
+    // reset launch); wave 0, which then writes the runs' entries, orders them after these
+    const uint32_t ntile = (nn + kDictTile - 1) / kDictTile;
+    for (uint32_t t = threadIdx.x; t < ntile; t += 64) rs.tile_first[t] = ~0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  }
   if (nn && pd.dict_bw > 0) {  // workgroup-uniform
     done = hyb_scan(lds, gp_u64<const uint8_t>(pd.data) + pd.val_off, pd.val_len, pd.dict_bw, nn, rs, b.dbg);
   }
@@ -4003,8 +4046,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
 
 // Dictionary tiles (WI_DICT) in a launch of their own: the registers and LDS are do_dict's alone
 // (not the maximum over every work-item kind), so more tiles are resident per CU.
+// (dictionary-only decodes: block 0 resets the next decode's error keys, err_next, on this stream)
+DEV void reset_err_next(const BatchDev &b) {
+  if (blockIdx.x == 0 && b.err_next)
+    for (uint32_t c = threadIdx.x; c < b.nchunks; c += blockDim.x) gp(b.err_next)[c] = ~0ull;
+}
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DICT_WPE))) k_values_dict(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
+  reset_err_next(b);
   __shared__ DictTileLDST<kDictRuns> lds;
   const WorkItem wi = items[blockIdx.x];
   const PageDesc &pd = b.pages[wi.page];
@@ -4012,6 +4061,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DIC
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_DICT_WPE))) k_values_dict2(BatchDev b_in, const WorkItem *items) {
   const BatchDev b = global_view(b_in);
+  reset_err_next(b);
   __shared__ DictTileLDST<kDictRuns> lds;
   const WorkItem wi = items[blockIdx.x];
   const PageDesc &pd = b.pages[wi.page];

@@ -126,7 +126,7 @@ _EXPORTS = [
     "pqgpu_file_close", "pqgpu_file_num_row_groups", "pqgpu_file_num_columns", "pqgpu_file_row_group_num_rows",
     "pqgpu_file_column", "pqgpu_file_chunk_meta", "pqgpu_batch_create", "pqgpu_batch_destroy", "pqgpu_batch_reset",
     "pqgpu_batch_add_chunk", "pqgpu_batch_add_file_chunk", "pqgpu_batch_upload", "pqgpu_batch_decode",
-    "pqgpu_batch_sync", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
+    "pqgpu_batch_sync", "pqgpu_batch_wait", "pqgpu_batch_num_chunks", "pqgpu_batch_chunk_status", "pqgpu_batch_chunk_result",
     "pqgpu_batch_copy_chunk", "pqgpu_batch_stats_get", "pqgpu_batch_kernel_timing", "pqgpu_batch_kernel_time",
     "pqgpu_batch_debug_counters", "pqgpu_batch_kernel_slot", "pqgpu_batch_chunk_pages", "pqgpu_batch_kernel_bytes",
     "pqgpu_copy", "pqgpu_pipeline_create", "pqgpu_pipeline_next", "pqgpu_pipeline_release", "pqgpu_pipeline_stats_get",
@@ -168,6 +168,7 @@ def lib():
         "pqgpu_batch_upload": ([P, P, E], ctypes.c_int),
         "pqgpu_batch_decode": ([P, P, E], ctypes.c_int),
         "pqgpu_batch_sync": ([P, P, E], ctypes.c_int),
+        "pqgpu_batch_wait": ([P, P, E], ctypes.c_int),
         "pqgpu_batch_num_chunks": ([P], ctypes.c_int),
         "pqgpu_batch_chunk_status": ([P, ctypes.c_int32, E], ctypes.c_int),
         "pqgpu_batch_chunk_result": ([P, ctypes.c_int32, ctypes.POINTER(ChunkResult), E], ctypes.c_int),
@@ -426,6 +427,11 @@ class Batch:
         err = Error()
         rc = lib().pqgpu_batch_sync(self._h, None, ctypes.byref(err))
         return DecodeError(err) if rc else None
+
+    def wait(self):
+        """Wait for the queued decodes on the device (no error collection: sync() does that)."""
+        err = Error()
+        _check(lib().pqgpu_batch_wait(self._h, None, ctypes.byref(err)), err)
 
     def status(self, cid):
         err = Error()

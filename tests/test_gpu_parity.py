@@ -239,3 +239,52 @@ def test_back_to_back_delta_major(gpu_ctx, which):
                 assert g is None, (where, g)
                 pqtest.assert_chunk_equal(b.result(ids[(rg, col)]), r, where)
     b.close()
+
+
+def _cfg1_run_corrupt(page=2, run=3):
+    """cfg1 with run header `run` of dictionary data page `page` set to 0x00 (an RLE run of count 0:
+    the reference's next() fails with "rle: empty RLE run", hybrid_decoder.go:123-125)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
+    import pqinspect
+    buf = bytearray(pqtest.load("cfg1"))
+    ph, j = [(ph, j) for ph, j in pqinspect.pages(bytes(buf)) if ph[1] == 0][page]
+    bw = buf[j]
+    q = j + 1
+    for _ in range(run):
+        h, q2 = pqinspect.uvar(buf, q)
+        q = q2 + ((h >> 1) * bw if h & 1 else (bw + 7) // 8)
+    buf[q] = 0
+    return bytes(buf)
+
+
+@pytest.mark.parametrize("which", ["good", "dict_error", "run_error"])
+def test_back_to_back_dict_only(gpu_ctx, which):
+    """The dictionary-only schedule (host.cpp decode_impl: flat REQUIRED dictionary columns, cfg1's
+    shape) puts only k_scan_runs and the dictionary launch on the stream per decode: the scan resets its
+    pages' tile tables and the dictionary launch the next decode's error keys. Queued decodes, then
+    decode + sync pairs: every chunk equals the oracle each time, and an index outside the dictionary
+    (k_values_dict) or an empty run (k_scan_runs) is reported with the reference's (code, page)."""
+    data = {"good": lambda: pqtest.load("cfg1"), "dict_error": lambda: pqtest.load("bad_dict_index"),
+            "run_error": _cfg1_run_corrupt}[which]()
+    orc = pqtest.oracle_decode(data)
+    bad = [(rg, col, r) for rg, col, r in orc if isinstance(r, O.OracleError)]
+    assert bool(bad) == (which != "good"), bad
+    f = pqgpu.File(data)
+    b = pqgpu.Batch(gpu_ctx)
+    ids = {(rg, col): b.add_file_chunk(f, rg, col)[0] for rg in range(f.num_row_groups) for col in range(f.num_columns)}
+    for rounds in (3, 1, 1, 2, 1):
+        for _ in range(rounds):
+            b.decode()
+        e = b.sync()
+        assert (e is None) == (not bad), e
+        for rg, col, r in orc:
+            g = b.status(ids[(rg, col)])
+            where = f"{which} x{rounds} rg{rg} col{col}"
+            if isinstance(r, O.OracleError):
+                assert g is not None and (g.code, g.page) == (r.code, r.page), (where, g, r)
+            else:
+                assert g is None, (where, g)
+                pqtest.assert_chunk_equal(b.result(ids[(rg, col)]), r, where)
+    b.close()
