@@ -2422,7 +2422,8 @@ __global__ void __launch_bounds__(256) k_levels_hyb(BatchDev b_in, const uint32_
   if (!(pd.flags & (rep ? PF_REP : PF_DEF))) {
     if (ns) sk.error(0, PQ_ERR_INVALID);  // "reader is not initialized"
   } else if (ns) {
-    done = hyb_scan<LvRunSink, false, 48>(lds, gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off),
+    done = hyb_scan<LvRunSink, true, 48>(lds,  // (stride prelude first: profiles/r06_u_probe_hyb_pre.txt)
+                                          gp_u64<const uint8_t>(pd.data) + (rep ? pd.rep_off : pd.def_off),
                                           rep ? pd.rep_len : pd.def_len, (uint32_t)(rep ? cd.rep_bw : cd.def_bw), ns, sk,
                                           b.dbg);
   }
