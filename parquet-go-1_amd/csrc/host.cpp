@@ -510,6 +510,12 @@ struct pqgpu_batch {
   std::vector<uint64_t> page_vbase_spec; // their per-chunk exclusive prefix
   bool spec = false;                     // this upload runs values concurrently with k_levels
   bool bases_known = false;              // flat REQUIRED batch: value bases uploaded, no k_bases
+  // Serial batch whose unfused copies all belong to chunks of PLAIN fixed-width pages: a page's non-null
+  // count is speculated as its value bytes / width (a well-formed page holds exactly its non-null
+  // values), so k_values_copy starts beside the level kernels instead of after k_bases; k_bases checks
+  // the decoded counts of those chunks (CF_NN_SPEC) and a miss re-decodes serially, as in spec mode.
+  bool copies_early = false;
+  std::vector<uint8_t> chunk_nn_spec;
   // Speculative concurrent schedule (values beside k_levels) whenever every page's non-null count
   // is known up front; PQ_SPEC=0 keeps the serial order. cfg2: 0.559 vs 0.595 ms per step.
   bool force_serial = spec_disabled();
@@ -1687,6 +1693,31 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->n_delta_tiles += it.kind == WI_DELTA_TILE;
     b->n_copy_items += rank(it.kind) == 5;
   }
+  b->copies_early = false;
+  b->chunk_nn_spec.assign(nc, 0);
+  if (!b->spec && !b->bases_known && !b->force_serial && !fused && b->n_copy_items && !b->one_stream &&
+      !(getenv("PQ_COPY_EARLY") && atoi(getenv("PQ_COPY_EARLY")) == 0)) {
+    bool ok = true;
+    for (size_t i = b->items.size() - b->n_copy_items; i < b->items.size() && ok; i++) {
+      const uint32_t c = b->pages[b->items[i].page].chunk;
+      if (b->chunk_nn_spec[c]) continue;
+      const HostChunk &hc = b->chunks[c];
+      const int w = hc.value_width;
+      ok = !hc.err.code && w > 0;
+      uint64_t base = 0;
+      for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages && ok; p++) {
+        const PageDesc &pd = b->pages[p];
+        ok = (pd.vkind == VK_PLAIN_FIXED || pd.vkind == VK_PLAIN_INT96) && pd.val_len % (uint64_t)w == 0 &&
+             pd.val_len / (uint64_t)w <= pd.num_slots;
+        b->page_nn_spec[p] = ok ? (uint32_t)(pd.val_len / (uint64_t)w) : 0u;
+        b->page_vbase_spec[p] = base;
+        base += b->page_nn_spec[p];
+      }
+      b->chunk_nn_spec[c] = 1;
+    }
+    b->copies_early = ok;
+    if (!ok) b->chunk_nn_spec.assign(nc, 0);
+  }
   if (G) {
     for (uint32_t g = 0; g <= G; g++) b->grp_job[g] = b->grp_scan[g] = b->grp_item[g] = 0;
     for (uint32_t g = 0; g < G; g++) b->grp_delta[g] = b->grp_dict[g] = 0;
@@ -1863,6 +1894,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     cd.num_slots = hc.num_slots;
     cd.nn_capacity = hc.num_slots;
     if (hc.err.code) { cd.flags |= CF_FAILED; continue; }
+    if (b->copies_early && b->chunk_nn_spec[c]) cd.flags |= CF_NN_SPEC;
     if (hc.has_dict) {
       cd.flags |= CF_DICT;
       cd.dict_raw = (uint64_t)(b->d_stage + hc.dict_off);
@@ -1957,7 +1989,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(up(b->o_chunks, b->chunk_desc.data(), b->chunk_desc.size() * sizeof(ChunkDesc)), err);
   HIPCHECK(up(b->o_run_base, b->run_base.data(), np * 8), err);
   HIPCHECK(up(b->o_nn, b->page_nn_init.data(), np * 4), err);
-  if (b->spec || b->bases_known) {
+  if (b->spec || b->bases_known || b->copies_early) {  // (copies_early: only its chunks' entries are used)
     HIPCHECK(up(b->o_nnv, b->page_nn_spec.data(), np * 4), err);
     HIPCHECK(up(b->o_vbase, b->page_vbase_spec.data(), np * 8), err);
   }
@@ -2432,11 +2464,14 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     }
     if (any_delta) HIPCHECK(hipStreamWaitEvent(s, b->ev_delta_join, 0), err);
   } else {
+    // (bases speculated: the copies beside the level kernels. cfg4 1.30 -> 1.27-1.28 ms; enqueued after
+    // the level kernels: equal; beside k_nest_tile: 1.33 ms, profiles/r06_z_probe_cfg4_copy_early.txt)
+    if (b->copies_early) HIPCHECK(fork_copies(s), err);
     HIPCHECK(levels(s), err);
     HIPCHECK(timed(b, 15, s, l.n_lf_list, [&] { return launch_level_fill(d, l, s); }), err);
     HIPCHECK(launch_nest_pass(s), err);
     HIPCHECK(timed(b, 3, s, l.n_base_chunks, [&] { return launch_bases(d, l, s); }), err);
-    if (b->copy_mode < 3) HIPCHECK(fork_copies(s), err);
+    if (b->copy_mode < 3 && !b->copies_early) HIPCHECK(fork_copies(s), err);
     if (!b->ev_fork) HIPCHECK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming), err);
     if (any_delta && !b->split_values)  // (only when the DELTA stream waits for it)
       HIPCHECK(hipEventRecord(b->ev_fork, s), err);  // after k_bases: the value bases are known
@@ -2537,7 +2572,7 @@ static int sync_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   HIPCHECK(join_deferred(b, s), err);
   HIPCHECK(hipStreamSynchronize(s), err);
   if (!b->decoded) return PQ_OK;
-  if (b->spec) {
+  if (b->spec || b->copies_early) {
     uint32_t miss = 0;
     HIPCHECK(hipMemcpy(&miss, b->d_arena + b->o_spec_flag, 4, hipMemcpyDeviceToHost), err);
     if (miss) {  // a page header's non-null count was wrong: decode again in serial order

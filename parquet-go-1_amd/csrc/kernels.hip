@@ -2557,11 +2557,10 @@ __global__ void __launch_bounds__(256) k_bases(BatchDev b_in, const uint32_t *ch
     uint64_t nv = p < cd.num_pages ? b.page_nn[gp] : 0;
     uint64_t nr = p < cd.num_pages ? b.page_rec[gp] : 0;
     if (p < cd.num_pages) {
-      if (b.spec) {
-        if (b.page_nn_v[gp] != (uint32_t)nv) atomicOr(b.spec_mismatch, 1u);
-      } else {
-        b.page_nn_v[gp] = (uint32_t)nv;
-      }
+      // speculated counts (spec mode: page headers; CF_NN_SPEC: PLAIN value bytes) are checked; a
+      // CF_NN_SPEC chunk's copies read the uploaded ones, which an equal count leaves in place
+      if ((b.spec || (cd.flags & CF_NN_SPEC)) && b.page_nn_v[gp] != (uint32_t)nv) atomicOr(b.spec_mismatch, 1u);
+      if (!b.spec && !(cd.flags & CF_NN_SPEC)) b.page_nn_v[gp] = (uint32_t)nv;
     }
     part_v[threadIdx.x] = nv;
     part_r[threadIdx.x] = nr;
@@ -2575,7 +2574,7 @@ __global__ void __launch_bounds__(256) k_bases(BatchDev b_in, const uint32_t *ch
       wg_barrier();
     }
     if (p < cd.num_pages) {
-      if (!b.spec) b.page_vbase[gp] = carry_v + part_v[threadIdx.x] - nv;
+      if (!b.spec && !(cd.flags & CF_NN_SPEC)) b.page_vbase[gp] = carry_v + part_v[threadIdx.x] - nv;
       b.page_rbase[gp] = carry_r + part_r[threadIdx.x] - nr;
     }
     wg_barrier();

@@ -139,7 +139,8 @@ static_assert(sizeof(ChunkDesc) == 480, "ChunkDesc layout: host and device share
 // Chunk flags
 enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8,
                  CF_BA_SYNC = 16,    // byte-array payload without an upload-time bound: sized after the scan
-                 CF_BA_PRESUM = 32 };  // byte-array tile bases from k_ba_sums + k_ba_scan (no look-back)
+                 CF_BA_PRESUM = 32,  // byte-array tile bases from k_ba_sums + k_ba_scan (no look-back)
+                 CF_NN_SPEC = 64 };  // serial batch: non-null counts speculated from PLAIN value bytes (k_bases checks)
 
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,

@@ -25,6 +25,8 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
 - PQ_NEST_TCOUNT=1   k_nest_tile's bases from k_nest_tcount + k_nest_scan instead of its look-back
 - PQ_SEG_GRID=1/2    k_levels_seg with one / two wavefronts walking every page in turn (the default
                      DELTA-major schedule walks two pages per wave once a batch has over 1,024 pages)
+- PQ_COPY_EARLY=0    serial batches' PLAIN copies after k_bases instead of beside the level kernels on
+                     counts speculated from the pages' value bytes
 - PQ_DICT_ONLY=0     dictionary-only batches through the generic speculative schedule (a reset launch
                      per decode) instead of the two-launch one
 - PQ_PLAIN_TILE_B=16 PLAIN copy tiles of 16 bytes (2-4 values: every tile boundary moved to a 16-B
@@ -70,6 +72,7 @@ SWITCHES = {
     "plain_tile16_unfused": {"PQ_PLAIN_TILE_B": "16", "PQ_COPY_FUSED": "0"},
     "nest_tcount": {"PQ_NEST_TCOUNT": "1"},
     "dict_only_off": {"PQ_DICT_ONLY": "0"},
+    "copy_early_off": {"PQ_COPY_EARLY": "0"},
 }
 
 
