@@ -288,3 +288,70 @@ def test_back_to_back_dict_only(gpu_ctx, which):
                 assert g is None, (where, g)
                 pqtest.assert_chunk_equal(b.result(ids[(rg, col)]), r, where)
     b.close()
+
+
+def _flip_def(name, col, to_null, page=1):
+    """Fixture `name` with one definition level of column `col`'s data page `page` changed inside a
+    bit-packed run (else the value of its first RLE run that has one): max_def -> max_def - 1
+    (non-null values become null) or back (nulls become non-null). The value bytes stay as they were."""
+    import io
+    import os
+    import sys
+    import pyarrow.parquet as pq
+    sys.path.insert(0, os.path.join(os.path.dirname(pqtest.GOLDEN), "..", "tools"))
+    import pqinspect
+    buf = bytearray(pqtest.load(name))
+    sc = pq.ParquetFile(io.BytesIO(bytes(buf))).metadata.schema.column(col)
+    mr, md = sc.max_repetition_level, sc.max_definition_level
+    ph, j = [(ph, j) for ph, j in pqinspect.pages(bytes(buf), 0, col) if ph[1] == 0][page]
+    assert ph[5][2] == 0  # PLAIN values
+    p = j
+    if mr:
+        p += 4 + int.from_bytes(buf[p:p + 4], "little")
+    end = p + 4 + int.from_bytes(buf[p:p + 4], "little")
+    p += 4
+    bw = md.bit_length()
+    src, dst = (md, md - 1) if to_null else (md - 1, md)
+    rle = None
+    while p < end:
+        h, q = pqinspect.uvar(buf, p)
+        if h & 1:
+            n = (h >> 1) * 8
+            for k in range(n):
+                bit = (q * 8) + k * bw
+                v = (int.from_bytes(buf[bit // 8:bit // 8 + 2], "little") >> (bit % 8)) & ((1 << bw) - 1)
+                if v == src:
+                    x = int.from_bytes(buf[bit // 8:bit // 8 + 2], "little")
+                    x = (x & ~(((1 << bw) - 1) << (bit % 8))) | (dst << (bit % 8))
+                    buf[bit // 8:bit // 8 + 2] = x.to_bytes(2, "little")
+                    return bytes(buf)
+            p = q + (h >> 1) * bw
+        else:
+            if rle is None and buf[q] == src:
+                rle = q
+            p = q + (bw + 7) // 8
+    assert rle is not None, "no level to flip"
+    buf[rle] = dst  # no bit-packed run holds one: a whole RLE run changes
+    return bytes(buf)
+
+
+@pytest.mark.parametrize("to_null", [True, False])
+@pytest.mark.parametrize("name,col", [("edge_nulls_v1", 0), ("types_v1", 1), ("types_v1", 5), ("cfg4_small", 0), ("cfg4_small", 2)])
+def test_copies_early_count_miss(gpu_ctx, name, col, to_null):
+    """Serial batches start their PLAIN copies on non-null counts speculated from the pages' value
+    bytes (host.cpp copies_early). A page whose definition levels hold one null more than its value
+    bytes imply (the reference reads one value less and ignores the last one) or one null less (it
+    runs out of values: io.EOF on that page) misses the speculation; the batch is decoded again in
+    the serial order and every chunk equals the oracle, errors at the reference's (code, page)."""
+    data = _flip_def(name, col, to_null)
+    orc = pqtest.oracle_decode(data)
+    gpu = _gpu_decode(gpu_ctx, data)
+    for rg, c, r in orc:
+        g = gpu[(rg, c)]
+        where = f"{name} col{col} to_null={to_null}: rg{rg} col{c}"
+        if isinstance(r, O.OracleError):
+            assert isinstance(g, pqgpu.DecodeError), f"{where}: oracle error {r} but GPU decoded"
+            assert (g.code, g.page) == (r.code, r.page), f"{where}: {g} vs {r}"
+        else:
+            assert not isinstance(g, pqgpu.DecodeError), f"{where}: GPU error {g}"
+            pqtest.assert_chunk_equal(g, r, where)
