@@ -82,9 +82,6 @@ DEV void lds_put(uint8_t *lb, uint32_t d, const uint8_t *src, uint32_t len) {
 // (the first and last words are shared with the neighbouring values). A slot's bytes past the
 // entry are zero (k_dict_slots), and so are the pieces not loaded, so the words need no masks:
 // the funnel shift brings zeros below the first byte and the padding supplies them past the last.
-#ifndef PQ_BA_NOMASK
-#define PQ_BA_NOMASK 1
-#endif
 template <int NP>
 DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
   constexpr int NW = 4 * NP;
@@ -103,7 +100,7 @@ DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
     if (4u * m >= end) break;
     const uint32_t prev = m ? W[m - 1] : 0u;
     const uint32_t word = sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m];
-    if (PQ_BA_NOMASK && NP == 2) {  // (64-B slots keep the masks: without them the 16-word loop is not unrolled)
+    if (NP == 2) {  // (64-B slots keep the masks: without them the 16-word loop is not unrolled)
       atomicOr(&lw[d0 + m], word);
     } else {
       const uint32_t lo = max(sh, 4u * m) - 4u * m, hi = min(end, 4u * m + 4) - 4u * m;  // valid bytes [lo, hi)
@@ -113,92 +110,13 @@ DEV void lds_put_slot(uint32_t *lw, uint32_t d, const uint4 *sl, uint32_t len) {
   }
 }
 
-#ifndef PQ_BA_STORES
-#define PQ_BA_STORES 0  // 1: pass B writes slot bytes with plain LDS stores (no atomics, no zeroing);
-                        // cfg3 k_ba_emit 0.55 ms against 0.43-0.46 ms with ds_or (byte stores at the edges)
-#endif
-// The same with plain stores: a destination word inside the value is written whole; the two edge
-// words (shared with the neighbouring values) byte by byte. Every byte of a round's range belongs
-// to exactly one value, so the buffer needs no zeroing and no atomics.
-template <int NP>
-DEV void lds_put_slot_st(uint8_t *lb, uint32_t d, const uint4 *sl, uint32_t len) {
-  constexpr int NW = 4 * NP;
-  uint32_t W[NW];
-#pragma unroll
-  for (int q = 0; q < NW / 4; q++) {
-    const uint32_t x[4] = {sl[q].x, sl[q].y, sl[q].z, sl[q].w};
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (4 * q + i >= 1) W[4 * q + i - 1] = x[i];
-  }
-  W[NW - 1] = 0;
-  uint32_t *lw = (uint32_t *)lb;
-  const uint32_t sh = d & 3u, d0 = d >> 2, end = sh + len;
-#pragma unroll
-  for (int m = 0; m < NW; m++) {
-    if (4u * m >= end) break;
-    const uint32_t prev = m ? W[m - 1] : 0u;
-    const uint32_t word = sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m];
-    const uint32_t lo = max(sh, 4u * m) - 4u * m, hi = min(end, 4u * m + 4) - 4u * m;  // valid bytes [lo, hi)
-    if (lo == 0 && hi == 4) {
-      lw[d0 + m] = word;
-    } else {
-      for (uint32_t k = lo; k < hi; k++) lb[4 * (d0 + m) + k] = (uint8_t)(word >> (8 * k));
-    }
-  }
-}
-
-// Non-temporal 16-B payload stores (PQ_BA_NT) and offsets stores (PQ_BA_NTO): the written stream
-// does not displace the dictionary's slot table from L2, which every value of the tile gathers from
-// (tools/ubench/ba_ubench.hip: cfg3-shaped emit 0.433 -> 0.350 ms with the payload stores alone).
-#ifndef PQ_BA_NT
-#define PQ_BA_NT 1
-#endif
-#ifndef PQ_BA_NTO
-#define PQ_BA_NTO 0
-#endif
+// Non-temporal 16-B payload stores: the written stream does not displace the dictionary's slot table
+// from L2, which every value of the tile gathers from (tools/ubench/ba_ubench.hip: cfg3-shaped emit
+// 0.433 -> 0.350 ms); the offsets stores keep the default policy.
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-DEV void st_payload16(uint8_t *p, uint4 v) {
-  if (PQ_BA_NT) __builtin_nontemporal_store(v4u32{v.x, v.y, v.z, v.w}, (v4u32 *)p);
-  else *(uint4 *)p = v;
-}
-DEV void st_offset(int32_t *p, int32_t v) {
-  if (PQ_BA_NTO) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-DEV uint32_t bperm(uint32_t v, uint32_t src_lane) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4), (int)v); }
-
-// Words W[0..4] (entry bytes, zero past the entry) OR-ed into the zeroed LDS buffer at byte d: the
-// words that hold any of the n bytes [d, d + n) (dword funnel shifts to d's alignment).
-DEV void lds_or_words(uint32_t *lw, uint32_t d, const uint32_t (&W)[5], uint32_t n) {
-  const uint32_t sh = d & 3u, d0 = d >> 2, end = sh + n;
-#pragma unroll
-  for (int m = 0; m < 5; m++) {
-    if (4u * m >= end) break;
-    const uint32_t prev = m ? W[m - 1] : 0u;
-    atomicOr(&lw[d0 + m], sh ? __builtin_amdgcn_alignbyte(W[m], prev, 4 - sh) : W[m]);
-  }
-}
-// Pair-loaded slots (PA, 16- and 32-B slots): lane l holds piece (l & 1) of value (l >> 1) + 32 h of
-// the round in x[h]; its bytes go to the round's LDS buffer at the value's offset (piece 0: entry
-// bytes [0, 12) after the length word; piece 1: entry bytes [12, 28)). All lanes must be active.
-DEV void lds_put_pair(uint32_t *lw, uint32_t cur, uint32_t l, uint32_t ex, const uint4 (&x)[2], uint32_t lane) {
-#pragma unroll
-  for (uint32_t h = 0; h < 2; h++) {
-    const uint32_t v = (lane >> 1) + 32 * h;
-    const uint32_t lv = bperm(l, v), ev = bperm(ex, v);
-    const uint4 y = x[h];
-    if (!(lane & 1)) {
-      const uint32_t W0[5] = {y.y, y.z, y.w, 0u, 0u};
-      if (lv) lds_or_words(lw, cur + ev, W0, min(lv, 12u));
-    } else if (lv > 12) {
-      const uint32_t W1[5] = {y.x, y.y, y.z, y.w, 0u};
-      lds_or_words(lw, cur + ev + 12, W1, lv - 12);
-    }
-  }
-}
-
-// The same straight to global memory (rounds whose bytes exceed the LDS buffer).
+DEV void st_payload16(uint8_t *p, uint4 v) { __builtin_nontemporal_store(v4u32{v.x, v.y, v.z, v.w}, (v4u32 *)p); }
+DEV void st_offset(int32_t *p, int32_t v) { *p = v; }
+// lds_put's bytes straight to global memory (rounds whose bytes exceed the LDS buffer).
 DEV void global_put(uint8_t *dst, const uint8_t *src, uint32_t len) {
   uint32_t k = 0;
   const uint32_t head = min(len, (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u));
@@ -394,15 +312,10 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 // slot table (any slot size: a value loads the 16-B pieces its entry occupies), else bytes are
 // read from their source (dictionaries without slots, PLAIN / DELTA pages). Pass B works in
 // groups of G rounds: the G rounds' loads are issued together.
-// PA (16- and 32-B slots): pass A loads every value's whole slot by lane pairs — lanes 2k and 2k + 1
-// take pieces 0 and 1 of one value in the same instruction, one cache line and one L2 request per
-// value instead of the length's and then each piece's — and keeps the pieces in registers for pass
-// B, which gathers nothing (tools/ubench/ba_ubench.hip: the emit 0.433 -> 0.351 ms, with
-// non-temporal payload stores 0.288 ms).
-#ifndef PQ_BA_PA
-#define PQ_BA_PA 0  // product kernel: 128 VGPRs with 68 B of spills at 4 waves per SIMD; cfg3 k_ba_emit
-                    // 0.428 ms against 0.352 ms without (profiles/r05_s4_probe_ba_emit.txt): off
-#endif
+// (Tried and removed: pass A loading every value's whole 32-B slot by lane pairs and keeping the
+// pieces in registers -- 0.288 ms in tools/ubench/ba_ubench.hip, but 128 VGPRs with spills in the
+// product kernel, 0.428 against 0.352 ms, profiles/r05_s4_probe_ba_emit.txt; the second pieces by
+// LDS-DMA, profiles/r06_t_probe_ba_dma.txt.)
 // P0 (16- and 32-B slots): pass A loads every value's first slot piece (its length and first 12
 // bytes) instead of the length word, and keeps it; pass B loads only the second piece of entries
 // longer than 12 bytes: 1 + P(len > 12) texture requests per value instead of 2 + P(len > 12).
@@ -414,7 +327,7 @@ DEV uint64_t lookback(const BatchDev &b, const ChunkDesc &cd, uint32_t c, uint32
 #ifndef PQ_BA_G
 #define PQ_BA_G 2  // pass B: rounds whose slot pieces are loaded together
 #endif
-template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, bool PA = false, class EL, bool P0 = false>
+template <bool SLOT, uint32_t SV = SLOT ? 4 : 1, bool LS = false, class EL, bool P0 = false>
 DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, uint32_t t, uint32_t p, uint32_t v0,
                    uint32_t lo, uint32_t hi, bool is_dict, bool have, DictTile &tl, EL &L, Stamps &st,
                    const uint4 *lslots = nullptr) {
@@ -450,7 +363,6 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   }
   uint32_t pos[R];  // S == 0 dictionaries: the entry's position in the dictionary page
   uint32_t len[R];
-  uint4 pk[PA ? R : 1][2];  // PA: lane l's slot pieces (piece l & 1 of values (l >> 1) + 32 h)
   uint4 p0[P0 ? R : 1];     // P0: the values' first slot pieces
 #pragma unroll
   for (uint32_t r = 0; r < R; r++) {
@@ -459,19 +371,6 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
     if constexpr (P0) {
       p0[r] = idx[r] != ~0u ? slots[(uint64_t)idx[r] << s4] : make_uint4(0u, 0u, 0u, 0u);
       len[r] = p0[r].x;  // (0 where there is no value)
-      continue;
-    }
-    if constexpr (PA) {  // (every lane active: bpermute)
-      const uint32_t pc = lane & 1u;
-#pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t x = bperm(idx[r], (lane >> 1) + 32 * h);
-        pk[r][h] = x != ~0u && (s4 || !pc) ? slots[((uint64_t)x << s4) + pc] : make_uint4(0u, 0u, 0u, 0u);
-      }
-      // this lane's own value's length: word 0 of piece 0 of value `lane`, held by lane 2 lane mod 64
-      const uint32_t src = (2 * lane) & 63u;
-      const uint32_t a = bperm(pk[r][0].x, src), c = bperm(pk[r][1].x, src);
-      len[r] = lane < 32 ? a : c;  // 0 where there is no value (its pieces are zero)
       continue;
     }
     if (idx[r] != ~0u) {
@@ -502,8 +401,7 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   const uint64_t wt = wave_sum64(mine);
   st.lap(1);
   uint4 *wb = &L.wbuf[wv][0];
-  if (!PQ_BA_STORES)
-    for (uint32_t k = lane; k < kWaveVec; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t k = lane; k < kWaveVec; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
   if (lane == 0) L.wtot[wv] = wt;
   wg_barrier();
   st.lap(2);
@@ -544,14 +442,14 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
       src[rr] = nullptr;
       if (!SLOT && idx[r] != ~0u) src[rr] = is_dict ? draw + pos[r] : gp_u64<const uint8_t>(srcs[idx[r]]);
     }
-    if constexpr (SLOT && !PA) {
+    if constexpr (SLOT) {
 #pragma unroll
       for (uint32_t rr = 0; rr < G; rr++) {
         const uint32_t r = g * G + rr;
 #pragma unroll
         for (uint32_t q = 0; q < SV; q++)  // the slot pieces holding bytes of the entry (none: no value)
           sl[rr][q] = (P0 && q == 0) ? p0[r]
-                      : len[r] && len[r] + 4 > 16 * q
+                      : len[r] && len[r] + 4 > 16 * q && !(q && PQ_ABLATE(b, 14))  // (diagnostic: no later pieces)
                           ? ((LS && q == 0) ? lslots[idx[r]] : slots[((uint64_t)idx[r] << s4) + q])
                           : make_uint4(0u, 0u, 0u, 0u);
       }
@@ -564,15 +462,12 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
       const uint32_t incl = wave_incl_scan32(l);
       const uint32_t T = rdlane(incl, 63);
       const uint32_t ex = incl - l;
-      if (v >= lo && v < hi) st_offset(&offs[v + 1], (int32_t)(wbase + incl));
+      if (v >= lo && v < hi && !PQ_ABLATE(b, 13)) st_offset(&offs[v + 1], (int32_t)(wbase + incl));  // (diagnostic: no stores)
       if (!T) continue;
       if (cur + T <= kWaveBuf) {
-        if constexpr (PA) {
-          lds_put_pair(lw, cur, l, ex, pk[r], lane);
-        } else if (l) {
+        if (l) {
           if constexpr (SLOT) {
-            if (PQ_BA_STORES) lds_put_slot_st<SV>(lb, cur + ex, sl[rr], l);
-            else lds_put_slot<SV>(lw, cur + ex, sl[rr], l);
+            lds_put_slot<SV>(lw, cur + ex, sl[rr], l);
           } else if (src[rr]) {
             lds_put(lb, cur + ex, src[rr], l);
           }
@@ -580,16 +475,16 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
         wave_lds_sync();
         const uint32_t end = cur + T, full = end >> 4;
         const uint32_t k0 = own ? 1u : 0u;
-        for (uint32_t k = k0 + lane; k < full; k += 64) st_payload16(gblk + 16 * k, wb[k]);
-        if (own && full && lane >= own && lane < 16) gblk[lane] = lb[lane];
+        if (!PQ_ABLATE(b, 13)) {
+          for (uint32_t k = k0 + lane; k < full; k += 64) st_payload16(gblk + 16 * k, wb[k]);
+          if (own && full && lane >= own && lane < 16) gblk[lane] = lb[lane];
+        }
         wave_lds_sync();
         if (full) {
           if (lane == 0) wb[0] = wb[full];  // the unfinished piece becomes piece 0
           wave_lds_sync();
-          if (!PQ_BA_STORES) {
-            for (uint32_t k = 1 + lane; k <= full; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
-            wave_lds_sync();
-          }
+          for (uint32_t k = 1 + lane; k <= full; k += 64) wb[k] = make_uint4(0u, 0u, 0u, 0u);
+          wave_lds_sync();
           gblk += 16 * full;
           own = 0;
         }
@@ -642,18 +537,17 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   }
   st.lap(0);
   if (CLS == 3) emit_tile<true, 2, true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st, lslots);
-  else if (CLS == 0) emit_tile<true, 2, false, PQ_BA_PA != 0, EL, PQ_BA_P0 != 0>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
+  else if (CLS == 0) emit_tile<true, 2, false, EL, PQ_BA_P0 != 0>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else if (CLS == 1 || (is_dict && cd.slot_shift)) emit_tile<true>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   else emit_tile<false>(b, pd, cd, t, p, v0, lo, hi, is_dict, have, tl, L, st);
   st.count(7);
   st.flush(40);
 }
 
-// class 0: with the slots kept in registers (PQ_BA_PA) 4 waves per SIMD (two 8-wave workgroups per
-// CU, <= 128 VGPRs); with the first pieces (PQ_BA_P0) <= 96 VGPRs, which still seats two 8-wave
-// workgroups per CU; with neither, 6 (three workgroups: <= 80 VGPRs, 46 KB LDS each)
+// class 0: with the first pieces in registers (PQ_BA_P0) <= 96 VGPRs, which still seats two 8-wave
+// workgroups per CU; without, 6 (three workgroups: <= 80 VGPRs, 46 KB LDS each)
 #ifndef PQ_BA_WPE
-#define PQ_BA_WPE (PQ_BA_PA ? 4 : PQ_BA_P0 ? 5 : 6)
+#define PQ_BA_WPE (PQ_BA_P0 ? 5 : 6)
 #endif
 __global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(PQ_BA_WPE))) k_ba_emit_slots(BatchDev b_in) {
   const BatchDev b = global_view(b_in);

@@ -811,10 +811,8 @@ DEV uint32_t nest_resolve(const BatchDev &b, const ChunkDesc &cd, uint32_t pos, 
   return polls;
 }
 
-#ifndef PQ_NEST_TILES
-#define PQ_NEST_TILES 1  // tiles per k_nest_tile workgroup (2: cfg4 k_nest_tile 0.63 -> 0.73 ms, profiles/r05_s36_probe_nest_pairs.txt)
-#endif
-constexpr uint32_t kNestTiles = PQ_NEST_TILES;
+constexpr uint32_t kNestTiles = 1;  // tiles per k_nest_tile workgroup (2, the second counting while the
+                                    // first looks back: cfg4 0.63 -> 0.73 ms, profiles/r05_s36_probe_nest_pairs.txt)
 template <uint32_t R>
 struct NestTileLDS {
   union {
@@ -1052,17 +1050,12 @@ __global__ void __launch_bounds__(256) k_nest_tcount(BatchDev b_in, const uint4 
     }
 }
 
-// k_nest_tile<R>: kNestTiles tiles per workgroup (block-order positions from `order`): every tile's
-// counting half first, publishing its aggregates, then each tile's look-back and outputs -- the
-// look-back of the first tile waits while the second one counts. A tile whose chunk has group bitmaps
-// of its own (their masks live in one LDS set) is emitted right after its count.
+// k_nest_tile<R>: one tile per workgroup (block-order position from `order`): its counting half,
+// publishing its aggregates, then its look-back and outputs.
 template <uint32_t R>
-#ifndef PQ_NEST_TILE_WPE1
-#define PQ_NEST_TILE_WPE1 (PQ_NEST_TILES > 1 ? 4 : 5)  // R = 1: 125 / 96 VGPRs
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? PQ_NEST_TILE_WPE1 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
-                                                                                                                                     uint32_t n, uint32_t counted, const uint32_t *order, uint32_t based) {
-  constexpr uint32_t C = R + 1;
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1 ? 5 : R <= 3 ? 4 : 2))) k_nest_tile(BatchDev b_in, const uint4 *tiles, uint32_t first,
+                                                                                                                  uint32_t n, uint32_t counted, const uint32_t *order, uint32_t based) {
+  constexpr uint32_t C = R + 1;  // (R = 1: 96 VGPRs)
   const BatchDev b = global_view(b_in);
   __shared__ NestTileLDS<R> L;
   // diagnostic build (tools/diag_nest.py): slots 24-31 -- 0 run staging, 1 group marks, 2 expansion,
@@ -1072,33 +1065,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 1
   PQ_STAMPS(st, b.dbg);
   PQ_STAMPS(se, b.dbg);
   st.begin();
-  static_assert(kNestTiles == 1 || kNestTiles == 2, "one or two tiles per workgroup");
-  uint32_t fm0[C], vmm0[C], fm1[C], vmm1[C];  // (two named sets: an indexed pair would go to scratch)
-  uint32_t pend = 0;  // tiles counted, not yet emitted
-  auto count = [&](uint32_t q, uint32_t (&fm)[C], uint32_t (&vmm)[C]) {
-    const uint32_t k = blockIdx.x * kNestTiles + q;
-    if (k >= n) return;  // workgroup-uniform
-    const uint32_t pos = gp(order)[first + k];
+  if (blockIdx.x < n) {  // (workgroup-uniform)
+    uint32_t fm[C], vmm[C];
+    const uint32_t pos = gp(order)[first + blockIdx.x];
     const NestFill x = nest_fill(b, gp(tiles)[pos]);
-    nest_tile_count<R>(b, x, pos, q, counted != 0, based != 0, L, fm, vmm, st);
-    if (nest_groups_owned(b.chunks[x.chunk])) {  // (one set of group masks in LDS)
-      nest_tile_emit<R>(b, x, pos, q, based != 0, L, fm, vmm, st, se);
-      wg_barrier();
-    } else {
-      pend |= 1u << q;
-    }
-  };
-  auto emit = [&](uint32_t q, const uint32_t (&fm)[C], const uint32_t (&vmm)[C]) {
-    if (!((pend >> q) & 1u)) return;
-    const uint32_t pos = gp(order)[first + blockIdx.x * kNestTiles + q];
-    const NestFill x = nest_fill(b, gp(tiles)[pos]);
-    nest_tile_emit<R>(b, x, pos, q, based != 0, L, fm, vmm, st, se);
-    wg_barrier();  // (the next tile's bases and rows reuse the LDS)
-  };
-  count(0, fm0, vmm0);
-  if (kNestTiles > 1) count(1, fm1, vmm1);
-  emit(0, fm0, vmm0);
-  if (kNestTiles > 1) emit(1, fm1, vmm1);
+    nest_tile_count<R>(b, x, pos, 0, counted != 0, based != 0, L, fm, vmm, st);
+    nest_tile_emit<R>(b, x, pos, 0, based != 0, L, fm, vmm, st, se);
+  }
   st.flush(24);
   se.flush(32);
 }
@@ -1207,7 +1180,7 @@ static void launch_emit_r(const BatchDev &b, const LaunchLists &l, hipStream_t s
 template <uint32_t R>
 static void launch_tile_r(const BatchDev &b, const LaunchLists &l, hipStream_t s, uint32_t counted, uint32_t based) {
   const uint32_t n = l.nest_first[R + 1] - l.nest_first[R];
-  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3((n + kNestTiles - 1) / kNestTiles), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], n,
+  if (n) hipLaunchKernelGGL(k_nest_tile<R>, dim3(n), dim3(256), 0, s, b, l.nest_desc, l.nest_first[R], n,
                             counted, l.nest_order, based);
 }
 // (based: every tile's bases from k_nest_tcount + k_nest_scan, chunks with one list level only)

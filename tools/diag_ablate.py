@@ -3,7 +3,7 @@ PQ_ABLATE bits; timing only: outputs are wrong under any ablation).
 
 Bits: 1 k_values no stores, 2 k_values no unpack, 4 k_levels no run expansion, 8 k_levels serial
 walk of every run, 256 k_ba_emit no look-back, 512 no pass B, 2048 no length loads, 4096 every
-look-back by self-help, 65536 k_nest_emit no offset stores, 131072 no bitmaps, 262144 k_nest_count /
+look-back by self-help, 8192 k_ba_emit no payload / offsets stores, 16384 no second slot pieces, 65536 k_nest_emit no offset stores, 131072 no bitmaps, 262144 k_nest_count /
 k_nest_emit no level expansion.
 
 usage: python tools/diag_ablate.py cfg2 0,4,8 [rows]
