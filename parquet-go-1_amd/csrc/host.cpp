@@ -2483,8 +2483,22 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       HIPCHECK(fork_delta(b->ev_fork), err);
     }
     HIPCHECK(fork_nest(), err);  // on the DELTA stream after its pages
-    HIPCHECK(scan_runs(s), err);
-    HIPCHECK(timed(b, 8, s, n_dict, [&] { return launch_values_dict(d, dict_items, b->n_dict2_items, n_dict, s); }), err);
+    // DELTA pages on the batch stream (no level streams; cfg5): the run scan and the dictionary tiles
+    // beside them on the side stream (cfg5 5.67-5.68 -> 5.63 ms; the scan alone beside them: equal,
+    // profiles/r06_ac_probe_cfg5_scan_side.txt). PQ_SCAN_SIDE=0: after them on the batch stream
+    const bool side_dict = !(getenv("PQ_SCAN_SIDE") && atoi(getenv("PQ_SCAN_SIDE")) == 0) && ds == s && any_delta &&
+                           !b->split_values && (l.n_scan_pages || n_dict) && !b->one_stream;
+    hipStream_t vs = side_dict ? b->ctx->side : s;
+    if (side_dict) {
+      HIPCHECK(hipStreamWaitEvent(vs, b->ev_fork, 0), err);
+      if (!b->ev_join) HIPCHECK(hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming), err);
+    }
+    HIPCHECK(scan_runs(vs), err);
+    HIPCHECK(timed(b, 8, vs, n_dict, [&] { return launch_values_dict(d, dict_items, b->n_dict2_items, n_dict, vs); }), err);
+    if (side_dict) {
+      HIPCHECK(hipEventRecord(b->ev_join, vs), err);
+      HIPCHECK(hipStreamWaitEvent(s, b->ev_join, 0), err);
+    }
     HIPCHECK(timed(b, 9, s, l2.n_items, [&] { return launch_values(d, l2, s); }), err);
     HIPCHECK(timed(b, 17, s, pl.n_pages, [&] { return launch_plain_ba(d, pl, s); }), err);  // PLAIN BYTE_ARRAY chains
     HIPCHECK(timed(b, 18, s, l.n_ba_delta, [&] { return launch_ba_delta(d, l, s); }), err);  // DLBA / DBA lengths -> values

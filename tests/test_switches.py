@@ -27,6 +27,8 @@ same page (the reference's readChunk / readPages / getValuesDecoder path, chunk_
                      DELTA-major schedule walks two pages per wave once a batch has over 1,024 pages)
 - PQ_COPY_EARLY=0    serial batches' PLAIN copies after k_bases instead of beside the level kernels on
                      counts speculated from the pages' value bytes
+- PQ_SCAN_SIDE=0     batches whose DELTA pages run on the batch stream: the run scan and the dictionary
+                     tiles after them instead of beside them on the side stream
 - PQ_DICT_ONLY=0     dictionary-only batches through the generic speculative schedule (a reset launch
                      per decode) instead of the two-launch one
 - PQ_PLAIN_TILE_B=16 PLAIN copy tiles of 16 bytes (2-4 values: every tile boundary moved to a 16-B
@@ -73,6 +75,7 @@ SWITCHES = {
     "nest_tcount": {"PQ_NEST_TCOUNT": "1"},
     "dict_only_off": {"PQ_DICT_ONLY": "0"},
     "copy_early_off": {"PQ_COPY_EARLY": "0"},
+    "scan_side_off": {"PQ_SCAN_SIDE": "0"},
 }
 
 
