@@ -602,6 +602,12 @@ struct pqgpu_batch {
   uint64_t l_level_bw1 = 0;
   uint64_t l_level = 0, l_scan = 0, l_base = 0, l_ba = 0, l_rec = 0, l_pc = 0;
   uint64_t z_begin = 0, z_end = 0, f_begin = 0, f_end = 0;  // per-decode reset regions
+  // [z_begin, z_bm_end): the validity bitmaps OR-ed at shared edge words (zeroed by the first decode
+  // after an upload only: every decode of an uploaded batch writes the same bits, so the words an
+  // earlier decode left hold exactly what the OR adds); [z_bm_end, z_end): counters and look-back
+  // states, zeroed every decode
+  uint64_t z_bm_end = 0;
+  bool bm_zeroed = false;
   // Chunk error keys. DELTA-major decodes (cfg2) run their two streams without a join per decode:
   // the values launch on the batch stream reports into o_err / o_err2 (alternately: the launch resets
   // the next decode's buffer itself, err_next), the level stream into o_err_ds (reset with the rest of
@@ -1283,6 +1289,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       if (hc.grp_alias[g] < 0) hc.o_grp_valid[g] = take(words);
     }
   }
+  b->z_bm_end = a;
   b->o_rec = take((uint64_t)np * 4);
   b->o_run_count = take((uint64_t)np * 4);
   b->o_spec_flag = take(4);
@@ -1613,6 +1620,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->ds_synced = false;
   b->err_sel = 0;
   b->err_ready[0] = b->err_ready[1] = false;
+  b->bm_zeroed = false;
   // DELTA tiles first (k_delta_sums runs over exactly that prefix), then the scalar DELTA
   // pages (long-running), then the LDS-staged tiles, then the PLAIN / BOOLEAN copies (in the same
   // grid when fused, else their own zero-LDS launch, k_values_copy, on the copy stream)
@@ -2215,6 +2223,7 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     eu = b->err_sel ^ 1u;
     if (!b->err_ready[eu]) {  // the first decode after an upload: the whole per-decode state, once
       HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
+      b->bm_zeroed = true;
       b->ds_synced = false;
     }
     d.chunk_err = (unsigned long long *)(A + (eu ? b->o_err2 : b->o_err));
@@ -2232,7 +2241,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
     b->err_ready[eu ^ 1u] = true;
   } else {
     HIPCHECK(join_deferred(b, s), err);
-    HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->f_begin, b->f_end - b->f_begin, s), err);
+    const uint64_t z0 = b->bm_zeroed ? b->z_bm_end : b->z_begin;  // (the bitmaps: first decode only)
+    HIPCHECK(launch_reset(A + z0, b->z_end - z0, A + b->f_begin, b->f_end - b->f_begin, s), err);
+    b->bm_zeroed = true;
     b->err_ready[1] = true;  // (o_err2 is inside the region)
     b->ds_synced = false;
   }
@@ -2403,7 +2414,9 @@ static int decode_impl(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       b->ds_synced = true;
     }
     // the per-decode state and the level stream's keys: [o_tile_first, o_err_ds end) of the 0xff region
-    HIPCHECK(launch_reset(A + b->z_begin, b->z_end - b->z_begin, A + b->o_tile_first, b->f_end - b->o_tile_first, ds), err);
+    const uint64_t z0 = b->bm_zeroed ? b->z_bm_end : b->z_begin;  // (the bitmaps: first decode only)
+    HIPCHECK(launch_reset(A + z0, b->z_end - z0, A + b->o_tile_first, b->f_end - b->o_tile_first, ds), err);
+    b->bm_zeroed = true;
     // k_levels_seg beside the values launch: at most ~4 level waves per CU resident (each walks two
     // pages or more; cfg2's 2,048 pages: 1,024 waves, step 0.361 -> 0.346 ms; 768 or 1,536: slower)
     LaunchLists lv = l;
