@@ -334,6 +334,37 @@ def test_gpu_back_to_back_decodes(gpu_ctx, nest_mode, bad_page):
     b.close()
 
 
+@pytest.mark.gpu
+def test_gpu_batch_reuse_bitmaps(gpu_ctx, nest_mode):
+    """The validity bitmaps OR-written at shared edge words are zeroed by the first decode after an
+    upload only (host.cpp bm_zeroed). One batch reused for different files (pqgpu_batch_reset, then
+    new chunks and a new upload) must zero them again: every file's nested arrays and validity equal
+    the oracle's on each of two decodes, whatever the previous file left in the arena."""
+    import pqgpu
+    b = pqgpu.Batch(gpu_ctx)
+    for data in (_b2b_file(None), pqtest.load("cfg4_small"), _b2b_file(2), _b2b_file(None)):
+        orc = pqtest.oracle_decode(data)
+        f = pqgpu.File(data)
+        ids = {(rg, col): b.add_file_chunk(f, rg, col)[0] for rg in range(f.num_row_groups) for col in range(f.num_columns)}
+        for _ in range(2):
+            b.decode()
+            e = b.sync()
+            for rg, col, o in orc:
+                if isinstance(o, O.OracleError):
+                    assert e is not None
+                    g = b.status(ids[(rg, col)])
+                    assert g is not None and (g.code, g.page) == (o.code, o.page), (g, o)
+                    continue
+                r = b.result(ids[(rg, col)])
+                pqtest.assert_chunk_equal(r, o, f"reuse rg{rg} col{col}")
+                if r.nested:
+                    lnd, ld, md = _levels_of(data, col)
+                    want_levels, want_elem = nested_ref(o.rep_levels, o.def_levels, md, lnd, ld)
+                    _check_nested(r.nested, r.element_validity, want_levels, want_elem, f"reuse rg{rg} col{col}")
+        b.reset()
+    b.close()
+
+
 TORN_SCRIPT = r"""
 import sys
 sys.path[:0] = sys.argv[1:4]
