@@ -3,13 +3,13 @@
 // reference's []interface{} of []byte values (type_bytearray.go:24-55 PLAIN, type_dict.go:40-60
 // dictionary, :98-240 DELTA_LENGTH / DELTA_BYTE_ARRAY) without one allocation per value.
 //
-// Work unit: the byte-array tile, kBaTile consecutive values of one page (a dictionary page's
-// byte-array tiles are its dictionary tiles). Per decode:
+// Work unit: the byte-array tile, 2,048 consecutive values of one page (class 3: 4,096; a tile lies
+// inside one dictionary tile). Per decode:
 //   k_dict_slots  every byte-array dictionary whose entries are at most 60 bytes is copied
 //                 into 16/32/64-byte slots [u32 length | bytes | zero pad], so ONE aligned
 //                 16-B load gives a value's length and its first 12 bytes (page_dict.go:35-72:
 //                 the dictionary page's materialisation, redone every decode).
-//   k_ba_emit     per tile, single pass. Wave w owns 512 values of the tile in 8 rounds of
+//   k_ba_emit     per tile, single pass. Wave w owns 512 values of the tile (class 3: 256) in rounds of
 //                 64 consecutive values: their lengths (dictionary pages: indices decoded from
 //                 the run table, dict_tile.h; an index outside the dictionary fails the page,
 //                 type_dict.go:52-54; other pages: the lengths their value kernels wrote);
@@ -49,8 +49,16 @@ constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStMask = (1ull <<
 #define PQ_BA_HELP 24
 #endif
 constexpr uint32_t kHelpSpins = PQ_BA_HELP;       // look-back polls of a silent predecessor before computing its sum
-constexpr uint32_t kEmitWaves = 8;                // waves of a k_ba_emit workgroup
-constexpr uint32_t kRounds = kBaTile / (64 * kEmitWaves);  // 64-value rounds per wave
+// Waves of a k_ba_emit workgroup: 4 for classes 0-2 (a 2,048-value tile is 8 rounds of 64 values per
+// wave; with 256 LDS runs a workgroup takes 28 KB, so five are resident per CU and their phases --
+// tile load, gathers, look-back, emission -- overlap: cfg3 0.344 -> 0.336 ms against 4,096-value tiles
+// in 8-wave workgroups); 8 for class 3, whose 16 KB LDS slot table per workgroup would otherwise
+// seat fewer waves (cfg4 k_ba_emit_lds 0.255 ms; 4-wave workgroups 0.407 ms)
+constexpr uint32_t kEmitWaves = 4;
+constexpr uint32_t kEmitWavesLds = 8;
+constexpr uint32_t kRounds = 8;  // 64-value rounds per wave: kBaTile = 64 kRounds kEmitWaves, kBaTileLds likewise
+static_assert(kBaTile == 64 * kRounds * kEmitWaves && kBaTileLds == 64 * kRounds * kEmitWavesLds, "tile = rounds x waves");
+DEV uint32_t ba_tile_vals(const ChunkDesc &cd) { return (cd.flags & CF_BA_TILE4K) ? kBaTileLds : kBaTile; }
 
 DEV uint64_t block_sum64(uint64_t v, uint64_t *wsum) {
   v = wave_sum64(v);
@@ -146,7 +154,7 @@ __global__ void __launch_bounds__(256) k_ba_sums(BatchDev b_in) {
   const ChunkDesc &cd = b.chunks[pd.chunk];
   if (!(cd.flags & (CF_BA_SYNC | CF_BA_PRESUM))) return;  // workgroup-uniform
   const uint32_t nn = b.page_nn_v[p];
-  const uint32_t v0 = (t - pd.ba_tile) * kBaTile, v1 = min(v0 + kBaTile, nn);
+  const uint32_t tv = ba_tile_vals(cd), v0 = (t - pd.ba_tile) * tv, v1 = min(v0 + tv, nn);
   uint64_t sum = 0;
   if (v0 < v1 && !ba_page_failed(b, pd)) {
     if (pd.vkind == VK_DICT) {
@@ -193,14 +201,15 @@ __global__ void __launch_bounds__(256) k_ba_scan(BatchDev b_in, const uint32_t *
 // ---------------------------------------------------------------------------
 // k_ba_emit
 // ---------------------------------------------------------------------------
-template <uint32_t NR>
+template <uint32_t NR, uint32_t EW>
 struct EmitLDST {
+  static constexpr uint32_t kWaves = EW;
   DictTileLDST<NR> tile;
-  uint4 wbuf[kEmitWaves][kWaveVec];
-  uint64_t wtot[kEmitWaves];  // the waves' payload bytes
-  uint64_t base;              // the tile's payload base
+  uint4 wbuf[EW][kWaveVec];
+  uint64_t wtot[EW];  // the waves' payload bytes
+  uint64_t base;      // the tile's payload base
 };
-using EmitLDS = EmitLDST<kTileRuns>;
+using EmitLDS = EmitLDST<kDictRuns, kEmitWaves>;
 // Class 3: the first 16-B piece of every slot (length and the first 12 bytes) of a dictionary of at
 // most kLdsSlots entries in 16- or 32-B slots is copied into LDS per tile, so pass A's lengths and
 // pass B's first pieces are LDS reads instead of random gathers through the texture path (cfg4's
@@ -208,7 +217,7 @@ using EmitLDS = EmitLDST<kTileRuns>;
 // runs per tile in LDS keep three workgroups per CU.
 constexpr uint32_t kLdsSlots = 1024;
 struct EmitLDSSlots {
-  EmitLDST<kDictRuns> e;
+  EmitLDST<kDictRuns, kEmitWavesLds> e;
   uint4 slots[kLdsSlots];
 };
 
@@ -226,7 +235,7 @@ DEV uint64_t tile_aggregate(const BatchDev &b, uint32_t t, const TL &unstaged) {
   const PageDesc &pd = b.pages[p];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t nn = b.page_nn_v[p];
-  const uint32_t v0 = (t - pd.ba_tile) * kBaTile, v1 = min(v0 + kBaTile, nn);
+  const uint32_t tv = ba_tile_vals(cd), v0 = (t - pd.ba_tile) * tv, v1 = min(v0 + tv, nn);
   uint64_t sum = 0;
   if (v0 < v1) {
     if (pd.vkind == VK_DICT) {
@@ -408,7 +417,7 @@ DEV void emit_tile(const BatchDev &b, const PageDesc &pd, const ChunkDesc &cd, u
   // ---- the tile's base: k_ba_scan's (CF_BA_SYNC chunks) or the look-back's (wave 0)
   if (wv == 0) {
     uint64_t agg = 0;
-    for (uint32_t q = 0; q < kEmitWaves; q++) agg += L.wtot[q];
+    for (uint32_t q = 0; q < EL::kWaves; q++) agg += L.wtot[q];
     const uint64_t base = (cd.flags & (CF_BA_SYNC | CF_BA_PRESUM)) ? b.ba_tile_sum[t]
                           : PQ_ABLATE(b, 8) ? 0  // diagnostic: no look-back
                                             : lookback(b, cd, pd.chunk, t, agg, L.tile, st);
@@ -524,7 +533,7 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   const PageDesc &pd = b.pages[p];
   const ChunkDesc &cd = b.chunks[pd.chunk];
   const uint32_t nn = b.page_nn_v[p];
-  const uint32_t v0 = (t - pd.ba_tile) * kBaTile, v1 = min(v0 + kBaTile, nn);
+  const uint32_t tv = ba_tile_vals(cd), v0 = (t - pd.ba_tile) * tv, v1 = min(v0 + tv, nn);
   if (b.page_vbase[p] + v0 == 0 && threadIdx.x == 0 && cd.offsets) gp_u64<int32_t>(cd.offsets)[0] = 0;
   const bool is_dict = pd.vkind == VK_DICT;
   DictTile tl;
@@ -544,8 +553,7 @@ DEV void ba_emit(const BatchDev &b, EL &L, const uint4 *lslots = nullptr) {
   st.flush(40);
 }
 
-// class 0: with the first pieces in registers (PQ_BA_P0) <= 96 VGPRs, which still seats two 8-wave
-// workgroups per CU; without, 6 (three workgroups: <= 80 VGPRs, 46 KB LDS each)
+// class 0: with the first pieces in registers (PQ_BA_P0) <= 96 VGPRs (five 4-wave workgroups per CU)
 #ifndef PQ_BA_WPE
 #define PQ_BA_WPE (PQ_BA_P0 ? 5 : 6)
 #endif
@@ -564,7 +572,7 @@ __global__ void __launch_bounds__(64 * kEmitWaves) k_ba_emit(BatchDev b_in) {
   __shared__ EmitLDS L;
   ba_emit<2>(b, L);
 }
-__global__ void __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(6))) k_ba_emit_lds(BatchDev b_in) {
+__global__ void __launch_bounds__(64 * kEmitWavesLds) __attribute__((amdgpu_waves_per_eu(6))) k_ba_emit_lds(BatchDev b_in) {
   const BatchDev b = global_view(b_in);
   __shared__ EmitLDSSlots L;
   const uint32_t t = tile_of_block(b, 3, blockIdx.x);
@@ -597,7 +605,7 @@ hipError_t launch_ba_emit(const BatchDev &b, const LaunchLists &l, hipStream_t s
   if (l.n_ba_class[0]) hipLaunchKernelGGL(k_ba_emit_slots, dim3(l.n_ba_class[0]), dim3(64 * kEmitWaves), 0, s, b);
   if (l.n_ba_class[1]) hipLaunchKernelGGL(k_ba_emit_slots64, dim3(l.n_ba_class[1]), dim3(64 * kEmitWaves), 0, s, b);
   if (l.n_ba_class[2]) hipLaunchKernelGGL(k_ba_emit, dim3(l.n_ba_class[2]), dim3(64 * kEmitWaves), 0, s, b);
-  if (l.n_ba_class[3]) hipLaunchKernelGGL(k_ba_emit_lds, dim3(l.n_ba_class[3]), dim3(64 * kEmitWaves), 0, s, b);
+  if (l.n_ba_class[3]) hipLaunchKernelGGL(k_ba_emit_lds, dim3(l.n_ba_class[3]), dim3(64 * kEmitWavesLds), 0, s, b);
   return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cassert>
 #include <chrono>
 #include <functional>
 #include <memory>
@@ -252,6 +253,7 @@ struct HostChunk {
   // chunk share_from's (cleared by every decode)
   int32_t share_from = -1;
   int8_t ba_class = -1;  // k_ba_emit class (byte-array chunks)
+  uint32_t ba_tile_vals = kBaTile;  // values per byte-array tile (class 3: kBaTileLds)
   bool ba_presum = false;  // tile bases from k_ba_sums + k_ba_scan instead of the look-back
   uint32_t share_lists = 0, share_groups = 0;
   // byte-array dictionaries: (position, length) of every entry, from the host's walk of the
@@ -1193,6 +1195,22 @@ static int add_chunk_impl(pqgpu_batch *b, const uint8_t *file, int64_t flen, con
 // Upload: arena layout, descriptors, work lists
 // ---------------------------------------------------------------------------
 static hipError_t join_deferred(pqgpu_batch *b, hipStream_t s);
+// k_ba_emit class 3 (bytearray.hip k_ba_emit_lds): dictionary pages only (so no CF_BA_SYNC unless the
+// payload bound passes 2 GiB), 16- / 32-B slots (entries of at most 28 bytes: slot_shift <= 5) of a
+// dictionary of at most 1,024 entries, whose first slot pieces fit in LDS. Decided from the chunk's
+// dictionary before the slot table and the payload bound are (build_and_upload: the tile size
+// depends on it). PQ_BA_LDS_SLOTS=0: never (comparison runs).
+static bool ba_lds_class(const pqgpu_batch *b, const HostChunk &hc) {
+  const char *lsv = getenv("PQ_BA_LDS_SLOTS");
+  if ((lsv && atoi(lsv) == 0) || !hc.has_dict || hc.dict_count == 0 || hc.dict_count > 1024 || hc.dict_max_len > 28)
+    return false;
+  uint64_t bound = 0;
+  for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
+    if (b->pages[p].vkind != VK_DICT) return false;
+    bound += (uint64_t)b->pages[p].num_slots * hc.dict_max_len;
+  }
+  return bound <= 0x7fffffffULL - 64;
+}
 static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (b->ctx) HIPCHECK(join_deferred(b, s), err);  // (the level stream may still read the stage)
   const uint32_t np = (uint32_t)b->pages.size(), nc = (uint32_t)b->chunks.size();
@@ -1296,10 +1314,11 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   b->o_nest_done = take((uint64_t)nc * 4);
   uint64_t n_ba_tiles = 0;  // byte-array tiles (for the look-back state, zeroed per decode)
   for (uint32_t c = 0; c < nc; c++) {
-    const HostChunk &hc = b->chunks[c];
+    HostChunk &hc = b->chunks[c];
     if (hc.err.code || hc.value_width != 0) continue;
+    hc.ba_tile_vals = ba_lds_class(b, hc) ? kBaTileLds : kBaTile;
     for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
-      n_ba_tiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
+      n_ba_tiles += (b->pages[p].num_slots + hc.ba_tile_vals - 1) / hc.ba_tile_vals;
   }
   b->o_ba_state = take(n_ba_tiles * 128);  // one 128-B line per tile (bytearray.hip kStStride)
   uint64_t n_nest_tiles = 0;  // nested tiles (k_nest_tile's look-back state, zeroed per decode)
@@ -1346,7 +1365,7 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) {
         PageDesc &pd = b->pages[p];
         pd.ba_tile = (uint32_t)b->ba_tile_page.size();
-        for (uint32_t k = 0; k < (pd.num_slots + kBaTile - 1) / kBaTile; k++) b->ba_tile_page.push_back(p);
+        for (uint32_t k = 0; k < (pd.num_slots + hc.ba_tile_vals - 1) / hc.ba_tile_vals; k++) b->ba_tile_page.push_back(p);
         switch (pd.vkind) {
           case VK_DICT: bound += (uint64_t)pd.num_slots * hc.dict_max_len; break;
           case VK_PLAIN_BA: bound += pd.val_len; srcs = true; break;
@@ -1517,16 +1536,12 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
   if (!b->ba_tile_page.empty()) {
     std::vector<std::vector<uint32_t>> q(32);
     std::vector<int8_t> cls(nc, -1);
-    const char *lsv = getenv("PQ_BA_LDS_SLOTS");  // 0: no LDS slot class (comparison runs)
-    const bool lds_ok = !lsv || atoi(lsv) != 0;
     for (uint32_t c : b->ba_chunks) {
       const HostChunk &hc = b->chunks[c];
       bool slot_only = hc.slot_shift != 0 && !hc.ba_sync;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++) slot_only &= b->pages[p].vkind == VK_DICT;
-      // class 3: 16- / 32-B slots of a dictionary whose first slot pieces fit in LDS
-      // (bytearray.hip k_ba_emit_lds)
-      const bool lds = lds_ok && slot_only && hc.slot_shift <= 5 && hc.dict_count <= 1024;
-      cls[c] = lds ? 3 : slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
+      cls[c] = ba_lds_class(b, hc) ? 3 : slot_only ? (hc.slot_shift <= 5 ? 0 : 1) : 2;
+      assert((cls[c] == 3) == (hc.ba_tile_vals == kBaTileLds) && (cls[c] != 3 || (slot_only && hc.slot_shift <= 5)));
     }
     for (uint32_t c : b->ba_chunks) {
       HostChunk &hc = b->chunks[c];
@@ -1919,8 +1934,9 @@ static int build_and_upload(pqgpu_batch *b, hipStream_t s, pqgpu_error *err) {
       cd.ba_tile0 = fp ? fp->ba_tile : 0;
       cd.ba_ntiles = 0;
       for (uint32_t p = hc.first_page; p < hc.first_page + hc.num_pages; p++)
-        cd.ba_ntiles += (b->pages[p].num_slots + kBaTile - 1) / kBaTile;
+        cd.ba_ntiles += (b->pages[p].num_slots + hc.ba_tile_vals - 1) / hc.ba_tile_vals;
       if (hc.ba_presum) cd.flags |= CF_BA_PRESUM;
+      if (hc.ba_tile_vals == kBaTileLds) cd.flags |= CF_BA_TILE4K;
       if (hc.ba_sync) {
         cd.flags |= CF_BA_SYNC;
         cd.payload = hc.payload ? (uint64_t)hc.payload : 0;  // (re)sized after the scan of each decode

@@ -75,8 +75,12 @@ constexpr uint32_t kDictGroupHost = 2;     // kernels.hip kDictGroup: tiles per 
 __host__ __device__ constexpr inline bool dict2_eligible(uint32_t vkind, uint32_t value_width, uint64_t dict_count) {
   return vkind == VK_DICT && value_width == 4 && dict_count * 4 <= kDictEarlyHost;
 }
-constexpr uint32_t kBaTile = kDictTile; // values per byte-array tile (page-aligned; a dictionary
-                                        // page's BA tiles are its dictionary tiles)
+// Values per byte-array tile (page-aligned, inside one dictionary tile): kBaTile for emission classes
+// 0-2 (4-wave workgroups), kBaTileLds for class 3 (the LDS slot table; 8-wave workgroups, chunks
+// flagged CF_BA_TILE4K); bytearray.hip kEmitWaves
+constexpr uint32_t kBaTile = 2048;
+constexpr uint32_t kBaTileLds = 4096;
+static_assert(kDictTile % kBaTile == 0 && kDictTile % kBaTileLds == 0, "a byte-array tile lies inside one dictionary tile");
 
 struct LaunchLists {
   const uint32_t *level_pages; uint32_t n_level_pages;   // generic level streams: page << 1 | (0 rep, 1 def)

@@ -83,7 +83,7 @@ struct PageDesc {        // 104 B
   uint16_t pad0;
   uint32_t delta_mbvc;   // DELTA: values per miniblock
   uint32_t ba_delta;     // VK_DLBA / VK_DBA: index of the page's BaDelta entry
-  uint32_t ba_tile;      // byte-array chunks: global index of the page's first BA tile (kBaTile values)
+  uint32_t ba_tile;      // byte-array chunks: global index of the page's first BA tile (ba_tile_vals values)
   uint32_t dict_tile0;   // VK_DICT / VK_RLE_BOOL with a run scan: the page's first entry of the tile tables
 };
 
@@ -140,7 +140,8 @@ static_assert(sizeof(ChunkDesc) == 480, "ChunkDesc layout: host and device share
 enum : int32_t { CF_DICT = 1, CF_BASE_ON_DEVICE = 2, CF_BA_DICT = 4, CF_FAILED = 8,
                  CF_BA_SYNC = 16,    // byte-array payload without an upload-time bound: sized after the scan
                  CF_BA_PRESUM = 32,  // byte-array tile bases from k_ba_sums + k_ba_scan (no look-back)
-                 CF_NN_SPEC = 64 };  // serial batch: non-null counts speculated from PLAIN value bytes (k_bases checks)
+                 CF_NN_SPEC = 64,    // serial batch: non-null counts speculated from PLAIN value bytes (k_bases checks)
+                 CF_BA_TILE4K = 128 };  // byte-array chunk of emission class 3: kBaTileLds-value tiles
 
 // Work items of the values kernel.
 enum : uint8_t { WI_PLAIN = 0, WI_BOOL = 1, WI_DICT = 2, WI_DELTA = 3, WI_PLAIN_BA = 4, WI_DICT_BA_LEN = 5,
